@@ -1,0 +1,211 @@
+#!/usr/bin/env python3
+"""Benchmark: CKKS matvec ciphertexts/sec (N=2^15, L=10) on 1..8 MI355X — BASELINE.json metric.
+
+Workload (BASELINE cfg3): the reference's BatchedMatrix::matmul diag x col (he_linalg.cpp:943-1006)
+with n = 4096 diagonals at N = 2^15, coeff_modulus {60, 40 x 9, 60} (L = 10 data primes + P),
+default Galois key set (29 keys), lazy relinearization + one rescale per output.  One "step" = one
+pass of the hot path over one batch: B input vectors (the p columns of `other`) against the same
+encrypted matrix and keys, producing B output ciphertexts.  Inputs are resident in HBM before the
+timed region.  Multi-GPU: one process per GPU (torch.distributed over RCCL), each rank holds a
+replica of the matrix + keys and processes its own B vectors (weak scaling, no data-path
+collective — SURVEY §8(e) throughput mode).
+
+Data: synthetic — uniformly random RNS residues for ciphertexts and keys, generated on the device
+(RLWE ciphertexts and key-switching keys are pseudo-uniform; every kernel is data-oblivious, so the
+timing equals that of real encryptions; bit-exact parity on real encryptions is in tests/).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "homomorphic-encryption-algorithms-diploma-thesis_amd")
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+S_CT = lambda N, l: 2 * l * N * 8  # noqa: E731
+
+
+def load_hecdna():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("hecdna", os.path.join(PKG, "__init__.py"))
+    mod = importlib.util.module_from_spec(spec)
+    sys.modules["hecdna"] = mod
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def ks_total(N, n):
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from _helpers import ks_count
+    return ks_count(N, n)
+
+
+def algorithmic_bytes_per_matvec(N, l, n, B, ks):
+    """bytes(B) = (n*S_ct + KS*S_key + S_key)/B + KS*2*S_ct + n*S_ct + S_ct3 + S_ct."""
+    K = l + 1
+    s_ct, s_ct3, s_key = 2 * l * N * 8, 3 * l * N * 8, 2 * l * K * N * 8
+    return (n * s_ct + ks * s_key + s_key) / B + ks * 2 * s_ct + n * s_ct + s_ct3 + s_ct
+
+
+def cpu_baseline(N, moduli, n, sample_diags, threads):
+    """The oracle (C++ restatement of the reference's SEAL path, `port`) timed on this host on a bounded
+    sample: diagonals j in [0, sample_diags) of one matvec, extrapolated by key-switch count."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle_py as orc
+    o = orc.Oracle(N, moduli)
+    rng = np.random.default_rng(5)
+    L, K = len(moduli) - 1, len(moduli)
+
+    def rnd_ct():
+        return orc.Ct(np.stack([np.stack([rng.integers(0, moduli[i], N, dtype=np.uint64) for i in range(L)])
+                                for _ in range(2)]), 2.0**40)
+
+    def rnd_key():
+        k = np.empty((L, 2, K, N), dtype=np.uint64)
+        for i in range(K):
+            k[:, :, i] = rng.integers(0, moduli[i], (L, 2, N), dtype=np.uint64)
+        return k
+    elts = o.default_galois_elts()
+    gk = {e: rnd_key() for e in elts}
+    A = [rnd_ct() for _ in range(sample_diags)]
+    X = [rnd_ct()]
+    from _helpers import ks_count
+    ks_sample = ks_count(N, sample_diags)
+    res = {}
+    for th in (1, threads):
+        t0 = time.perf_counter()
+        # finish=False: the sample times rotations + tensors; rk is unused (any key array passes)
+        o.matmul_diag_col(A, X, gk[elts[0]], gk, nthreads=th, j_begin=0, j_end=sample_diags, finish=False)
+        dt = time.perf_counter() - t0
+        res[th] = dt * ks_total(N, n) / ks_sample  # seconds per full matvec
+    return res, ks_sample
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--batch", type=int, default=8, help="input vectors per GPU per step (p)")
+    ap.add_argument("--n", type=int, default=4096, help="matrix dimension (diagonals)")
+    ap.add_argument("--logn", type=int, default=15)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample-diags", type=int, default=48)
+    ap.add_argument("--no-profile", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    hec = load_hecdna()
+    N = 1 << args.logn
+    bits = [60] + [40] * 9 + [60]
+    moduli = hec.create_coeff_modulus(N, bits)
+    L = len(moduli) - 1
+    ctx = hec.Context(N, moduli, device=local)
+    elts = ctx.default_galois_elts()
+    rk = ctx.relin_key(seed=11 + rank)
+    gk = ctx.galois_keys(uniform_elts=elts, seed=1000 + 97 * rank)
+    scale = 2.0**40
+    diags = [ctx.ciphertext().fill_uniform(2, L, scale, 10_000 + j) for j in range(args.n)]
+    cols = [ctx.ciphertext().fill_uniform(2, L, scale, 90_000 + 100 * rank + i) for i in range(args.batch)]
+    outs = [hec.Ciphertext(ctx) for _ in range(args.batch)]
+    ctx.synchronize()
+
+    def barrier():
+        if dist is not None:
+            import torch
+            torch.cuda.synchronize(local)
+            dist.barrier()
+
+    def step():
+        ctx.matmul_diag_col(diags, cols, rk, gk, out=outs)
+
+    for _ in range(args.warmup):
+        step()
+    ctx.synchronize()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    ctx.synchronize()
+    barrier()
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+        t = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+
+    ms_per_step = dt / args.steps * 1e3
+    total = args.batch * world * args.steps
+    value = total / dt
+    ks = ks_total(N, args.n)
+
+    # per-phase breakdown: one extra (untimed) profiled step with HIP events on the context stream
+    breakdown = {}
+    if not args.no_profile:
+        ctx.profile(True)
+        step()
+        ctx.synchronize()
+        for cls in ("ks_intt", "ks_modup", "ks_mac", "ks_moddown", "galois", "tensor", "relin", "rescale"):
+            ms, cnt = ctx.profile_read(cls)
+            breakdown[cls] = {"ms": round(ms, 3), "launch_groups": cnt}
+        ctx.profile(False)
+
+    # roofline for the dominant kernel group: key-switch mod-up NTT (2 passes); algorithmic bytes per
+    # group = l*l limb-NTTs x 2*N*8 B (SURVEY §8(d) cfg2 unit) x batch
+    roof = None
+    if breakdown.get("ks_modup", {}).get("launch_groups"):
+        bm = breakdown["ks_modup"]
+        per = bm["ms"] / bm["launch_groups"]
+        algo = L * L * 2 * N * 8 * args.batch
+        ach = algo / (per * 1e-3) / 1e9
+        roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "kernel": "ks_modup (k_ntt pass A+B)",
+                "avg_ms": round(per, 4), "algorithmic_bytes_per_launch": algo}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        threads = min(16, os.cpu_count() or 1)
+        res, ks_s = cpu_baseline(N, moduli, args.n, args.cpu_sample_diags, threads)
+        cpu = {"value": round(1.0 / res[1], 6), "unit": "matvec/s", "cores": 1, "kind": "port",
+               "sample": f"oracle (C++ SEAL-semantics port) diagonals j<{args.cpu_sample_diags} of one "
+                         f"N=2^{args.logn} L={L} matvec ({ks_s} key switches), extrapolated to the "
+                         f"{ks} key switches of the n={args.n} matvec",
+               "all_cores": {"value": round(1.0 / res[threads], 6), "cores": threads}}
+
+    algo_mv = algorithmic_bytes_per_matvec(N, L, args.n, args.batch, ks)
+    if rank == 0:
+        line = {
+            "metric": "CKKS matvec ciphertexts/sec (N=2^15, L=10)",
+            "value": round(value, 6), "unit": "matvec/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u64", "data": "synthetic",
+            "config": {"workload": f"he_linalg BatchedMatrix::matmul diag x col, {args.n}x{args.n} ct x ct "
+                                   f"matvec, N=2^{args.logn}, L={L}, default Galois keys",
+                       "batch_per_gpu": args.batch, "n": args.n, "key_switches_per_matvec": ks,
+                       "parallelism": f"replicated matrix+keys, dp{world} over input vectors"},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+            "whole_step_algorithmic_GBps": round(algo_mv * total / dt / 1e9, 2),
+            "breakdown_ms_one_step": breakdown,
+        }
+        print(json.dumps(line))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,446 @@
+"""hecdna — MI355X-native CKKS homomorphic linear-algebra engine (Python plumbing).
+
+The product is the C-ABI in ``include/hecdna.h`` implemented by ``libhecdna.so`` (HIP kernels for
+gfx950, built in-tree by ``make`` in this directory).  This module is a thin ctypes binding of that
+C-ABI used by the tests, ``bench.py`` and ``__graft_entry__.py``; it mirrors the reference's
+operator surface (``he::operators`` / ``he::linalg``, see cpp/ for the C++ façade) but adds no
+computation of its own.  Loading fails loudly when the shared library is missing: there is no CPU
+fallback.
+
+Data layout (SEAL layout): ciphertext u64[size][level][N] (NTT form), key u64[L][2][K][N].
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libhecdna.so")
+HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "hecdna.h")
+
+_lib = None
+u64p = C.POINTER(C.c_uint64)
+
+
+class HecError(Exception):
+    """Mirrors SEAL's exception classes: code 1 = invalid_argument, 2 = logic_error, 3 = device."""
+
+    def __init__(self, code, msg):
+        super().__init__(msg)
+        self.code = code
+
+
+class InvalidArgument(HecError, ValueError):
+    pass
+
+
+class LogicError(HecError, RuntimeError):
+    pass
+
+
+def build(jobs: int = 8):
+    subprocess.check_call(["make", "-s", "-C", _HERE, f"-j{jobs}"])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} is missing: build the HIP engine first (make -C {_HERE})")
+        L = C.CDLL(LIB_PATH)
+        L.hec_last_error.restype = C.c_char_p
+        vp = C.c_void_p
+        sig = {
+            "hec_context_create": [C.c_uint64, u64p, C.c_uint64, C.c_int, C.POINTER(vp)],
+            "hec_context_destroy": [vp],
+            "hec_context_set_stream": [vp, vp],
+            "hec_context_synchronize": [vp],
+            "hec_ciphertext_create": [vp, C.POINTER(vp)],
+            "hec_ciphertext_destroy": [vp],
+            "hec_ciphertext_upload": [vp, u64p, C.c_uint64, C.c_uint64, C.c_double],
+            "hec_ciphertext_download": [vp, u64p],
+            "hec_ciphertext_info": [vp, u64p, u64p, C.POINTER(C.c_double)],
+            "hec_ciphertext_copy": [vp, vp],
+            "hec_ciphertext_export_device": [vp, vp],
+            "hec_ciphertext_import_device": [vp, vp, C.c_uint64, C.c_uint64, C.c_double],
+            "hec_ciphertext_reduce": [vp, vp],
+            "hec_ciphertext_fill_uniform": [vp, C.c_uint64, C.c_uint64, C.c_double, C.c_uint64],
+            "hec_plaintext_create": [vp, C.POINTER(vp)],
+            "hec_plaintext_destroy": [vp],
+            "hec_plaintext_upload": [vp, u64p, C.c_uint64, C.c_double],
+            "hec_kswitch_key_upload": [vp, u64p, C.POINTER(vp)],
+            "hec_kswitch_key_fill_uniform": [vp, C.c_uint64, C.POINTER(vp)],
+            "hec_kswitch_key_destroy": [vp],
+            "hec_galois_keys_create": [vp, C.POINTER(vp)],
+            "hec_galois_keys_add": [vp, C.c_uint32, u64p],
+            "hec_galois_keys_add_uniform": [vp, C.c_uint32, C.c_uint64],
+            "hec_galois_keys_destroy": [vp],
+            "hec_negate_inplace": [vp, vp],
+            "hec_add_inplace": [vp, vp, vp],
+            "hec_sub_inplace": [vp, vp, vp],
+            "hec_add_plain_inplace": [vp, vp, vp],
+            "hec_sub_plain_inplace": [vp, vp, vp],
+            "hec_multiply_inplace": [vp, vp, vp],
+            "hec_multiply_plain_inplace": [vp, vp, vp],
+            "hec_square_inplace": [vp, vp],
+            "hec_relinearize_inplace": [vp, vp, vp],
+            "hec_rescale_to_next_inplace": [vp, vp],
+            "hec_mod_switch_to_next_inplace": [vp, vp],
+            "hec_rotate_vector_inplace": [vp, vp, C.c_int, vp],
+            "hec_apply_galois_inplace": [vp, vp, C.c_uint32, vp],
+            "hec_matmul_diag_col": [vp, vp, C.c_uint64, vp, C.c_uint64, vp, vp, vp],
+            "hec_matmul_diag_col_partial": [vp, vp, C.c_uint64, C.c_uint64, C.c_uint64, vp, C.c_uint64, vp, vp],
+            "hec_matmul_finish": [vp, vp, C.c_uint64, vp, vp],
+            "hec_matmul_col_colT": [vp, vp, C.c_uint64, vp, C.c_uint64, vp, vp, vp],
+            "hec_matrix_matmul": [vp, vp, C.c_uint64, C.c_uint64, C.c_int, vp, C.c_uint64, C.c_uint64, C.c_int,
+                                  vp, vp],
+            "hec_ntt_forward": [vp, vp, C.c_uint64, C.c_uint64, C.c_uint64],
+            "hec_ntt_inverse": [vp, vp, C.c_uint64, C.c_uint64, C.c_uint64],
+            "hec_dyadic_multiply": [vp, vp, vp, vp, C.c_uint64, C.c_uint64, C.c_uint64],
+            "hec_device_alloc": [vp, C.c_uint64, C.POINTER(vp)],
+            "hec_device_free": [vp, vp],
+            "hec_memcpy_h2d": [vp, vp, vp, C.c_uint64],
+            "hec_memcpy_d2h": [vp, vp, vp, C.c_uint64],
+            "hec_time_ntt_forward": [vp, vp, C.c_uint64, C.c_uint64, C.c_int, C.POINTER(C.c_double)],
+            "hec_profile_enable": [vp, C.c_int],
+            "hec_profile_read": [vp, C.c_char_p, C.POINTER(C.c_double), u64p],
+            "hec_create_coeff_modulus": [C.c_uint64, C.POINTER(C.c_int), C.c_uint64, u64p],
+        }
+        for name, args in sig.items():
+            fn = getattr(L, name)
+            fn.argtypes = args
+            fn.restype = C.c_int
+        L.hec_galois_elt_from_step.argtypes = [vp, C.c_int]
+        L.hec_galois_elt_from_step.restype = C.c_uint32
+        L.hec_default_galois_elts.argtypes = [vp, C.POINTER(C.c_uint32)]
+        L.hec_default_galois_elts.restype = C.c_uint64
+        L.hec_galois_keys_has.argtypes = [vp, C.c_uint32]
+        L.hec_galois_keys_has.restype = C.c_int
+        _lib = L
+    return _lib
+
+
+def _check(rc):
+    if rc != 0:
+        msg = lib().hec_last_error().decode()
+        if rc == 1:
+            raise InvalidArgument(rc, msg)
+        if rc == 2:
+            raise LogicError(rc, msg)
+        raise HecError(rc, msg)
+
+
+def _p(a: np.ndarray):
+    assert a.dtype == np.uint64 and a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data_as(u64p)
+
+
+def exported_symbols():
+    """Names declared in include/hecdna.h (for the C-ABI export test)."""
+    import re
+    txt = open(HEADER_PATH).read()
+    return sorted(set(re.findall(r"\b(hec_[a-z0-9_]+)\s*\(", txt)))
+
+
+def create_coeff_modulus(N, bits):
+    out = np.zeros(len(bits), dtype=np.uint64)
+    _check(lib().hec_create_coeff_modulus(N, (C.c_int * len(bits))(*bits), len(bits), _p(out)))
+    return [int(x) for x in out]
+
+
+class Context:
+    """seal::SEALContext + seal::Evaluator on one GPU (one per process/device)."""
+
+    def __init__(self, N, coeff_modulus, device=0):
+        self.N = int(N)
+        self.moduli = [int(x) for x in coeff_modulus]
+        self.K = len(self.moduli)
+        self.L = self.K - 1
+        m = np.array(self.moduli, dtype=np.uint64)
+        h = C.c_void_p()
+        _check(lib().hec_context_create(self.N, _p(m), self.K, int(device), C.byref(h)))
+        self.h = h
+
+    def close(self):
+        if self.h:
+            lib().hec_context_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_stream(self, stream_ptr):
+        _check(lib().hec_context_set_stream(self.h, C.c_void_p(stream_ptr) if stream_ptr else None))
+
+    def synchronize(self):
+        _check(lib().hec_context_synchronize(self.h))
+
+    def elt_from_step(self, step):
+        e = lib().hec_galois_elt_from_step(self.h, int(step))
+        if e == 0:
+            _check(1)
+        return int(e)
+
+    def default_galois_elts(self):
+        n = lib().hec_default_galois_elts(self.h, None)
+        out = (C.c_uint32 * n)()
+        lib().hec_default_galois_elts(self.h, out)
+        return list(out)
+
+    # -------------------------------------------------------------- objects
+    def ciphertext(self, data=None, scale=1.0):
+        ct = Ciphertext(self)
+        if data is not None:
+            ct.upload(data, scale)
+        return ct
+
+    def plaintext(self, data, scale):
+        return Plaintext(self, data, scale)
+
+    def relin_key(self, data=None, seed=None):
+        return KSwitchKey(self, data, seed)
+
+    def galois_keys(self, keys: dict | None = None, uniform_elts=None, seed=0):
+        g = GaloisKeys(self)
+        for e, d in (keys or {}).items():
+            g.add(e, d)
+        for i, e in enumerate(uniform_elts or []):
+            g.add_uniform(e, seed + 7919 * i)
+        return g
+
+    # -------------------------------------------------------------- evaluator (in place)
+    def negate(self, a):
+        _check(lib().hec_negate_inplace(self.h, a.h)); return a
+
+    def add(self, a, b):
+        _check(lib().hec_add_inplace(self.h, a.h, b.h)); return a
+
+    def sub(self, a, b):
+        _check(lib().hec_sub_inplace(self.h, a.h, b.h)); return a
+
+    def add_plain(self, a, p):
+        _check(lib().hec_add_plain_inplace(self.h, a.h, p.h)); return a
+
+    def sub_plain(self, a, p):
+        _check(lib().hec_sub_plain_inplace(self.h, a.h, p.h)); return a
+
+    def multiply(self, a, b):
+        _check(lib().hec_multiply_inplace(self.h, a.h, b.h)); return a
+
+    def multiply_plain(self, a, p):
+        _check(lib().hec_multiply_plain_inplace(self.h, a.h, p.h)); return a
+
+    def square(self, a):
+        _check(lib().hec_square_inplace(self.h, a.h)); return a
+
+    def relinearize(self, a, rk):
+        _check(lib().hec_relinearize_inplace(self.h, a.h, rk.h)); return a
+
+    def rescale_to_next(self, a):
+        _check(lib().hec_rescale_to_next_inplace(self.h, a.h)); return a
+
+    def mod_switch_to_next(self, a):
+        _check(lib().hec_mod_switch_to_next_inplace(self.h, a.h)); return a
+
+    def rotate_vector(self, a, steps, gk):
+        _check(lib().hec_rotate_vector_inplace(self.h, a.h, int(steps), gk.h)); return a
+
+    def apply_galois(self, a, elt, gk):
+        _check(lib().hec_apply_galois_inplace(self.h, a.h, int(elt), gk.h)); return a
+
+    # -------------------------------------------------------------- linalg
+    @staticmethod
+    def _arr(cts):
+        return (C.c_void_p * len(cts))(*[c.h for c in cts])
+
+    def matmul_diag_col(self, diags, cols, rk, gk, out=None):
+        out = out or [Ciphertext(self) for _ in cols]
+        _check(lib().hec_matmul_diag_col(self.h, self._arr(diags), len(diags), self._arr(cols), len(cols), rk.h,
+                                         gk.h, self._arr(out)))
+        return out
+
+    def matmul_diag_col_partial(self, diags, j_begin, j_end, cols, gk, out=None):
+        out = out or [Ciphertext(self) for _ in cols]
+        _check(lib().hec_matmul_diag_col_partial(self.h, self._arr(diags), len(diags), j_begin, j_end,
+                                                 self._arr(cols), len(cols), gk.h, self._arr(out)))
+        return out
+
+    def matmul_finish(self, accs, rk, out=None):
+        out = out or [Ciphertext(self) for _ in accs]
+        _check(lib().hec_matmul_finish(self.h, self._arr(accs), len(accs), rk.h, self._arr(out)))
+        return out
+
+    def matmul_col_colT(self, A, B, p, rk, gk):
+        out = [Ciphertext(self) for _ in range(p)]
+        _check(lib().hec_matmul_col_colT(self.h, self._arr(A), len(A), self._arr(B), p, rk.h, gk.h,
+                                         self._arr(out)))
+        return out
+
+    def matrix_matmul(self, A, ar, ac, atr, B, br, bc, btr, rk):
+        r1 = ac if atr else ar
+        c2 = br if btr else bc
+        out = [Ciphertext(self) for _ in range(r1 * c2)]
+        _check(lib().hec_matrix_matmul(self.h, self._arr(A), ar, ac, int(atr), self._arr(B), br, bc, int(btr),
+                                       rk.h, self._arr(out)))
+        return out
+
+    # -------------------------------------------------------------- primitives
+    def ntt(self, host: np.ndarray, limb0=0, inverse=False):
+        """host u64[npolys][nlimbs][N] -> transformed copy (device round trip)."""
+        a = np.ascontiguousarray(host, dtype=np.uint64)
+        npolys, nl = (a.shape[0], a.shape[1]) if a.ndim == 3 else (1, a.shape[0])
+        buf = DeviceBuffer(self, a.nbytes)
+        buf.upload(a)
+        fn = lib().hec_ntt_inverse if inverse else lib().hec_ntt_forward
+        _check(fn(self.h, buf.p, limb0, nl, npolys))
+        return buf.download(a.shape)
+
+    def profile(self, on=True):
+        _check(lib().hec_profile_enable(self.h, int(on)))
+
+    def profile_read(self, cls):
+        ms = C.c_double()
+        n = C.c_uint64()
+        _check(lib().hec_profile_read(self.h, cls.encode(), C.byref(ms), C.byref(n)))
+        return ms.value, n.value
+
+
+class DeviceBuffer:
+    def __init__(self, ctx: Context, nbytes):
+        self.ctx = ctx
+        self.nbytes = int(nbytes)
+        p = C.c_void_p()
+        _check(lib().hec_device_alloc(ctx.h, self.nbytes, C.byref(p)))
+        self.p = p
+
+    def upload(self, a):
+        a = np.ascontiguousarray(a)
+        _check(lib().hec_memcpy_h2d(self.ctx.h, self.p, a.ctypes.data_as(C.c_void_p), a.nbytes))
+
+    def download(self, shape, dtype=np.uint64):
+        out = np.empty(shape, dtype=dtype)
+        _check(lib().hec_memcpy_d2h(self.ctx.h, out.ctypes.data_as(C.c_void_p), self.p, out.nbytes))
+        return out
+
+    def __del__(self):
+        try:
+            if self.p:
+                lib().hec_device_free(self.ctx.h, self.p)
+                self.p = None
+        except Exception:
+            pass
+
+
+class Ciphertext:
+    def __init__(self, ctx: Context):
+        self.ctx = ctx
+        h = C.c_void_p()
+        _check(lib().hec_ciphertext_create(ctx.h, C.byref(h)))
+        self.h = h
+
+    def __del__(self):
+        try:
+            if self.h:
+                lib().hec_ciphertext_destroy(self.h)
+                self.h = None
+        except Exception:
+            pass
+
+    def upload(self, data: np.ndarray, scale: float):
+        a = np.ascontiguousarray(data, dtype=np.uint64)
+        _check(lib().hec_ciphertext_upload(self.h, _p(a), a.shape[0], a.shape[1], float(scale)))
+        return self
+
+    def fill_uniform(self, size, level, scale, seed):
+        _check(lib().hec_ciphertext_fill_uniform(self.h, size, level, float(scale), seed))
+        return self
+
+    def info(self):
+        s, l, sc = C.c_uint64(), C.c_uint64(), C.c_double()
+        _check(lib().hec_ciphertext_info(self.h, C.byref(s), C.byref(l), C.byref(sc)))
+        return s.value, l.value, sc.value
+
+    @property
+    def scale(self):
+        return self.info()[2]
+
+    def download(self):
+        s, l, _ = self.info()
+        out = np.empty((s, l, self.ctx.N), dtype=np.uint64)
+        _check(lib().hec_ciphertext_download(self.h, _p(out)))
+        return out
+
+    def copy(self):
+        c = Ciphertext(self.ctx)
+        _check(lib().hec_ciphertext_copy(c.h, self.h))
+        return c
+
+
+class Plaintext:
+    def __init__(self, ctx: Context, data, scale):
+        self.ctx = ctx
+        h = C.c_void_p()
+        _check(lib().hec_plaintext_create(ctx.h, C.byref(h)))
+        self.h = h
+        a = np.ascontiguousarray(data, dtype=np.uint64)
+        _check(lib().hec_plaintext_upload(self.h, _p(a), a.shape[0], float(scale)))
+
+    def __del__(self):
+        try:
+            if self.h:
+                lib().hec_plaintext_destroy(self.h)
+                self.h = None
+        except Exception:
+            pass
+
+
+class KSwitchKey:
+    def __init__(self, ctx: Context, data=None, seed=None):
+        self.ctx = ctx
+        h = C.c_void_p()
+        if data is not None:
+            a = np.ascontiguousarray(data, dtype=np.uint64)
+            _check(lib().hec_kswitch_key_upload(ctx.h, _p(a), C.byref(h)))
+        else:
+            _check(lib().hec_kswitch_key_fill_uniform(ctx.h, int(seed or 0), C.byref(h)))
+        self.h = h
+
+    def __del__(self):
+        try:
+            if self.h:
+                lib().hec_kswitch_key_destroy(self.h)
+                self.h = None
+        except Exception:
+            pass
+
+
+class GaloisKeys:
+    def __init__(self, ctx: Context):
+        self.ctx = ctx
+        h = C.c_void_p()
+        _check(lib().hec_galois_keys_create(ctx.h, C.byref(h)))
+        self.h = h
+
+    def add(self, elt, data):
+        a = np.ascontiguousarray(data, dtype=np.uint64)
+        _check(lib().hec_galois_keys_add(self.h, int(elt), _p(a)))
+
+    def add_uniform(self, elt, seed):
+        _check(lib().hec_galois_keys_add_uniform(self.h, int(elt), int(seed)))
+
+    def has(self, elt):
+        return bool(lib().hec_galois_keys_has(self.h, int(elt)))
+
+    def __del__(self):
+        try:
+            if self.h:
+                lib().hec_galois_keys_destroy(self.h)
+                self.h = None
+        except Exception:
+            pass

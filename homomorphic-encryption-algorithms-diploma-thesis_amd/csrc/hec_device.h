@@ -1,0 +1,82 @@
+// Device-side modular arithmetic for the CKKS engine (gfx950).
+//
+// All residues are u64 < q < 2^61.  CDNA4 has no 64x64->128 multiply: __umul64hi lowers to
+// v_mul_hi_u32 / v_mad_u64_u32 sequences, so the hot paths use Shoup multiplication (one mulhi +
+// two low multiplies per product) with precomputed quotients, and Barrett only where both operands
+// vary (ciphertext tensor products, key-switch accumulators).  Every routine here returns the
+// canonical residue when its name does not say "lazy", so results are bit-identical to SEAL's
+// canonical outputs regardless of the lazy-reduction schedule inside a kernel.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+typedef uint64_t u64;
+typedef uint32_t u32;
+
+#define HEC_MAXL 32  // max RNS limbs handled by per-limb constant tables passed by value
+
+struct DevPrime {
+    u64 q;
+    u64 r0, r1;         // floor(2^128 / q) = r1:r0 (SEAL Modulus::const_ratio)
+    u64 ninv, ninv_q;   // N^-1 mod q and its Shoup quotient
+};
+
+__device__ __forceinline__ u64 mulhi64(u64 a, u64 b) { return __umul64hi(a, b); }
+
+// x * w mod q in [0, 2q) for any x < 2^64, w < q, wq = floor(w * 2^64 / q)
+__device__ __forceinline__ u64 shoup_lazy(u64 x, u64 w, u64 wq, u64 q) { return x * w - mulhi64(x, wq) * q; }
+__device__ __forceinline__ u64 csub(u64 x, u64 q) { return x >= q ? x - q : x; }
+__device__ __forceinline__ u64 shoup(u64 x, u64 w, u64 wq, u64 q) { return csub(shoup_lazy(x, w, wq, q), q); }
+
+// SEAL util::barrett_reduce_64: any 64-bit x -> x mod q
+__device__ __forceinline__ u64 barrett64(u64 x, u64 q, u64 r1) { return csub(x - mulhi64(x, r1) * q, q); }
+
+// SEAL util::barrett_reduce_128: 128-bit (hi:lo) -> mod q
+__device__ __forceinline__ u64 barrett128(u64 lo, u64 hi, u64 q, u64 r0, u64 r1)
+{
+    u64 carry = mulhi64(lo, r0);
+    u64 t_lo = lo * r1, t_hi = mulhi64(lo, r1);
+    u64 tmp1 = t_lo + carry;
+    u64 tmp3 = t_hi + (tmp1 < carry);
+    u64 u_lo = hi * r0, u_hi = mulhi64(hi, r0);
+    u64 sum = tmp1 + u_lo;
+    carry = u_hi + (sum < tmp1);
+    u64 est = hi * r1 + tmp3 + carry;
+    return csub(lo - est * q, q);
+}
+__device__ __forceinline__ u64 mulmod(u64 a, u64 b, const DevPrime &p)
+{
+    return barrett128(a * b, mulhi64(a, b), p.q, p.r0, p.r1);
+}
+__device__ __forceinline__ u64 addmod(u64 a, u64 b, u64 q) { return csub(a + b, q); }
+__device__ __forceinline__ u64 submod(u64 a, u64 b, u64 q) { return a >= b ? a - b : a + q - b; }
+
+// 128-bit accumulator
+struct U128 {
+    u64 lo, hi;
+};
+__device__ __forceinline__ void mac128(U128 &acc, u64 a, u64 b)
+{
+    const u64 plo = a * b, phi = mulhi64(a, b);
+    acc.lo += plo;
+    acc.hi += phi + (acc.lo < plo);
+}
+
+// Cooley-Tukey (Harvey) forward butterfly, inputs/outputs in [0, 4q)
+__device__ __forceinline__ void ct_bfly(u64 &X, u64 &Y, u64 w, u64 wq, u64 q, u64 two_q)
+{
+    u64 x = X >= two_q ? X - two_q : X;
+    const u64 t = shoup_lazy(Y, w, wq, q);
+    X = x + t;
+    Y = x - t + two_q;
+}
+// Gentleman-Sande inverse butterfly, inputs/outputs in [0, 2q); w = inverse twiddle
+__device__ __forceinline__ void gs_bfly(u64 &X, u64 &Y, u64 w, u64 wq, u64 q, u64 two_q)
+{
+    const u64 s = X + Y;
+    const u64 d = X - Y + two_q;
+    X = s >= two_q ? s - two_q : s;
+    Y = shoup_lazy(d, w, wq, q);
+}
+
+__device__ __forceinline__ u32 bitrev(u32 x, int bits) { return __brev(x) >> (32 - bits); }

@@ -1,0 +1,1320 @@
+// Host orchestration + C-ABI of the CKKS engine (include/hecdna.h).
+//
+// Every public entry point restates one seal::Evaluator call that the reference's he_operators /
+// he_linalg layer makes (file:line cited per function in hecdna.h), on device-resident SEAL-layout
+// objects.  Internally all ciphertext work is BATCHED: the key switch, rotation and rescale
+// routines take B ciphertexts in one strided array so that one launch sequence (and one read of
+// the key) serves the whole batch; the single-object C-ABI calls are the B = 1 case.
+//
+// Key switch dataflow (SEAL 4.1 Evaluator::switch_key_inplace, per-prime digits + special prime P,
+// SURVEY §8(a) a5), B targets T[b] (NTT form, l limbs):
+//   (1) D[b][J]    = INTT_J(T[b][J])                                    ntt_strided (inverse)
+//   (2) E[b][I][J] = NTT_I(D[b][J] mod q_I),  I in {0..l-1, P}, I != J   ks_modup (reduction fused)
+//   (3) ACC[b][k][I] = sum_J E[b][I][J] * key[J][k][I]   (E[b][I][I] = T[b][I])   ks_mac
+//   (4) y = INTT_P(ACC[b][k][P])                                        ntt_strided (inverse)
+//   (5) OUT[b][k][i] = IN[b][k][i] + (ACC[b][k][i] - NTT_i(round(y))) * P^-1     divide_round
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <limits>
+
+#include "hec_internal.h"
+#include "hecdna.h"
+
+using namespace hec;
+using u128 = unsigned __int128;
+
+// =============================================================================== objects ===
+struct hec_context {
+    Ctx c;
+};
+struct hec_ciphertext {
+    hec_context *ctx = nullptr;
+    u64 *d = nullptr;
+    std::size_t cap = 0;  // words
+    std::size_t size = 0, level = 0;
+    double scale = 1.0;
+};
+struct hec_plaintext {
+    hec_context *ctx = nullptr;
+    u64 *d = nullptr;
+    std::size_t cap = 0;
+    std::size_t level = 0;
+    double scale = 1.0;
+};
+struct hec_kswitch_key {
+    hec_context *ctx = nullptr;
+    u64 *d = nullptr;
+};
+struct hec_galois_keys {
+    hec_context *ctx = nullptr;
+    std::map<u32, u64 *> keys;
+};
+
+namespace {
+
+thread_local std::string g_err;
+
+template <class F>
+int guard(F &&f)
+{
+    try {
+        f();
+        return HEC_OK;
+    } catch (const HipError &e) {
+        g_err = e.what();
+        return HEC_EDEVICE;
+    } catch (const std::invalid_argument &e) {
+        g_err = e.what();
+        return HEC_EINVAL;
+    } catch (const std::logic_error &e) {
+        g_err = e.what();
+        return HEC_ELOGIC;
+    } catch (const std::exception &e) {
+        g_err = e.what();
+        return HEC_EDEVICE;
+    }
+}
+
+void need(bool cond, const char *msg)
+{
+    if (!cond) throw std::invalid_argument(msg);
+}
+
+// ------------------------------------------------------------------ host number theory -----
+u64 powm(u64 b, u64 e, u64 q)
+{
+    u64 r = 1 % q;
+    b %= q;
+    for (; e; e >>= 1) {
+        if (e & 1) r = (u64)((u128)r * b % q);
+        b = (u64)((u128)b * b % q);
+    }
+    return r;
+}
+u64 invm(u64 a, u64 q)
+{
+    __int128 t = 0, nt = 1, r = q, nr = a % q;
+    while (nr) {
+        const __int128 k = r / nr;
+        __int128 x = t - k * nt; t = nt; nt = x;
+        x = r - k * nr; r = nr; nr = x;
+    }
+    if (r != 1) throw std::invalid_argument("value is not invertible");
+    return (u64)(t < 0 ? t + q : t);
+}
+bool isprime(u64 n)
+{
+    if (n < 2) return false;
+    static const u64 sp[] = {2, 3, 5, 7, 11, 13, 17, 19, 23, 29, 31, 37};
+    for (u64 p : sp) {
+        if (n % p == 0) return n == p;
+    }
+    u64 d = n - 1;
+    int s = 0;
+    while (!(d & 1)) { d >>= 1; ++s; }
+    for (u64 a : sp) {
+        u64 x = powm(a, d, n);
+        if (x == 1 || x == n - 1) continue;
+        bool composite = true;
+        for (int i = 1; i < s && composite; ++i) {
+            x = (u64)((u128)x * x % n);
+            if (x == n - 1) composite = false;
+        }
+        if (composite) return false;
+    }
+    return true;
+}
+u64 shoupq(u64 w, u64 q) { return (u64)(((u128)w << 64) / q); }
+u32 brev(u32 x, int bits)
+{
+    u32 r = 0;
+    for (int i = 0; i < bits; ++i) r |= ((x >> i) & 1u) << (bits - 1 - i);
+    return r;
+}
+// SEAL util::try_minimal_primitive_root: the smallest primitive 2N-th root of unity mod q
+u64 minimal_root(u64 two_n, u64 q)
+{
+    u64 g = 0;
+    for (u64 x = 2; x < q && !g; ++x) {
+        const u64 c = powm(x, (q - 1) / two_n, q);
+        if (powm(c, two_n / 2, q) == q - 1) g = c;
+    }
+    if (!g) throw std::logic_error("no primitive root found");
+    const u64 g2 = (u64)((u128)g * g % q);
+    u64 cur = g, best = g;
+    for (u64 k = 0; k < two_n / 2; ++k) {
+        best = std::min(best, cur);
+        cur = (u64)((u128)cur * g2 % q);
+    }
+    return best;
+}
+bool are_close(double a, double b)  // SEAL util::are_close
+{
+    const double sf = std::max({std::fabs(a), std::fabs(b), 1.0});
+    return std::fabs(a - b) < std::numeric_limits<double>::epsilon() * sf;
+}
+bool scale_ok(const Ctx &c, double scale, std::size_t level)  // SEAL is_scale_within_bounds
+{
+    return !(scale <= 0 || (int)std::log2(scale) >= c.total_bits(level));
+}
+std::vector<int> naf(int value)  // SEAL util::naf: least-significant term first
+{
+    std::vector<int> res;
+    const bool sign = value < 0;
+    value = std::abs(value);
+    for (int i = 0; value; ++i) {
+        const int zi = (value & 1) ? 2 - (value & 3) : 0;
+        value = (value - zi) >> 1;
+        if (zi) res.push_back((sign ? -zi : zi) * (1 << i));
+    }
+    return res;
+}
+u32 elt_from_step(const Ctx &c, int step)  // SEAL GaloisTool::get_elt_from_step
+{
+    const u32 n = (u32)c.N, m = 2 * n;
+    if (step == 0) return m - 1;
+    const bool sign = step < 0;
+    u32 pos = (u32)std::abs(step);
+    if (pos >= (n >> 1)) throw std::invalid_argument("step count too large");
+    pos &= m - 1;
+    int s = sign ? (int)(n >> 1) - (int)pos : (int)pos;
+    u64 elt = 1;
+    while (s--) { elt *= 3; elt &= m - 1; }
+    return (u32)elt;
+}
+// SEAL Evaluator::rotate_internal flattened into the sequence of Galois elements it applies
+void rotation_elts(const Ctx &c, int steps, const hec_galois_keys &gk, std::vector<u32> &out)
+{
+    if (steps == 0) return;
+    const u32 elt = elt_from_step(c, steps);
+    if (gk.keys.count(elt)) { out.push_back(elt); return; }
+    const std::vector<int> terms = naf(steps);
+    if (terms.size() == 1) throw std::invalid_argument("Galois key not present");
+    for (int s : terms)
+        if ((std::size_t)std::abs(s) != (c.N >> 1)) rotation_elts(c, s, gk, out);
+}
+
+// ------------------------------------------------------------------ device memory ----------
+u64 *dalloc(std::size_t words)
+{
+    void *p = nullptr;
+    if (words == 0) words = 1;
+    HEC_HIP(hipMalloc(&p, words * sizeof(u64)));
+    return (u64 *)p;
+}
+void ensure(hec_ciphertext *ct, std::size_t words)
+{
+    if (ct->cap >= words) return;
+    if (ct->d) HEC_HIP(hipFree(ct->d));
+    ct->d = dalloc(words);
+    ct->cap = words;
+}
+
+// stack-style carving of the context workspace; kernels are stream ordered, so a region released
+// here may be reused by the next enqueued operation.
+struct Scratch {
+    Ctx &c;
+    std::size_t top = 0;
+    explicit Scratch(Ctx &cc, std::size_t words) : c(cc) { c.ws.reserve(words); }
+    u64 *take(std::size_t w)
+    {
+        w = (w + 63) & ~(std::size_t)63;
+        if (top + w > c.ws.words) throw std::logic_error("workspace overflow");
+        u64 *p = c.ws.base + top;
+        top += w;
+        return p;
+    }
+};
+
+// ------------------------------------------------------------------ profiling -------------
+struct ProfScope {
+    Ctx &c;
+    std::string name;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    ProfScope(Ctx &cc, const char *n) : c(cc), name(n)
+    {
+        if (!c.prof) return;
+        HEC_HIP(hipEventCreate(&e0));
+        HEC_HIP(hipEventCreate(&e1));
+        HEC_HIP(hipEventRecord(e0, c.stream));
+    }
+    ~ProfScope()
+    {
+        if (!c.prof || !e0) return;
+        (void)hipEventRecord(e1, c.stream);
+        (void)hipEventSynchronize(e1);
+        float ms = 0;
+        (void)hipEventElapsedTime(&ms, e0, e1);
+        auto &r = c.prof_tab[name];
+        r.ms += ms;
+        r.n += 1;
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+    }
+};
+
+// ------------------------------------------------------------------ batched building blocks
+std::size_t ks_words(const Ctx &c, std::size_t B, std::size_t l)
+{
+    return c.N * B * (l + (l + 1) * l + 2 * (l + 1) + 2 * l) + 4 * 64;
+}
+
+void keyswitch(Ctx &c, Scratch &s, PolyArr T, const u64 *key, PolyArr IN, int in_nk, PolyArr OUT, int B, int l)
+{
+    const u64 N = c.N;
+    const std::size_t top = s.top;
+    u64 *D = s.take(B * l * N), *E = s.take((u64)B * (l + 1) * l * N), *ACC = s.take((u64)B * 2 * (l + 1) * N),
+        *Z = s.take((u64)B * 2 * l * N);
+    int pmap[HEC_MAXL + 1];
+    for (int i = 0; i <= HEC_MAXL; ++i) pmap[i] = i;
+    {
+        ProfScope ps(c, "ks_intt");
+        ntt_strided(c, true, T.p, T.sb, D, l * N, l, pmap, B * l);
+    }
+    {
+        ProfScope ps(c, "ks_modup");
+        ks_modup(c, D, E, B, l);
+    }
+    {
+        ProfScope ps(c, "ks_mac");
+        ks_mac(c, T, E, key, ACC, B, l);
+    }
+    {
+        ProfScope ps(c, "ks_moddown");
+        const int pP[1] = {(int)c.K - 1};
+        ntt_strided(c, true, ACC + l * N, (l + 1) * N, ACC + l * N, (l + 1) * N, 1, pP, 2 * B);
+        divide_round(c, ACC + l * N, 2 * (l + 1) * N, (l + 1) * N, PolyArr{ACC, 2 * (l + 1) * N, (l + 1) * N}, IN,
+                     in_nk, OUT, B, 2, l, (int)c.K - 1, c.p_inv.data(), c.p_inv_q.data(), Z);
+    }
+    s.top = top;
+}
+
+// X (size 2) -> OUT = apply_galois(X, elt) followed by key switching; OUT may alias X
+void galois_ks(Ctx &c, Scratch &s, PolyArr X, PolyArr OUT, int B, int l, u32 elt, const u64 *key)
+{
+    const u64 N = c.N;
+    const std::size_t top = s.top;
+    u64 *S = s.take((u64)2 * B * l * N);
+    {
+        ProfScope ps(c, "galois");
+        galois_permute(c, X, PolyArr{S, l * N, (u64)B * l * N}, B, 2, l, elt);
+    }
+    keyswitch(c, s, PolyArr{S + (u64)B * l * N, l * N, 0}, key, PolyArr{S, l * N, 0}, 1, OUT, B, l);
+    s.top = top;
+}
+
+// divide-and-round by q_{l-1}: X = B entries of nk polys at level l -> OUT at level l-1
+void rescale_batch(Ctx &c, Scratch &s, PolyArr X, int B, int nk, int l, PolyArr OUT)
+{
+    ProfScope ps(c, "rescale");
+    const u64 N = c.N;
+    const std::size_t top = s.top;
+    u64 *Y = s.take((u64)B * nk * N), *Z = s.take((u64)B * nk * (l - 1) * N);
+    const int pm[1] = {l - 1};
+    for (int k = 0; k < nk; ++k)
+        ntt_strided(c, true, X.p + k * X.sk + (u64)(l - 1) * N, X.sb, Y + k * N, nk * N, 1, pm, B);
+    divide_round(c, Y, nk * N, N, X, PolyArr{}, 0, OUT, B, nk, l - 1, l - 1, c.ql_inv[l].data(),
+                 c.ql_inv_q[l].data(), Z);
+    s.top = top;
+}
+std::size_t rescale_words(const Ctx &c, std::size_t B, std::size_t nk, std::size_t l)
+{
+    return c.N * B * nk * (1 + 2 * l) + 3 * 64;
+}
+
+void check_ct(const hec_context *ctx, const hec_ciphertext *a)
+{
+    need(a && a->ctx == ctx, "encrypted is not valid for encryption parameters");
+    need(a->level >= 1 && a->level <= ctx->c.L && a->size >= 2 && a->d,
+         "encrypted is not valid for encryption parameters");
+}
+void set_device(hec_context *ctx)
+{
+    need(ctx != nullptr, "context is null");
+    HEC_HIP(hipSetDevice(ctx->c.device));
+}
+
+void d2d(Ctx &c, void *dst, const void *src, std::size_t words)
+{
+    if (words) HEC_HIP(hipMemcpyAsync(dst, src, words * sizeof(u64), hipMemcpyDeviceToDevice, c.stream));
+}
+
+// ------------------------------------------------------------------ he::linalg driver -----
+struct MatvecPlan {
+    std::size_t l = 0;
+    double prod_scale = 0;
+    std::vector<std::vector<u32>> elts;  // per diagonal j
+};
+
+// BatchedMatrix::matmul diag x col (he_linalg.cpp:943-1006) for the p columns at once, diagonals
+// [jb, je).  The loop over i (output column) is interchanged with the loop over j so that one
+// rotation launch sequence and one key read serve all p columns; every out[i] still sums the same
+// terms in the same order, and modular addition is exact, so the bits equal the reference loop's.
+void matvec_core(hec_context *ctx, const hec_ciphertext *const *diags, std::size_t n, std::size_t jb, std::size_t je,
+                 const hec_ciphertext *const *cols, std::size_t p, const hec_kswitch_key *rk,
+                 const hec_galois_keys *gk, bool finish, hec_ciphertext *const *out)
+{
+    Ctx &c = ctx->c;
+    need(n >= 1 && p >= 1 && jb < je && je <= n, "empty matrix operand");
+    need(gk && gk->ctx == ctx, "galois_keys is not valid for encryption parameters");
+    if (finish) need(rk && rk->ctx == ctx, "relin_keys is not valid for encryption parameters");
+    const std::size_t l = cols[0]->level, N = c.N;
+    for (std::size_t j = jb; j < je; ++j) check_ct(ctx, diags[j]);
+    for (std::size_t i = 0; i < p; ++i) check_ct(ctx, cols[i]);
+    for (std::size_t i = 0; i < p; ++i) need(cols[i]->size == 2, "encrypted size must be 2");
+    for (std::size_t j = jb; j < je; ++j) need(diags[j]->size == 2, "encrypted size must be 2");
+    for (std::size_t j = jb; j < je; ++j)
+        need(diags[j]->level == l, "encrypted1 and encrypted2 parameter mismatch");
+    for (std::size_t i = 0; i < p; ++i) need(cols[i]->level == l, "encrypted1 and encrypted2 parameter mismatch");
+    // scale bookkeeping exactly as multiply_inplace (bound) + add_inplace (are_close) would see it
+    std::vector<double> ps(p);
+    for (std::size_t i = 0; i < p; ++i) {
+        for (std::size_t j = jb; j < je; ++j) {
+            const double sc = cols[i]->scale * diags[j]->scale;
+            need(scale_ok(c, sc, l), "scale out of bounds");
+            if (j == jb) ps[i] = sc;
+            else need(are_close(ps[i], sc), "scale mismatch");
+        }
+    }
+    if (finish && l < 2) throw std::invalid_argument("end of modulus switching chain reached");
+    std::vector<std::vector<u32>> elts(je - jb);
+    for (std::size_t j = jb; j < je; ++j) rotation_elts(c, (int)j, *gk, elts[j - jb]);
+
+    const u64 S2 = 2 * l * N, S3 = 3 * l * N;
+    std::size_t words = p * (S2 + S3 + S2) + 2 * p * l * N + ks_words(c, p, l) + 64 * 64;
+    if (finish) words += rescale_words(c, p, 2, l) + p * 2 * (l - 1) * N;
+    Scratch s(c, words);
+    u64 *Xw = s.take(p * S2), *ACC3 = s.take(p * S3), *Rb = s.take(p * S2);
+    for (std::size_t i = 0; i < p; ++i) d2d(c, Xw + i * S2, cols[i]->d, S2);
+    const PolyArr Xa{Xw, S2, l * N}, Ra{Rb, S2, l * N}, Aa{ACC3, S3, l * N};
+    for (std::size_t j = jb; j < je; ++j) {
+        PolyArr src = Xa;
+        for (u32 e : elts[j - jb]) {
+            galois_ks(c, s, src, Ra, (int)p, (int)l, e, gk->keys.at(e));
+            src = Ra;
+        }
+        ProfScope pr(c, "tensor");
+        tensor_acc(c, src, diags[j]->d, l * N, Aa, (int)p, (int)l, j == jb);
+    }
+    if (!finish) {
+        for (std::size_t i = 0; i < p; ++i) {
+            ensure(out[i], S3);
+            d2d(c, out[i]->d, ACC3 + i * S3, S3);
+            out[i]->size = 3; out[i]->level = l; out[i]->scale = ps[i];
+        }
+        return;
+    }
+    {   // relinearize (SMART_RELIN == 1: once per output) — he_linalg.cpp:1000
+        ProfScope pr(c, "relin");
+        keyswitch(c, s, PolyArr{ACC3 + 2 * l * N, S3, 0}, rk->d, Aa, 2, Aa, (int)p, (int)l);
+    }
+    const u64 So = 2 * (l - 1) * N;  // rescale (he_linalg.cpp:1001)
+    u64 *O = s.take(p * So);
+    rescale_batch(c, s, Aa, (int)p, 2, (int)l, PolyArr{O, So, (l - 1) * N});
+    const double ql = (double)c.q[l - 1];
+    for (std::size_t i = 0; i < p; ++i) {
+        ensure(out[i], So);
+        d2d(c, out[i]->d, O + i * So, So);
+        out[i]->size = 2; out[i]->level = l - 1; out[i]->scale = ps[i] / ql;
+    }
+}
+
+}  // namespace
+
+// =============================================================================== workspace ==
+void hec::Workspace::reserve(std::size_t w)
+{
+    if (w <= words) return;
+    if (base) {
+        HEC_HIP(hipDeviceSynchronize());
+        HEC_HIP(hipFree(base));
+        base = nullptr;
+    }
+    base = dalloc(w);
+    words = w;
+}
+void hec::Workspace::release()
+{
+    if (base) (void)hipFree(base);
+    base = nullptr;
+    words = 0;
+}
+
+// =============================================================================== C-ABI =====
+extern "C" {
+
+const char *hec_last_error(void) { return g_err.c_str(); }
+int hec_version(void) { return 100; }
+
+int hec_create_coeff_modulus(uint64_t N, const int *bit_sizes, uint64_t count, uint64_t *out)
+{
+    return guard([&] {
+        need(N >= 2 && !(N & (N - 1)), "poly_modulus_degree is invalid");
+        std::map<int, std::size_t> cnt;
+        for (uint64_t i = 0; i < count; ++i) {
+            need(bit_sizes[i] >= 2 && bit_sizes[i] <= 60, "bit_sizes is invalid");
+            ++cnt[bit_sizes[i]];
+        }
+        const u64 factor = 2 * N;
+        std::map<int, std::vector<u64>> table;
+        for (auto &[b, k] : cnt) {  // SEAL util::get_primes: walk down from ((2^b-1)/2N)*2N+1
+            u64 v = (((u64)1 << b) - 1) / factor * factor + 1;
+            const u64 lo = (u64)1 << (b - 1);
+            std::size_t left = k;
+            while (left && v > lo) {
+                if (isprime(v)) { table[b].push_back(v); --left; }
+                v -= factor;
+            }
+            if (left) throw std::logic_error("failed to find enough qualifying primes");
+        }
+        for (uint64_t i = 0; i < count; ++i) {  // CoeffModulus::Create: back(), pop_back()
+            out[i] = table[bit_sizes[i]].back();
+            table[bit_sizes[i]].pop_back();
+        }
+    });
+}
+
+int hec_context_create(uint64_t N, const uint64_t *mod, uint64_t K, int device, hec_context **out)
+{
+    return guard([&] {
+        need(out != nullptr, "out is null");
+        need(N >= 1024 && N <= 65536 && !(N & (N - 1)), "poly_modulus_degree must be a power of two in [2^10, 2^16]");
+        need(K >= 2 && K - 1 <= HEC_MAXL, "coeff_modulus size is invalid");
+        for (uint64_t i = 0; i < K; ++i)
+            need(isprime(mod[i]) && (mod[i] - 1) % (2 * N) == 0 && !(mod[i] >> 61), "coeff_modulus is invalid");
+        HEC_HIP(hipSetDevice(device));
+        auto *ctx = new hec_context();
+        Ctx &c = ctx->c;
+        c.device = device;
+        c.N = N;
+        c.logN = __builtin_ctzll(N);
+        c.K = K;
+        c.L = K - 1;
+        c.q.assign(mod, mod + K);
+        for (u64 q : c.q) c.bits.push_back(64 - __builtin_clzll(q));
+        HEC_HIP(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
+        c.own_stream = true;
+        std::vector<ulonglong2> tw(K * N), itw(K * N);
+        for (uint64_t i = 0; i < K; ++i) {
+            const u64 q = c.q[i];
+            DevPrime p{};
+            p.q = q;
+            u128 all = ~(u128)0, r = all / q;
+            if (all % q == q - 1) r += 1;
+            p.r0 = (u64)r;
+            p.r1 = (u64)(r >> 64);
+            p.ninv = invm(N % q, q);
+            p.ninv_q = shoupq(p.ninv, q);
+            c.hprimes.push_back(p);
+            const u64 root = minimal_root(2 * N, q), iroot = invm(root, q);
+            u64 pw = 1, ipw = 1;
+            for (uint64_t k = 0; k < N; ++k) {  // tw[bitrev(k)] = root^k
+                const u32 t = brev((u32)k, c.logN);
+                tw[i * N + t] = ulonglong2{pw, shoupq(pw, q)};
+                itw[i * N + t] = ulonglong2{ipw, shoupq(ipw, q)};
+                pw = (u64)((u128)pw * root % q);
+                ipw = (u64)((u128)ipw * iroot % q);
+            }
+        }
+        HEC_HIP(hipMalloc(&c.primes, K * sizeof(DevPrime)));
+        HEC_HIP(hipMemcpy(c.primes, c.hprimes.data(), K * sizeof(DevPrime), hipMemcpyHostToDevice));
+        HEC_HIP(hipMalloc(&c.tw, K * N * sizeof(ulonglong2)));
+        HEC_HIP(hipMalloc(&c.itw, K * N * sizeof(ulonglong2)));
+        HEC_HIP(hipMemcpy(c.tw, tw.data(), K * N * sizeof(ulonglong2), hipMemcpyHostToDevice));
+        HEC_HIP(hipMemcpy(c.itw, itw.data(), K * N * sizeof(ulonglong2), hipMemcpyHostToDevice));
+        const u64 P = c.q[K - 1];
+        for (uint64_t i = 0; i < c.L; ++i) {
+            const u64 q = c.q[i], pi = invm(P % q, q);
+            c.p_inv.push_back(pi);
+            c.p_inv_q.push_back(shoupq(pi, q));
+            c.p_half_mod.push_back((P >> 1) % q);
+        }
+        c.ql_inv.assign(c.L + 1, {});
+        c.ql_inv_q.assign(c.L + 1, {});
+        c.ql_half_mod.assign(c.L + 1, {});
+        for (uint64_t l = 2; l <= c.L; ++l)
+            for (uint64_t i = 0; i + 1 < l; ++i) {
+                const u64 q = c.q[i], ql = c.q[l - 1], v = invm(ql % q, q);
+                c.ql_inv[l].push_back(v);
+                c.ql_inv_q[l].push_back(shoupq(v, q));
+                c.ql_half_mod[l].push_back((ql >> 1) % q);
+            }
+        *out = ctx;
+    });
+}
+
+int hec_context_destroy(hec_context *ctx)
+{
+    return guard([&] {
+        if (!ctx) return;
+        Ctx &c = ctx->c;
+        (void)hipSetDevice(c.device);
+        (void)hipStreamSynchronize(c.stream);
+        c.ws.release();
+        (void)hipFree(c.primes);
+        (void)hipFree(c.tw);
+        (void)hipFree(c.itw);
+        if (c.own_stream) (void)hipStreamDestroy(c.stream);
+        delete ctx;
+    });
+}
+
+int hec_context_set_stream(hec_context *ctx, void *stream)
+{
+    return guard([&] {
+        set_device(ctx);
+        Ctx &c = ctx->c;
+        HEC_HIP(hipStreamSynchronize(c.stream));
+        if (c.own_stream) HEC_HIP(hipStreamDestroy(c.stream));
+        if (stream) {
+            c.stream = (hipStream_t)stream;
+            c.own_stream = false;
+        } else {
+            HEC_HIP(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
+            c.own_stream = true;
+        }
+    });
+}
+
+int hec_context_synchronize(hec_context *ctx)
+{
+    return guard([&] {
+        set_device(ctx);
+        HEC_HIP(hipStreamSynchronize(ctx->c.stream));
+    });
+}
+uint64_t hec_context_poly_degree(const hec_context *ctx) { return ctx ? ctx->c.N : 0; }
+uint64_t hec_context_key_moduli(const hec_context *ctx) { return ctx ? ctx->c.K : 0; }
+
+uint32_t hec_galois_elt_from_step(const hec_context *ctx, int step)
+{
+    u32 e = 0;
+    if (guard([&] { e = elt_from_step(ctx->c, step); })) return 0;
+    return e;
+}
+
+uint64_t hec_default_galois_elts(const hec_context *ctx, uint32_t *out)
+{
+    const u32 m = (u32)(2 * ctx->c.N);
+    std::vector<u32> v{m - 1};
+    u64 pos = 3, neg = invm(3, m);
+    for (int i = 0; i < ctx->c.logN - 1; ++i) {  // SEAL GaloisTool::get_elts_all
+        v.push_back((u32)pos);
+        pos = (pos * pos) & (m - 1);
+        v.push_back((u32)neg);
+        neg = (neg * neg) & (m - 1);
+    }
+    if (out) std::memcpy(out, v.data(), v.size() * sizeof(u32));
+    return v.size();
+}
+
+// ------------------------------------------------------------------ ciphertext / plaintext
+int hec_ciphertext_create(hec_context *ctx, hec_ciphertext **out)
+{
+    return guard([&] {
+        need(ctx && out, "null argument");
+        auto *ct = new hec_ciphertext();
+        ct->ctx = ctx;
+        *out = ct;
+    });
+}
+int hec_ciphertext_destroy(hec_ciphertext *ct)
+{
+    return guard([&] {
+        if (!ct) return;
+        if (ct->d) {
+            (void)hipSetDevice(ct->ctx->c.device);
+            (void)hipStreamSynchronize(ct->ctx->c.stream);
+            (void)hipFree(ct->d);
+        }
+        delete ct;
+    });
+}
+int hec_ciphertext_upload(hec_ciphertext *ct, const uint64_t *host, uint64_t size, uint64_t level, double scale)
+{
+    return guard([&] {
+        need(ct && host, "null argument");
+        Ctx &c = ct->ctx->c;
+        set_device(ct->ctx);
+        need(size >= 1 && level >= 1 && level <= c.K, "encrypted is not valid for encryption parameters");
+        const std::size_t w = size * level * c.N;
+        ensure(ct, w);
+        HEC_HIP(hipMemcpyAsync(ct->d, host, w * sizeof(u64), hipMemcpyHostToDevice, c.stream));
+        HEC_HIP(hipStreamSynchronize(c.stream));
+        ct->size = size; ct->level = level; ct->scale = scale;
+    });
+}
+int hec_ciphertext_download(const hec_ciphertext *ct, uint64_t *host)
+{
+    return guard([&] {
+        need(ct && host && ct->d, "null argument");
+        Ctx &c = ct->ctx->c;
+        set_device(ct->ctx);
+        const std::size_t w = ct->size * ct->level * c.N;
+        HEC_HIP(hipMemcpyAsync(host, ct->d, w * sizeof(u64), hipMemcpyDeviceToHost, c.stream));
+        HEC_HIP(hipStreamSynchronize(c.stream));
+    });
+}
+int hec_ciphertext_info(const hec_ciphertext *ct, uint64_t *size, uint64_t *level, double *scale)
+{
+    return guard([&] {
+        need(ct != nullptr, "null argument");
+        if (size) *size = ct->size;
+        if (level) *level = ct->level;
+        if (scale) *scale = ct->scale;
+    });
+}
+int hec_ciphertext_copy(hec_ciphertext *dst, const hec_ciphertext *src)
+{
+    return guard([&] {
+        need(dst && src && dst->ctx == src->ctx, "null argument");
+        set_device(dst->ctx);
+        if (dst == src) return;
+        const std::size_t w = src->size * src->level * src->ctx->c.N;
+        ensure(dst, w);
+        d2d(src->ctx->c, dst->d, src->d, w);
+        dst->size = src->size; dst->level = src->level; dst->scale = src->scale;
+    });
+}
+int hec_ciphertext_export_device(const hec_ciphertext *ct, void *dev_dst)
+{
+    return guard([&] {
+        need(ct && dev_dst && ct->d, "null argument");
+        set_device(ct->ctx);
+        d2d(ct->ctx->c, dev_dst, ct->d, ct->size * ct->level * ct->ctx->c.N);
+    });
+}
+int hec_ciphertext_import_device(hec_ciphertext *ct, const void *dev_src, uint64_t size, uint64_t level, double scale)
+{
+    return guard([&] {
+        need(ct && dev_src, "null argument");
+        set_device(ct->ctx);
+        const std::size_t w = size * level * ct->ctx->c.N;
+        ensure(ct, w);
+        d2d(ct->ctx->c, ct->d, dev_src, w);
+        ct->size = size; ct->level = level; ct->scale = scale;
+    });
+}
+int hec_ciphertext_reduce(hec_context *ctx, hec_ciphertext *ct)
+{
+    return guard([&] {
+        check_ct(ctx, ct);
+        set_device(ctx);
+        ew_reduce(ctx->c, ct->d, (int)ct->size, (int)ct->level);
+    });
+}
+int hec_ciphertext_fill_uniform(hec_ciphertext *ct, uint64_t size, uint64_t level, double scale, uint64_t seed)
+{
+    return guard([&] {
+        need(ct != nullptr, "null argument");
+        Ctx &c = ct->ctx->c;
+        set_device(ct->ctx);
+        need(size >= 1 && level >= 1 && level <= c.L, "encrypted is not valid for encryption parameters");
+        ensure(ct, size * level * c.N);
+        fill_uniform(c, ct->d, (int)size, (int)level, 0, 0, seed);
+        ct->size = size; ct->level = level; ct->scale = scale;
+    });
+}
+
+int hec_plaintext_create(hec_context *ctx, hec_plaintext **out)
+{
+    return guard([&] {
+        need(ctx && out, "null argument");
+        auto *p = new hec_plaintext();
+        p->ctx = ctx;
+        *out = p;
+    });
+}
+int hec_plaintext_destroy(hec_plaintext *pt)
+{
+    return guard([&] {
+        if (!pt) return;
+        if (pt->d) {
+            (void)hipStreamSynchronize(pt->ctx->c.stream);
+            (void)hipFree(pt->d);
+        }
+        delete pt;
+    });
+}
+int hec_plaintext_upload(hec_plaintext *pt, const uint64_t *host, uint64_t level, double scale)
+{
+    return guard([&] {
+        need(pt && host, "null argument");
+        Ctx &c = pt->ctx->c;
+        set_device(pt->ctx);
+        need(level >= 1 && level <= c.L, "plain is not valid for encryption parameters");
+        const std::size_t w = level * c.N;
+        if (pt->cap < w) {
+            if (pt->d) HEC_HIP(hipFree(pt->d));
+            pt->d = dalloc(w);
+            pt->cap = w;
+        }
+        HEC_HIP(hipMemcpyAsync(pt->d, host, w * sizeof(u64), hipMemcpyHostToDevice, c.stream));
+        HEC_HIP(hipStreamSynchronize(c.stream));
+        pt->level = level; pt->scale = scale;
+    });
+}
+
+// ------------------------------------------------------------------ keys ------------------
+static std::size_t key_words(const Ctx &c) { return c.L * 2 * c.K * c.N; }
+
+int hec_kswitch_key_upload(hec_context *ctx, const uint64_t *host, hec_kswitch_key **out)
+{
+    return guard([&] {
+        need(ctx && host && out, "null argument");
+        set_device(ctx);
+        auto *k = new hec_kswitch_key();
+        k->ctx = ctx;
+        k->d = dalloc(key_words(ctx->c));
+        HEC_HIP(hipMemcpy(k->d, host, key_words(ctx->c) * sizeof(u64), hipMemcpyHostToDevice));
+        *out = k;
+    });
+}
+int hec_kswitch_key_fill_uniform(hec_context *ctx, uint64_t seed, hec_kswitch_key **out)
+{
+    return guard([&] {
+        need(ctx && out, "null argument");
+        set_device(ctx);
+        Ctx &c = ctx->c;
+        auto *k = new hec_kswitch_key();
+        k->ctx = ctx;
+        k->d = dalloc(key_words(c));
+        fill_uniform(c, k->d, (int)(c.L * 2), (int)c.K, 0, 0, seed);
+        HEC_HIP(hipStreamSynchronize(c.stream));
+        *out = k;
+    });
+}
+int hec_kswitch_key_destroy(hec_kswitch_key *key)
+{
+    return guard([&] {
+        if (!key) return;
+        (void)hipStreamSynchronize(key->ctx->c.stream);
+        (void)hipFree(key->d);
+        delete key;
+    });
+}
+int hec_galois_keys_create(hec_context *ctx, hec_galois_keys **out)
+{
+    return guard([&] {
+        need(ctx && out, "null argument");
+        auto *g = new hec_galois_keys();
+        g->ctx = ctx;
+        *out = g;
+    });
+}
+static void gk_check_elt(const Ctx &c, u32 elt)
+{
+    need((elt & 1) && elt < 2 * c.N, "Galois element is not valid");
+}
+int hec_galois_keys_add(hec_galois_keys *gk, uint32_t elt, const uint64_t *host)
+{
+    return guard([&] {
+        need(gk && host, "null argument");
+        Ctx &c = gk->ctx->c;
+        set_device(gk->ctx);
+        gk_check_elt(c, elt);
+        u64 *&d = gk->keys[elt];
+        if (!d) d = dalloc(key_words(c));
+        HEC_HIP(hipMemcpy(d, host, key_words(c) * sizeof(u64), hipMemcpyHostToDevice));
+    });
+}
+int hec_galois_keys_add_uniform(hec_galois_keys *gk, uint32_t elt, uint64_t seed)
+{
+    return guard([&] {
+        need(gk != nullptr, "null argument");
+        Ctx &c = gk->ctx->c;
+        set_device(gk->ctx);
+        gk_check_elt(c, elt);
+        u64 *&d = gk->keys[elt];
+        if (!d) d = dalloc(key_words(c));
+        fill_uniform(c, d, (int)(c.L * 2), (int)c.K, 0, 0, seed);
+        HEC_HIP(hipStreamSynchronize(c.stream));
+    });
+}
+int hec_galois_keys_has(const hec_galois_keys *gk, uint32_t elt) { return gk && gk->keys.count(elt) ? 1 : 0; }
+int hec_galois_keys_destroy(hec_galois_keys *gk)
+{
+    return guard([&] {
+        if (!gk) return;
+        (void)hipStreamSynchronize(gk->ctx->c.stream);
+        for (auto &kv : gk->keys) (void)hipFree(kv.second);
+        delete gk;
+    });
+}
+
+// ------------------------------------------------------------------ evaluator -------------
+int hec_negate_inplace(hec_context *ctx, hec_ciphertext *a)
+{
+    return guard([&] {
+        check_ct(ctx, a);
+        set_device(ctx);
+        ew_negate(ctx->c, PolyArr{a->d, 0, a->level * ctx->c.N}, 1, (int)a->size, (int)a->level);
+    });
+}
+
+static void add_sub(hec_context *ctx, hec_ciphertext *a, const hec_ciphertext *b, bool sub)
+{
+    check_ct(ctx, a);
+    check_ct(ctx, b);
+    set_device(ctx);
+    need(a->level == b->level, "encrypted1 and encrypted2 parameter mismatch");
+    need(are_close(a->scale, b->scale), "scale mismatch");
+    Ctx &c = ctx->c;
+    const u64 ps = a->level * c.N;
+    const std::size_t mn = std::min(a->size, b->size), mx = std::max(a->size, b->size);
+    if (mx > a->size) {  // grow a, keeping its polys
+        if (a->cap < mx * ps) {
+            u64 *nd = dalloc(mx * ps);
+            d2d(c, nd, a->d, a->size * ps);
+            HEC_HIP(hipStreamSynchronize(c.stream));
+            HEC_HIP(hipFree(a->d));
+            a->d = nd;
+            a->cap = mx * ps;
+        }
+    }
+    ew_add(c, PolyArr{a->d, 0, ps}, PolyArr{b->d, 0, ps}, PolyArr{a->d, 0, ps}, 1, (int)mn, (int)a->level,
+           sub ? 1 : 0);
+    if (b->size > a->size) {  // SEAL: copy (add) or negate (sub) the extra polys of b
+        const int extra = (int)(b->size - a->size);
+        if (sub)
+            ew_add(c, PolyArr{a->d + a->size * ps, 0, ps}, PolyArr{b->d + a->size * ps, 0, ps},
+                   PolyArr{a->d + a->size * ps, 0, ps}, 1, extra, (int)a->level, 2);
+        else
+            d2d(c, a->d + a->size * ps, b->d + a->size * ps, extra * ps);
+    }
+    a->size = mx;
+}
+int hec_add_inplace(hec_context *ctx, hec_ciphertext *a, const hec_ciphertext *b)
+{
+    return guard([&] { add_sub(ctx, a, b, false); });
+}
+int hec_sub_inplace(hec_context *ctx, hec_ciphertext *a, const hec_ciphertext *b)
+{
+    return guard([&] { add_sub(ctx, a, b, true); });
+}
+
+static void plain_addsub(hec_context *ctx, hec_ciphertext *a, const hec_plaintext *p, bool sub)
+{
+    check_ct(ctx, a);
+    need(p && p->ctx == ctx && p->d, "plain is not valid for encryption parameters");
+    set_device(ctx);
+    need(a->level == p->level, "encrypted and plain parameter mismatch");
+    need(are_close(a->scale, p->scale), "scale mismatch");
+    const u64 ps = a->level * ctx->c.N;
+    ew_add(ctx->c, PolyArr{a->d, 0, ps}, PolyArr{p->d, 0, ps}, PolyArr{a->d, 0, ps}, 1, 1, (int)a->level,
+           sub ? 1 : 0);
+}
+int hec_add_plain_inplace(hec_context *ctx, hec_ciphertext *a, const hec_plaintext *p)
+{
+    return guard([&] { plain_addsub(ctx, a, p, false); });
+}
+int hec_sub_plain_inplace(hec_context *ctx, hec_ciphertext *a, const hec_plaintext *p)
+{
+    return guard([&] { plain_addsub(ctx, a, p, true); });
+}
+int hec_multiply_plain_inplace(hec_context *ctx, hec_ciphertext *a, const hec_plaintext *p)
+{
+    return guard([&] {
+        check_ct(ctx, a);
+        need(p && p->ctx == ctx && p->d, "plain is not valid for encryption parameters");
+        set_device(ctx);
+        need(a->level == p->level, "encrypted_ntt and plain_ntt parameter mismatch");
+        const double ns = a->scale * p->scale;
+        need(scale_ok(ctx->c, ns, a->level), "scale out of bounds");
+        ew_mul_plain(ctx->c, PolyArr{a->d, 0, 0}, p->d, (int)a->size, (int)a->level);
+        a->scale = ns;
+    });
+}
+
+static void multiply(hec_context *ctx, hec_ciphertext *a, const hec_ciphertext *b)
+{
+    check_ct(ctx, a);
+    check_ct(ctx, b);
+    set_device(ctx);
+    need(a->level == b->level, "encrypted1 and encrypted2 parameter mismatch");
+    const double ns = a->scale * b->scale;
+    need(scale_ok(ctx->c, ns, a->level), "scale out of bounds");
+    Ctx &c = ctx->c;
+    const std::size_t ds = a->size + b->size - 1, ps = a->level * c.N;
+    Scratch s(c, ds * ps + 64);
+    u64 *tmp = s.take(ds * ps);
+    ct_multiply(c, a->d, (int)a->size, b->d, (int)b->size, tmp, (int)a->level);
+    if (a->cap < ds * ps) {
+        HEC_HIP(hipStreamSynchronize(c.stream));
+        HEC_HIP(hipFree(a->d));
+        a->d = dalloc(ds * ps);
+        a->cap = ds * ps;
+    }
+    d2d(c, a->d, tmp, ds * ps);
+    a->size = ds;
+    a->scale = ns;
+}
+int hec_multiply_inplace(hec_context *ctx, hec_ciphertext *a, const hec_ciphertext *b)
+{
+    return guard([&] { multiply(ctx, a, b); });
+}
+int hec_square_inplace(hec_context *ctx, hec_ciphertext *a)
+{
+    return guard([&] { multiply(ctx, a, a); });
+}
+
+int hec_relinearize_inplace(hec_context *ctx, hec_ciphertext *a, const hec_kswitch_key *rk)
+{
+    return guard([&] {
+        check_ct(ctx, a);
+        need(rk && rk->ctx == ctx, "relin_keys is not valid for encryption parameters");
+        set_device(ctx);
+        if (a->size == 2) return;
+        need(a->size == 3, "not enough relinearization keys");
+        Ctx &c = ctx->c;
+        const u64 ps = a->level * c.N;
+        Scratch s(c, ks_words(c, 1, a->level));
+        const PolyArr io{a->d, 0, ps};
+        keyswitch(c, s, PolyArr{a->d + 2 * ps, 0, 0}, rk->d, io, 2, io, 1, (int)a->level);
+        a->size = 2;
+    });
+}
+
+int hec_rescale_to_next_inplace(hec_context *ctx, hec_ciphertext *a)
+{
+    return guard([&] {
+        check_ct(ctx, a);
+        set_device(ctx);
+        if (a->level == 1) throw std::invalid_argument("end of modulus switching chain reached");
+        Ctx &c = ctx->c;
+        const std::size_t l = a->level, N = c.N, nk = a->size, So = nk * (l - 1) * N;
+        Scratch s(c, rescale_words(c, 1, nk, l) + So + 64);
+        u64 *O = s.take(So);
+        rescale_batch(c, s, PolyArr{a->d, nk * l * N, l * N}, 1, (int)nk, (int)l, PolyArr{O, So, (l - 1) * N});
+        d2d(c, a->d, O, So);
+        a->level = l - 1;
+        a->scale = a->scale / (double)c.q[l - 1];
+    });
+}
+
+int hec_mod_switch_to_next_inplace(hec_context *ctx, hec_ciphertext *a)
+{
+    return guard([&] {
+        check_ct(ctx, a);
+        set_device(ctx);
+        if (a->level == 1) throw std::invalid_argument("end of modulus switching chain reached");
+        need(scale_ok(ctx->c, a->scale, a->level - 1), "scale out of bounds");
+        Ctx &c = ctx->c;
+        const std::size_t l = a->level, N = c.N, nk = a->size;
+        Scratch s(c, nk * (l - 1) * N + 64);
+        u64 *O = s.take(nk * (l - 1) * N);
+        for (std::size_t k = 0; k < nk; ++k) d2d(c, O + k * (l - 1) * N, a->d + k * l * N, (l - 1) * N);
+        d2d(c, a->d, O, nk * (l - 1) * N);
+        a->level = l - 1;
+    });
+}
+
+static void galois_single(hec_context *ctx, hec_ciphertext *a, const std::vector<u32> &elts, const hec_galois_keys *gk)
+{
+    Ctx &c = ctx->c;
+    const std::size_t l = a->level, N = c.N;
+    Scratch s(c, ks_words(c, 1, l) + 2 * l * N + 128);
+    const PolyArr x{a->d, 0, l * N};
+    for (u32 e : elts) galois_ks(c, s, x, x, 1, (int)l, e, gk->keys.at(e));
+}
+
+int hec_rotate_vector_inplace(hec_context *ctx, hec_ciphertext *a, int steps, const hec_galois_keys *gk)
+{
+    return guard([&] {
+        check_ct(ctx, a);
+        need(gk && gk->ctx == ctx, "galois_keys is not valid for encryption parameters");
+        set_device(ctx);
+        if (steps == 0) return;  // Evaluator::rotate_internal
+        need(a->size == 2, "encrypted size must be 2");
+        std::vector<u32> elts;
+        rotation_elts(ctx->c, steps, *gk, elts);
+        galois_single(ctx, a, elts, gk);
+    });
+}
+
+int hec_apply_galois_inplace(hec_context *ctx, hec_ciphertext *a, uint32_t elt, const hec_galois_keys *gk)
+{
+    return guard([&] {
+        check_ct(ctx, a);
+        need(gk && gk->ctx == ctx, "galois_keys is not valid for encryption parameters");
+        set_device(ctx);
+        need(gk->keys.count(elt) > 0, "Galois key not present");
+        gk_check_elt(ctx->c, elt);
+        need(a->size == 2, "encrypted size must be 2");
+        galois_single(ctx, a, {elt}, gk);
+    });
+}
+
+// ------------------------------------------------------------------ he::linalg ------------
+int hec_matmul_diag_col(hec_context *ctx, const hec_ciphertext *const *diags, uint64_t n,
+                        const hec_ciphertext *const *cols, uint64_t p, const hec_kswitch_key *rk,
+                        const hec_galois_keys *gk, hec_ciphertext *const *out)
+{
+    return guard([&] {
+        set_device(ctx);
+        need(diags && cols && out, "null argument");
+        matvec_core(ctx, diags, n, 0, n, cols, p, rk, gk, true, out);
+    });
+}
+
+int hec_matmul_diag_col_partial(hec_context *ctx, const hec_ciphertext *const *diags, uint64_t n, uint64_t j_begin,
+                                uint64_t j_end, const hec_ciphertext *const *cols, uint64_t p,
+                                const hec_galois_keys *gk, hec_ciphertext *const *acc_out)
+{
+    return guard([&] {
+        set_device(ctx);
+        need(diags && cols && acc_out, "null argument");
+        matvec_core(ctx, diags, n, j_begin, j_end, cols, p, nullptr, gk, false, acc_out);
+    });
+}
+
+int hec_matmul_finish(hec_context *ctx, hec_ciphertext *const *acc, uint64_t p, const hec_kswitch_key *rk,
+                      hec_ciphertext *const *out)
+{
+    return guard([&] {
+        set_device(ctx);
+        need(acc && out && p >= 1, "null argument");
+        need(rk && rk->ctx == ctx, "relin_keys is not valid for encryption parameters");
+        Ctx &c = ctx->c;
+        const std::size_t l = acc[0]->level, N = c.N, S3 = 3 * l * N, So = 2 * (l - 1) * N;
+        for (uint64_t i = 0; i < p; ++i) {
+            check_ct(ctx, acc[i]);
+            need(acc[i]->size == 3 && acc[i]->level == l, "encrypted1 and encrypted2 parameter mismatch");
+        }
+        if (l < 2) throw std::invalid_argument("end of modulus switching chain reached");
+        Scratch s(c, p * (S3 + So) + ks_words(c, p, l) + rescale_words(c, p, 2, l) + 256);
+        u64 *A3 = s.take(p * S3), *O = s.take(p * So);
+        for (uint64_t i = 0; i < p; ++i) d2d(c, A3 + i * S3, acc[i]->d, S3);
+        const PolyArr Aa{A3, S3, l * N};
+        keyswitch(c, s, PolyArr{A3 + 2 * l * N, S3, 0}, rk->d, Aa, 2, Aa, (int)p, (int)l);
+        rescale_batch(c, s, Aa, (int)p, 2, (int)l, PolyArr{O, So, (l - 1) * N});
+        std::vector<double> sc(p);
+        for (uint64_t i = 0; i < p; ++i) sc[i] = acc[i]->scale / (double)c.q[l - 1];
+        for (uint64_t i = 0; i < p; ++i) {
+            ensure(out[i], So);
+            d2d(c, out[i]->d, O + i * So, So);
+            out[i]->size = 2; out[i]->level = l - 1; out[i]->scale = sc[i];
+        }
+    });
+}
+
+int hec_matmul_col_colT(hec_context *ctx, const hec_ciphertext *const *A, uint64_t n, const hec_ciphertext *const *B,
+                        uint64_t p, const hec_kswitch_key *rk, const hec_galois_keys *gk,
+                        hec_ciphertext *const *out)
+{
+    return guard([&] {
+        set_device(ctx);
+        need(A && B && out && n >= 1 && p >= 1, "null argument");
+        need(rk && rk->ctx == ctx && gk && gk->ctx == ctx, "keys are not valid for encryption parameters");
+        Ctx &c = ctx->c;
+        const std::size_t l = A[0]->level, N = c.N, S2 = 2 * l * N, S3 = 3 * l * N, So = 2 * (l - 1) * N;
+        for (uint64_t j = 0; j < n; ++j) {
+            check_ct(ctx, A[j]);
+            check_ct(ctx, B[j]);
+            need(A[j]->size == 2 && B[j]->size == 2, "encrypted size must be 2");
+            need(A[j]->level == l && B[j]->level == l, "encrypted1 and encrypted2 parameter mismatch");
+        }
+        double sc = 0;
+        for (uint64_t j = 0; j < n; ++j) {
+            const double s = B[j]->scale * A[j]->scale;
+            need(scale_ok(c, s, l), "scale out of bounds");
+            if (j == 0) sc = s;
+            else need(are_close(sc, s), "scale mismatch");
+        }
+        if (l < 2) throw std::invalid_argument("end of modulus switching chain reached");
+        std::vector<std::vector<u32>> elts(p);
+        for (uint64_t i = 0; i < p; ++i) rotation_elts(c, (int)i, *gk, elts[i]);
+        Scratch s(c, n * S2 * 3 + p * (S3 + So) + ks_words(c, std::max<uint64_t>(n, p), l) + 2 * n * l * N +
+                         rescale_words(c, p, 2, l) + 512);
+        u64 *Aw = s.take(n * S2), *Bw = s.take(n * S2), *Rb = s.take(n * S2), *AC = s.take(p * S3),
+            *O = s.take(p * So);
+        for (uint64_t j = 0; j < n; ++j) {
+            d2d(c, Aw + j * S2, A[j]->d, S2);
+            d2d(c, Bw + j * S2, B[j]->d, S2);
+        }
+        const PolyArr Ba{Bw, S2, l * N}, Ra{Rb, S2, l * N}, Aa{Aw, S2, l * N};
+        for (uint64_t i = 0; i < p; ++i) {
+            PolyArr src = Ba;
+            for (u32 e : elts[i]) {
+                galois_ks(c, s, src, Ra, (int)n, (int)l, e, gk->keys.at(e));
+                src = Ra;
+            }
+            tensor_sum(c, src, Aa, AC + i * S3, l * N, (int)n, (int)l);
+        }
+        const PolyArr Ca{AC, S3, l * N};
+        keyswitch(c, s, PolyArr{AC + 2 * l * N, S3, 0}, rk->d, Ca, 2, Ca, (int)p, (int)l);
+        rescale_batch(c, s, Ca, (int)p, 2, (int)l, PolyArr{O, So, (l - 1) * N});
+        for (uint64_t i = 0; i < p; ++i) {
+            ensure(out[i], So);
+            d2d(c, out[i]->d, O + i * So, So);
+            out[i]->size = 2; out[i]->level = l - 1; out[i]->scale = sc / (double)c.q[l - 1];
+        }
+    });
+}
+
+int hec_matrix_matmul(hec_context *ctx, const hec_ciphertext *const *A, uint64_t ar, uint64_t ac, int atr,
+                      const hec_ciphertext *const *B, uint64_t br, uint64_t bc, int btr, const hec_kswitch_key *rk,
+                      hec_ciphertext *const *out)
+{
+    return guard([&] {
+        set_device(ctx);
+        need(A && B && out, "null argument");
+        need(rk && rk->ctx == ctx, "relin_keys is not valid for encryption parameters");
+        Ctx &c = ctx->c;
+        // Matrix::get_dims / ij_to_idx (he_linalg.cpp:25-28, 376-379)
+        const uint64_t r1 = atr ? ac : ar, c1 = atr ? ar : ac, r2 = btr ? bc : br, c2 = btr ? br : bc;
+        need(c1 == r2, "dimension mismatch");
+        auto at = [](const hec_ciphertext *const *M, uint64_t rows, int tr, uint64_t i, uint64_t j) {
+            return M[(tr ? j : i) + rows * (tr ? i : j)];
+        };
+        const std::size_t l = A[0]->level, N = c.N, S3 = 3 * l * N, So = 2 * (l - 1) * N;
+        for (uint64_t k = 0; k < ar * ac; ++k) {
+            check_ct(ctx, A[k]);
+            need(A[k]->size == 2 && A[k]->level == l, "encrypted1 and encrypted2 parameter mismatch");
+        }
+        for (uint64_t k = 0; k < br * bc; ++k) {
+            check_ct(ctx, B[k]);
+            need(B[k]->size == 2 && B[k]->level == l, "encrypted1 and encrypted2 parameter mismatch");
+        }
+        if (l < 2) throw std::invalid_argument("end of modulus switching chain reached");
+        const uint64_t no = r1 * c2;
+        std::vector<double> sc(no);
+        for (uint64_t j = 0; j < c2; ++j)
+            for (uint64_t i = 0; i < r1; ++i)
+                for (uint64_t k = 0; k < c1; ++k) {
+                    const double s = at(A, ar, atr, i, k)->scale * at(B, br, btr, k, j)->scale;
+                    need(scale_ok(c, s, l), "scale out of bounds");
+                    if (k == 0) sc[i + r1 * j] = s;
+                    else need(are_close(sc[i + r1 * j], s), "scale mismatch");
+                }
+        Scratch s(c, no * (S3 + So) + S3 + ks_words(c, no, l) + rescale_words(c, no, 2, l) + 512);
+        u64 *AC = s.take(no * S3), *T = s.take(S3), *O = s.take(no * So);
+        const PolyArr one{nullptr, 0, l * N};
+        for (uint64_t j = 0; j < c2; ++j)
+            for (uint64_t i = 0; i < r1; ++i) {  // he_linalg.cpp:218-228
+                u64 *dst = AC + (i + r1 * j) * S3;
+                for (uint64_t k = 0; k < c1; ++k) {
+                    const hec_ciphertext *x = at(A, ar, atr, i, k), *y = at(B, br, btr, k, j);
+                    ct_multiply(c, x->d, 2, y->d, 2, k == 0 ? dst : T, (int)l);
+                    if (k) ew_add(c, PolyArr{dst, 0, l * N}, PolyArr{T, 0, l * N}, PolyArr{dst, 0, l * N}, 1, 3,
+                                  (int)l, 0);
+                }
+            }
+        (void)one;
+        const PolyArr Ca{AC, S3, l * N};
+        keyswitch(c, s, PolyArr{AC + 2 * l * N, S3, 0}, rk->d, Ca, 2, Ca, (int)no, (int)l);
+        rescale_batch(c, s, Ca, (int)no, 2, (int)l, PolyArr{O, So, (l - 1) * N});
+        for (uint64_t o = 0; o < no; ++o) {
+            ensure(out[o], So);
+            d2d(c, out[o]->d, O + o * So, So);
+            out[o]->size = 2; out[o]->level = l - 1; out[o]->scale = sc[o] / (double)c.q[l - 1];
+        }
+    });
+}
+
+// ------------------------------------------------------------------ primitives ------------
+int hec_ntt_forward(hec_context *ctx, uint64_t *d, uint64_t limb0, uint64_t nl, uint64_t np)
+{
+    return guard([&] {
+        set_device(ctx);
+        need(d && nl >= 1 && limb0 + nl <= ctx->c.K && nl <= HEC_MAXL + 1, "invalid limb range");
+        int pm[HEC_MAXL + 1];
+        for (uint64_t i = 0; i < nl; ++i) pm[i] = (int)(limb0 + i);
+        ntt_strided(ctx->c, false, d, nl * ctx->c.N, d, nl * ctx->c.N, (int)nl, pm, (int)(nl * np));
+    });
+}
+int hec_ntt_inverse(hec_context *ctx, uint64_t *d, uint64_t limb0, uint64_t nl, uint64_t np)
+{
+    return guard([&] {
+        set_device(ctx);
+        need(d && nl >= 1 && limb0 + nl <= ctx->c.K && nl <= HEC_MAXL + 1, "invalid limb range");
+        int pm[HEC_MAXL + 1];
+        for (uint64_t i = 0; i < nl; ++i) pm[i] = (int)(limb0 + i);
+        ntt_strided(ctx->c, true, d, nl * ctx->c.N, d, nl * ctx->c.N, (int)nl, pm, (int)(nl * np));
+    });
+}
+int hec_dyadic_multiply(hec_context *ctx, const uint64_t *a, const uint64_t *b, uint64_t *out, uint64_t limb0,
+                        uint64_t nl, uint64_t np)
+{
+    return guard([&] {
+        set_device(ctx);
+        need(a && b && out && limb0 + nl <= ctx->c.K, "invalid limb range");
+        ew_dyadic(ctx->c, a, b, out, (int)limb0, (int)nl, (int)np);
+    });
+}
+int hec_device_alloc(hec_context *ctx, uint64_t bytes, void **out)
+{
+    return guard([&] {
+        set_device(ctx);
+        HEC_HIP(hipMalloc(out, bytes ? bytes : 8));
+    });
+}
+int hec_device_free(hec_context *ctx, void *p)
+{
+    return guard([&] {
+        set_device(ctx);
+        HEC_HIP(hipStreamSynchronize(ctx->c.stream));
+        HEC_HIP(hipFree(p));
+    });
+}
+int hec_memcpy_h2d(hec_context *ctx, void *dst, const void *src, uint64_t bytes)
+{
+    return guard([&] {
+        set_device(ctx);
+        HEC_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->c.stream));
+        HEC_HIP(hipStreamSynchronize(ctx->c.stream));
+    });
+}
+int hec_memcpy_d2h(hec_context *ctx, void *dst, const void *src, uint64_t bytes)
+{
+    return guard([&] {
+        set_device(ctx);
+        HEC_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->c.stream));
+        HEC_HIP(hipStreamSynchronize(ctx->c.stream));
+    });
+}
+
+int hec_time_ntt_forward(hec_context *ctx, uint64_t *d, uint64_t nl, uint64_t np, int reps, double *ms)
+{
+    return guard([&] {
+        set_device(ctx);
+        need(d && ms && reps >= 1 && nl <= ctx->c.K, "invalid argument");
+        Ctx &c = ctx->c;
+        int pm[HEC_MAXL + 1];
+        for (uint64_t i = 0; i < nl; ++i) pm[i] = (int)i;
+        hipEvent_t e0, e1;
+        HEC_HIP(hipEventCreate(&e0));
+        HEC_HIP(hipEventCreate(&e1));
+        HEC_HIP(hipEventRecord(e0, c.stream));
+        for (int r = 0; r < reps; ++r)
+            ntt_strided(c, false, d, nl * c.N, d, nl * c.N, (int)nl, pm, (int)(nl * np));
+        HEC_HIP(hipEventRecord(e1, c.stream));
+        HEC_HIP(hipEventSynchronize(e1));
+        float t = 0;
+        HEC_HIP(hipEventElapsedTime(&t, e0, e1));
+        *ms = t / reps;
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+    });
+}
+
+int hec_profile_enable(hec_context *ctx, int on)
+{
+    return guard([&] {
+        need(ctx != nullptr, "null");
+        ctx->c.prof = on != 0;
+        if (on) ctx->c.prof_tab.clear();
+    });
+}
+int hec_profile_read(hec_context *ctx, const char *cls, double *total_ms, uint64_t *launches)
+{
+    return guard([&] {
+        need(ctx && cls, "null");
+        auto it = ctx->c.prof_tab.find(cls);
+        if (total_ms) *total_ms = it == ctx->c.prof_tab.end() ? 0 : it->second.ms;
+        if (launches) *launches = it == ctx->c.prof_tab.end() ? 0 : it->second.n;
+    });
+}
+
+}  // extern "C"

@@ -1,0 +1,94 @@
+// Internal host-side structures of the CKKS engine and the kernel launcher interface.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <map>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "hec_device.h"
+
+namespace hec {
+
+struct HipError : std::runtime_error {
+    using std::runtime_error::runtime_error;
+};
+#define HEC_HIP(call)                                                                          \
+    do {                                                                                       \
+        hipError_t e_ = (call);                                                                \
+        if (e_ != hipSuccess)                                                                  \
+            throw ::hec::HipError(std::string(#call) + ": " + hipGetErrorString(e_));          \
+    } while (0)
+
+// Batched polynomial array: address(b, k, i) = p + b*sb + k*sk + i*N
+struct PolyArr {
+    u64 *p = nullptr;
+    u64 sb = 0, sk = 0;
+};
+
+struct Ctx;
+
+// Grow-only device scratch with named carving (no allocation inside steady-state launches).
+struct Workspace {
+    u64 *base = nullptr;
+    std::size_t words = 0;
+    void reserve(std::size_t w);
+    void release();
+};
+
+struct Ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    std::size_t N = 0;
+    int logN = 0;
+    std::size_t K = 0, L = 0;
+    std::vector<u64> q;             // host copy of the key moduli
+    std::vector<DevPrime> hprimes;  // host copy
+    std::vector<int> bits;
+    DevPrime *primes = nullptr;     // device [K]
+    ulonglong2 *tw = nullptr;       // device [K][N] {w, w_shoup}, w = psi^bitrev(idx)
+    ulonglong2 *itw = nullptr;      // device [K][N] inverse twiddles psi^-bitrev(idx)
+    Workspace ws;
+    // host-side constants
+    std::vector<u64> p_inv, p_inv_q, p_half_mod;            // key switch mod-down (per data prime)
+    std::vector<std::vector<u64>> ql_inv, ql_inv_q, ql_half_mod;  // rescale at level l (drop prime l-1)
+    // profiling
+    bool prof = false;
+    struct ProfRec { double ms = 0; uint64_t n = 0; };
+    std::map<std::string, ProfRec> prof_tab;
+    int total_bits(std::size_t level) const
+    {
+        int b = 0;
+        for (std::size_t i = 0; i < level; ++i) b += bits[i];
+        return b;
+    }
+};
+
+// ---------------------------------------------------------------- launchers (hec_kernels.hip)
+// Batched NTT: job -> poly = job / nl, limb = job % nl; reads src + poly*ps_src + limb*N, writes
+// dst + poly*ps_dst + limb*N (src may equal dst), prime = pmap[limb].
+void ntt_strided(Ctx &c, bool inverse, const u64 *src, u64 ps_src, u64 *dst, u64 ps_dst, int nl, const int *pmap,
+                 int njobs);
+// Key-switch phases (B targets at level l; see hec_engine.hip for the dataflow)
+void ks_modup(Ctx &c, const u64 *D, u64 *E, int B, int l);
+void ks_mac(Ctx &c, PolyArr T, const u64 *E, const u64 *key, u64 *ACC, int B, int l);
+// divide-and-round by `last_idx` prime: Y = coefficient-form last limb per (b,k) (address Y + b*ysb + k*ysk),
+// X / IN / OUT addressed (b,k,i), nk polys per batch entry, nl output limbs.
+//   OUT = IN + (X - NTT(corr)) * inv   (IN optional; inv = last^-1 mod q_i)
+void divide_round(Ctx &c, const u64 *Y, u64 ysb, u64 ysk, PolyArr X, PolyArr IN, int in_nk, PolyArr OUT, int B,
+                  int nk, int nl, int last_idx, const u64 *inv, const u64 *inv_q, u64 *Z);
+void galois_permute(Ctx &c, PolyArr in, PolyArr out, int B, int nk, int nl, u32 elt);
+void tensor_acc(Ctx &c, PolyArr R, const u64 *A, u64 a_sk, PolyArr ACC, int B, int l, bool assign);
+void tensor_sum(Ctx &c, PolyArr R, PolyArr A, u64 *ACC, u64 acc_sk, int B, int l);
+void ew_add(Ctx &c, PolyArr a, PolyArr b, PolyArr out, int B, int nk, int nl, int mode);  // 0 add, 1 sub
+void ew_negate(Ctx &c, PolyArr a, int B, int nk, int nl);
+void ew_mul_plain(Ctx &c, PolyArr a, const u64 *pt, int nk, int nl);
+void ew_dyadic(Ctx &c, const u64 *a, const u64 *b, u64 *out, int limb0, int nl, int npolys);
+void ct_multiply(Ctx &c, const u64 *a, int sa, const u64 *b, int sb, u64 *out, int nl);
+void ew_reduce(Ctx &c, u64 *p, int npoly, int nl);
+void fill_uniform(Ctx &c, u64 *p, int npoly, int nl, int limb_prime0, int special_last, u64 seed);
+
+}  // namespace hec

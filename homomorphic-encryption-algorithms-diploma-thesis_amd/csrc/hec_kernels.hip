@@ -1,0 +1,643 @@
+// CDNA4 (gfx950) kernels of the CKKS engine.
+//
+// NTT: an N-point negacyclic NTT (SEAL convention: Cooley-Tukey with bit-reversed twiddles
+// psi^bitrev(k), bit-reversed output) is split into two LDS-staged passes over
+// N = R x C (R = 2^ceil(logN/2) rows, C = 2^floor(logN/2) columns):
+//   pass A: global stages 0..logR-1 run independently on each column (stride-C elements);
+//   pass B: global stages logR..logN-1 run independently on each contiguous chunk of C elements.
+// At local stage s of a P-point sub-transform the butterfly whose upper element has local index x
+// uses global twiddle index  base*2^s + (x >> (logP - s)),  base = 1 in pass A and R + chunk in
+// pass B, so both passes read the same SEAL-ordered twiddle table.  Inside a pass every thread
+// owns 16 elements and does 4 radix-2 stages in registers per round (2 rounds), exchanging through
+// LDS between rounds; the global<->LDS copies are linear so that every wave reads/writes one
+// contiguous 512-B run.  Pre-/post-operations (mod-up reduction, mod-down rounding, P^-1 scaling,
+// accumulation into the ciphertext) are fused into the first-pass load and last-pass store through
+// small IO functors, so the key switch never materialises them separately.
+#include "hec_internal.h"
+
+namespace hec {
+
+// =============================================================================== NTT IO ====
+struct StridedIO {  // job -> (poly = job / nl, limb = job % nl); src/dst may alias (in place)
+    const u64 *src;
+    u64 *dst;
+    u64 ps_src, ps_dst;
+    int nl, logN;
+    int pmap[HEC_MAXL + 1];
+    struct Bound {
+        const u64 *s;
+        u64 *d;
+        int prime;
+        __device__ u64 load(u64 g) const { return s[g]; }
+        __device__ void store(u64 g, u64 v) const { d[g] = v; }
+    };
+    __device__ Bound bind(int job) const
+    {
+        const int poly = job / nl, limb = job % nl;
+        return Bound{src + (u64)poly * ps_src + ((u64)limb << logN), dst + (u64)poly * ps_dst + ((u64)limb << logN),
+                     pmap[limb]};
+    }
+};
+
+// Key-switch mod-up: job t -> (b, I, J), I in [0, l] (I == l is the special prime P), J in [0, l),
+// I != J.  E layout [b][I][J][N].
+struct ModUpMap {
+    int l, logN, kP;
+    __device__ void map(int job, int &b, int &I, int &J) const
+    {
+        const int per = l * l;
+        b = job / per;
+        const int t = job % per;
+        if (t < l * (l - 1)) {
+            I = t / (l - 1);
+            const int r = t % (l - 1);
+            J = r < I ? r : r + 1;
+        } else {
+            I = l;
+            J = t - l * (l - 1);
+        }
+    }
+    __device__ u64 eoff(int b, int I, int J) const { return ((u64)((b * (l + 1) + I) * l + J)) << logN; }
+};
+struct ModUpIO_A {  // load digit J (coefficient form, canonical mod q_J) reduced mod q_I
+    ModUpMap m;
+    const u64 *D;
+    u64 *E;
+    const DevPrime *primes;
+    struct Bound {
+        const u64 *s;
+        u64 *d;
+        u64 q, r1;
+        int prime;
+        __device__ u64 load(u64 g) const { return barrett64(s[g], q, r1); }
+        __device__ void store(u64 g, u64 v) const { d[g] = v; }
+    };
+    __device__ Bound bind(int job) const
+    {
+        int b, I, J;
+        m.map(job, b, I, J);
+        const int p = I == m.l ? m.kP : I;
+        return Bound{D + ((u64)(b * m.l + J) << m.logN), E + m.eoff(b, I, J), primes[p].q, primes[p].r1, p};
+    }
+};
+struct ModUpIO_B {
+    ModUpMap m;
+    u64 *E;
+    struct Bound {
+        u64 *p;
+        int prime;
+        __device__ u64 load(u64 g) const { return p[g]; }
+        __device__ void store(u64 g, u64 v) const { p[g] = v; }
+    };
+    __device__ Bound bind(int job) const
+    {
+        int b, I, J;
+        m.map(job, b, I, J);
+        return Bound{E + m.eoff(b, I, J), I == m.l ? m.kP : I};
+    }
+};
+
+// Divide-and-round by a prime `last` (key-switch mod-down by P, or rescale by q_{l-1}):
+// pass A loads y (coefficient form of the last limb, canonical mod last) and emits
+//   ((y + h) mod last) mod q_i + (q_i - h mod q_i),  h = last >> 1     (in [0, 2 q_i))
+// pass B stores  OUT = IN + (X - NTT(that)) * last^-1 mod q_i.
+struct DivRoundIO_A {
+    const u64 *Y;
+    u64 ysb, ysk;
+    u64 *Z;
+    int nk, nl, logN;
+    u64 last, half;
+    const DevPrime *primes;
+    u64 fix[HEC_MAXL];
+    struct Bound {
+        const u64 *y;
+        u64 *z;
+        u64 last, half, q, r1, fix;
+        int prime;
+        __device__ u64 load(u64 g) const
+        {
+            u64 v = y[g] + half;
+            v = v >= last ? v - last : v;
+            return barrett64(v, q, r1) + fix;
+        }
+        __device__ void store(u64 g, u64 v) const { z[g] = v; }
+    };
+    __device__ Bound bind(int job) const
+    {
+        const int i = job % nl, t = job / nl, k = t % nk, b = t / nk;
+        return Bound{Y + b * ysb + k * ysk, Z + ((u64)job << logN), last, half, primes[i].q, primes[i].r1, fix[i], i};
+    }
+};
+struct DivRoundIO_B {
+    u64 *Z;
+    PolyArr X, IN, OUT;
+    int nk, nl, logN, in_nk;  // IN is added for polys k < in_nk only
+    const DevPrime *primes;
+    u64 inv[HEC_MAXL], inv_q[HEC_MAXL];
+    struct Bound {
+        const u64 *z, *x, *in;
+        u64 *out;
+        u64 q, w, wq;
+        int prime;
+        __device__ u64 load(u64 g) const { return z[g]; }
+        __device__ void store(u64 g, u64 v) const
+        {
+            u64 r = shoup(x[g] + q - v, w, wq, q);
+            if (in) r = addmod(r, in[g], q);
+            out[g] = r;
+        }
+    };
+    __device__ Bound bind(int job) const
+    {
+        const int i = job % nl, t = job / nl, k = t % nk, b = t / nk;
+        const u64 li = (u64)i << logN;
+        return Bound{Z + ((u64)job << logN), X.p + b * X.sb + k * X.sk + li,
+                     (IN.p && k < in_nk) ? IN.p + b * IN.sb + k * IN.sk + li : nullptr, OUT.p + b * OUT.sb + k * OUT.sk + li,
+                     primes[i].q, inv[i], inv_q[i], i};
+    }
+};
+
+// =============================================================================== NTT core ==
+// One round: stages [S0, S1) of a P = 2^LOGP point sub-transform.  Thread `ts` of its segment owns
+// 16 elements = 2^(4-D) groups of 2^D elements (D = S1 - S0).
+template <int LOGP, int RND, bool INV, class AddrF>
+__device__ __forceinline__ void ntt_round(u64 *lds, const AddrF &addr, int ts, u64 base, const ulonglong2 *tw,
+                                          u64 q, u64 two_q)
+{
+    constexpr int S0 = RND * 4;
+    constexpr int S1 = (S0 + 4 < LOGP) ? S0 + 4 : LOGP;
+    constexpr int D = S1 - S0, G = 1 << (4 - D), NQ = 1 << D;
+#pragma unroll
+    for (int gi = 0; gi < G; ++gi) {
+        const int g = ts * G + gi;
+        const int lo = g & ((1 << (LOGP - S1)) - 1);
+        const int hi = g >> (LOGP - S1);
+        const int xb = (hi << (LOGP - S0)) | lo;
+        u64 v[NQ];
+#pragma unroll
+        for (int a = 0; a < NQ; ++a) v[a] = lds[addr(xb | (a << (LOGP - S1)))];
+        if constexpr (!INV) {
+#pragma unroll
+            for (int s = S0; s < S1; ++s) {
+                const int bit = 1 << (S1 - s - 1);
+#pragma unroll
+                for (int a = 0; a < NQ; ++a) {
+                    if (a & bit) continue;
+                    const int xu = xb | (a << (LOGP - S1));
+                    const ulonglong2 w = tw[(base << s) + (u64)(xu >> (LOGP - s))];
+                    ct_bfly(v[a], v[a | bit], w.x, w.y, q, two_q);
+                }
+            }
+        } else {
+#pragma unroll
+            for (int s = S1 - 1; s >= S0; --s) {
+                const int bit = 1 << (S1 - s - 1);
+#pragma unroll
+                for (int a = 0; a < NQ; ++a) {
+                    if (a & bit) continue;
+                    const int xu = xb | (a << (LOGP - S1));
+                    const ulonglong2 w = tw[(base << s) + (u64)(xu >> (LOGP - s))];
+                    gs_bfly(v[a], v[a | bit], w.x, w.y, q, two_q);
+                }
+            }
+        }
+#pragma unroll
+        for (int a = 0; a < NQ; ++a) lds[addr(xb | (a << (LOGP - S1)))] = v[a];
+    }
+}
+
+template <int LOGP, int NSEG, bool INV, bool PASS_A, bool FINAL, class IO>
+__global__ void __launch_bounds__(NSEG *(1 << LOGP) / 16)
+    k_ntt(const IO io, const ulonglong2 *__restrict__ twt, const DevPrime *__restrict__ primes, int logN)
+{
+    constexpr int P = 1 << LOGP, TPS = P / 16, THREADS = NSEG * TPS;
+    constexpr int LD = PASS_A ? (NSEG + 1) : (P + 1);
+    __shared__ u64 lds[PASS_A ? P * (NSEG + 1) : NSEG * (P + 1)];
+    static_assert(LOGP >= 5 && LOGP <= 8, "two rounds of 4 stages");
+
+    const auto bio = io.bind(blockIdx.y);
+    const DevPrime pr = primes[bio.prime];
+    const u64 q = pr.q, two_q = 2 * q;
+    const ulonglong2 *tw = twt + ((u64)bio.prime << logN);
+    const int seg0 = blockIdx.x * NSEG;
+    const int lc = logN - LOGP;  // pass A: log2(#columns)
+
+#pragma unroll 4
+    for (int li = threadIdx.x; li < P * NSEG; li += THREADS) {
+        if constexpr (PASS_A) {
+            const int x = li / NSEG, sg = li % NSEG;
+            lds[x * LD + sg] = bio.load(((u64)x << lc) + seg0 + sg);
+        } else {
+            const int sg = li / P, x = li % P;
+            lds[sg * LD + x] = bio.load(((u64)(seg0 + sg) << LOGP) + x);
+        }
+    }
+    __syncthreads();
+
+    const int ts = threadIdx.x / NSEG, sg = threadIdx.x % NSEG;
+    const u64 base = PASS_A ? 1ull : ((1ull << (logN - LOGP)) + seg0 + sg);
+    auto addr = [sg](int x) { return PASS_A ? x * LD + sg : sg * LD + x; };
+    if constexpr (!INV) {
+        ntt_round<LOGP, 0, false>(lds, addr, ts, base, tw, q, two_q);
+        __syncthreads();
+        ntt_round<LOGP, 1, false>(lds, addr, ts, base, tw, q, two_q);
+    } else {
+        ntt_round<LOGP, 1, true>(lds, addr, ts, base, tw, q, two_q);
+        __syncthreads();
+        ntt_round<LOGP, 0, true>(lds, addr, ts, base, tw, q, two_q);
+    }
+    __syncthreads();
+
+#pragma unroll 4
+    for (int li = threadIdx.x; li < P * NSEG; li += THREADS) {
+        u64 v, g;
+        if constexpr (PASS_A) {
+            const int x = li / NSEG, s2 = li % NSEG;
+            v = lds[x * LD + s2];
+            g = ((u64)x << lc) + seg0 + s2;
+        } else {
+            const int s2 = li / P, x = li % P;
+            v = lds[s2 * LD + x];
+            g = ((u64)(seg0 + s2) << LOGP) + x;
+        }
+        if constexpr (FINAL) {
+            if constexpr (!INV) v = csub(csub(v, two_q), q);
+            else v = shoup(v, pr.ninv, pr.ninv_q, q);
+        }
+        bio.store(g, v);
+    }
+}
+
+template <int LOGR, int LOGC, int NA, int NB, bool INV, class IO1, class IO2>
+static void run_ntt2(Ctx &c, int njobs, const IO1 &first, const IO2 &second)
+{
+    constexpr int R = 1 << LOGR, C = 1 << LOGC;
+    const dim3 gA(C / NA, njobs), gB(R / NB, njobs);
+    constexpr int TA = NA * R / 16, TB = NB * C / 16;
+    if constexpr (!INV) {
+        k_ntt<LOGR, NA, false, true, false><<<gA, TA, 0, c.stream>>>(first, c.tw, c.primes, c.logN);
+        k_ntt<LOGC, NB, false, false, true><<<gB, TB, 0, c.stream>>>(second, c.tw, c.primes, c.logN);
+    } else {
+        k_ntt<LOGC, NB, true, false, false><<<gB, TB, 0, c.stream>>>(first, c.itw, c.primes, c.logN);
+        k_ntt<LOGR, NA, true, true, true><<<gA, TA, 0, c.stream>>>(second, c.itw, c.primes, c.logN);
+    }
+    HEC_HIP(hipGetLastError());
+}
+
+// forward: first = pass A IO (pre-op load), second = pass B IO (post-op store);
+// inverse: first = pass B IO, second = pass A IO.
+template <bool INV, class IO1, class IO2>
+static void ntt_dispatch(Ctx &c, int njobs, const IO1 &first, const IO2 &second)
+{
+    if (njobs <= 0) return;
+    switch (c.logN) {
+    case 10: run_ntt2<5, 5, 32, 32, INV>(c, njobs, first, second); break;
+    case 11: run_ntt2<6, 5, 32, 64, INV>(c, njobs, first, second); break;
+    case 12: run_ntt2<6, 6, 64, 64, INV>(c, njobs, first, second); break;
+    case 13: run_ntt2<7, 6, 32, 64, INV>(c, njobs, first, second); break;
+    case 14: run_ntt2<7, 7, 32, 32, INV>(c, njobs, first, second); break;
+    case 15: run_ntt2<8, 7, 16, 32, INV>(c, njobs, first, second); break;
+    case 16: run_ntt2<8, 8, 16, 16, INV>(c, njobs, first, second); break;
+    default: throw std::invalid_argument("poly_modulus_degree must be 2^10 .. 2^16");
+    }
+}
+
+static StridedIO strided(const u64 *src, u64 *dst, u64 ps_src, u64 ps_dst, int nl, int logN, const int *pmap)
+{
+    StridedIO io{};
+    io.src = src; io.dst = dst; io.ps_src = ps_src; io.ps_dst = ps_dst; io.nl = nl; io.logN = logN;
+    for (int i = 0; i < nl && i <= HEC_MAXL; ++i) io.pmap[i] = pmap[i];
+    return io;
+}
+
+void ntt_strided(Ctx &c, bool inverse, const u64 *src, u64 ps_src, u64 *dst, u64 ps_dst, int nl, const int *pmap,
+                 int njobs)
+{
+    if (nl > HEC_MAXL + 1) throw std::invalid_argument("too many limbs");
+    const StridedIO first = strided(src, dst, ps_src, ps_dst, nl, c.logN, pmap);
+    const StridedIO second = strided(dst, dst, ps_dst, ps_dst, nl, c.logN, pmap);
+    if (inverse) ntt_dispatch<true>(c, njobs, first, second);
+    else ntt_dispatch<false>(c, njobs, first, second);
+}
+
+void ks_modup(Ctx &c, const u64 *D, u64 *E, int B, int l)
+{
+    ModUpMap m{l, c.logN, (int)c.K - 1};
+    ModUpIO_A a{m, D, E, c.primes};
+    ModUpIO_B b{m, E};
+    ntt_dispatch<false>(c, B * l * l, a, b);
+}
+
+void divide_round(Ctx &c, const u64 *Y, u64 ysb, u64 ysk, PolyArr X, PolyArr IN, int in_nk, PolyArr OUT, int B,
+                  int nk, int nl, int last_idx, const u64 *inv, const u64 *inv_q, u64 *Z)
+{
+    if (nl > HEC_MAXL) throw std::invalid_argument("too many limbs");
+    DivRoundIO_A a{};
+    a.Y = Y; a.ysb = ysb; a.ysk = ysk; a.Z = Z; a.nk = nk; a.nl = nl; a.logN = c.logN;
+    a.last = c.q[last_idx]; a.half = a.last >> 1; a.primes = c.primes;
+    for (int i = 0; i < nl; ++i) a.fix[i] = c.q[i] - (a.half % c.q[i]);
+    DivRoundIO_B b{};
+    b.Z = Z; b.X = X; b.IN = IN; b.OUT = OUT; b.nk = nk; b.nl = nl; b.logN = c.logN; b.in_nk = in_nk;
+    b.primes = c.primes;
+    for (int i = 0; i < nl; ++i) { b.inv[i] = inv[i]; b.inv_q[i] = inv_q[i]; }
+    ntt_dispatch<false>(c, B * nk * nl, a, b);
+}
+
+// =============================================================================== key MAC ===
+// ACC[b][k][I] = sum_J E[b][I][J] * key[J][k][I]  (E[b][I][I] = T[b][I], the NTT-form target),
+// 128-bit lazy accumulation then one Barrett reduction (SEAL switch_key_inplace step 3).
+// A thread owns one coefficient for BT batch entries, so each key word is read once per BT targets.
+template <int BT>
+__global__ void __launch_bounds__(256)
+    k_ks_mac(PolyArr T, const u64 *__restrict__ E, const u64 *__restrict__ key, u64 *__restrict__ ACC, int B,
+             int l, int K, int logN, const DevPrime *__restrict__ primes)
+{
+    const u64 N = 1ull << logN;
+    const u64 g = (u64)blockIdx.x * 256 + threadIdx.x;
+    const int I = blockIdx.y;
+    const int b0 = blockIdx.z * BT;
+    const int kI = I == l ? K - 1 : I;
+    const DevPrime pr = primes[kI];
+    U128 a0[BT], a1[BT];
+#pragma unroll
+    for (int t = 0; t < BT; ++t) a0[t] = a1[t] = U128{0, 0};
+    for (int J = 0; J < l; ++J) {
+        const u64 k0 = key[((u64)(J * 2 + 0) * K + kI) * N + g];
+        const u64 k1 = key[((u64)(J * 2 + 1) * K + kI) * N + g];
+#pragma unroll
+        for (int t = 0; t < BT; ++t) {
+            const int b = b0 + t;
+            if (b < B) {
+                const u64 e = (I == J) ? T.p[b * T.sb + (u64)J * N + g]
+                                       : E[((u64)((b * (l + 1) + I) * l + J) << logN) + g];
+                mac128(a0[t], e, k0);
+                mac128(a1[t], e, k1);
+            }
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < BT; ++t) {
+        const int b = b0 + t;
+        if (b < B) {
+            ACC[((u64)((b * 2 + 0) * (l + 1) + I) << logN) + g] = barrett128(a0[t].lo, a0[t].hi, pr.q, pr.r0, pr.r1);
+            ACC[((u64)((b * 2 + 1) * (l + 1) + I) << logN) + g] = barrett128(a1[t].lo, a1[t].hi, pr.q, pr.r0, pr.r1);
+        }
+    }
+}
+
+void ks_mac(Ctx &c, PolyArr T, const u64 *E, const u64 *key, u64 *ACC, int B, int l)
+{
+    constexpr int BT = 8;
+    const dim3 grid((unsigned)(c.N / 256), l + 1, (B + BT - 1) / BT);
+    k_ks_mac<BT><<<grid, 256, 0, c.stream>>>(T, E, key, ACC, B, l, (int)c.K, c.logN, c.primes);
+    HEC_HIP(hipGetLastError());
+}
+
+// =============================================================================== Galois ====
+// SEAL GaloisTool::apply_galois_ntt: out[t] = in[tbl[t]],
+//   tbl[t] = bitrev(((elt * (2 bitrev(t) + 1)) >> 1) & (N - 1))
+__global__ void __launch_bounds__(256)
+    k_galois(PolyArr in, PolyArr out, int nk, int nl, u32 elt, int logN, u64 total)
+{
+    const u64 idx = (u64)blockIdx.x * 256 + threadIdx.x;
+    if (idx >= total) return;
+    const u64 mask = (1ull << logN) - 1;
+    const u32 t = (u32)(idx & mask);
+    u64 rest = idx >> logN;
+    const int i = (int)(rest % nl);
+    rest /= nl;
+    const int k = (int)(rest % nk);
+    const u64 b = rest / nk;
+    const u64 rev = 2ull * bitrev(t, logN) + 1;
+    const u32 src = bitrev((u32)(((u64)elt * rev >> 1) & mask), logN);
+    const u64 li = (u64)i << logN;
+    out.p[b * out.sb + k * out.sk + li + t] = in.p[b * in.sb + k * in.sk + li + src];
+}
+
+void galois_permute(Ctx &c, PolyArr in, PolyArr out, int B, int nk, int nl, u32 elt)
+{
+    const u64 total = (u64)B * nk * nl * c.N;
+    k_galois<<<(unsigned)((total + 255) / 256), 256, 0, c.stream>>>(in, out, nk, nl, elt, c.logN, total);
+    HEC_HIP(hipGetLastError());
+}
+
+// =============================================================================== tensor ====
+// ACC[b] (size 3) (=|+=) R[b] (x) A  (SEAL ckks_multiply 2x2 -> 3, then add_inplace).  A is read once
+// per coefficient for the whole batch.
+__global__ void __launch_bounds__(256)
+    k_tensor_acc(PolyArr R, const u64 *__restrict__ A, u64 a_sk, PolyArr ACC, int B, int logN, u64 total,
+                 int assign, const DevPrime *__restrict__ primes)
+{
+    const u64 idx = (u64)blockIdx.x * 256 + threadIdx.x;
+    if (idx >= total) return;
+    const int i = (int)(idx >> logN);
+    const DevPrime pr = primes[i];
+    const u64 a0 = A[idx], a1 = A[a_sk + idx];
+    for (int b = 0; b < B; ++b) {
+        const u64 *r = R.p + b * R.sb;
+        const u64 r0 = r[idx], r1 = r[R.sk + idx];
+        const u64 d0 = mulmod(r0, a0, pr), d2 = mulmod(r1, a1, pr);
+        U128 t{r0 * a1, mulhi64(r0, a1)};
+        mac128(t, r1, a0);
+        const u64 d1 = barrett128(t.lo, t.hi, pr.q, pr.r0, pr.r1);
+        u64 *o = ACC.p + b * ACC.sb;
+        if (assign) {
+            o[idx] = d0; o[ACC.sk + idx] = d1; o[2 * ACC.sk + idx] = d2;
+        } else {
+            o[idx] = addmod(o[idx], d0, pr.q);
+            o[ACC.sk + idx] = addmod(o[ACC.sk + idx], d1, pr.q);
+            o[2 * ACC.sk + idx] = addmod(o[2 * ACC.sk + idx], d2, pr.q);
+        }
+    }
+}
+
+void tensor_acc(Ctx &c, PolyArr R, const u64 *A, u64 a_sk, PolyArr ACC, int B, int l, bool assign)
+{
+    const u64 total = (u64)l * c.N;
+    k_tensor_acc<<<(unsigned)((total + 255) / 256), 256, 0, c.stream>>>(R, A, a_sk, ACC, B, c.logN, total,
+                                                                         assign ? 1 : 0, c.primes);
+    HEC_HIP(hipGetLastError());
+}
+
+// ACC (size 3) = sum_b R[b] (x) A[b]  (col x col^T form: one output, the batch is the j-sum)
+__global__ void __launch_bounds__(256)
+    k_tensor_sum(PolyArr R, PolyArr A, u64 *__restrict__ ACC, u64 acc_sk, int B, int logN, u64 total,
+                 const DevPrime *__restrict__ primes)
+{
+    const u64 idx = (u64)blockIdx.x * 256 + threadIdx.x;
+    if (idx >= total) return;
+    const int i = (int)(idx >> logN);
+    const DevPrime pr = primes[i];
+    U128 s0{0, 0}, s1{0, 0}, s2{0, 0};
+    for (int b = 0; b < B; ++b) {  // reduce each product (SEAL reduces per multiply), add canonically
+        const u64 *r = R.p + b * R.sb, *a = A.p + b * A.sb;
+        const u64 r0 = r[idx], r1 = r[R.sk + idx], a0 = a[idx], a1 = a[A.sk + idx];
+        U128 t{r0 * a1, mulhi64(r0, a1)};
+        mac128(t, r1, a0);
+        s0.lo = addmod(s0.lo, mulmod(r0, a0, pr), pr.q);
+        s1.lo = addmod(s1.lo, barrett128(t.lo, t.hi, pr.q, pr.r0, pr.r1), pr.q);
+        s2.lo = addmod(s2.lo, mulmod(r1, a1, pr), pr.q);
+    }
+    ACC[idx] = s0.lo;
+    ACC[acc_sk + idx] = s1.lo;
+    ACC[2 * acc_sk + idx] = s2.lo;
+}
+
+void tensor_sum(Ctx &c, PolyArr R, PolyArr A, u64 *ACC, u64 acc_sk, int B, int l)
+{
+    const u64 total = (u64)l * c.N;
+    k_tensor_sum<<<(unsigned)((total + 255) / 256), 256, 0, c.stream>>>(R, A, ACC, acc_sk, B, c.logN, total, c.primes);
+    HEC_HIP(hipGetLastError());
+}
+
+// =============================================================================== misc ======
+__global__ void __launch_bounds__(256) k_ew_add(PolyArr a, PolyArr b, PolyArr out, int nk, int nl, int logN,
+                                                 u64 total, int mode, const DevPrime *__restrict__ primes)
+{
+    const u64 idx = (u64)blockIdx.x * 256 + threadIdx.x;
+    if (idx >= total) return;
+    const u64 N = 1ull << logN, t = idx & (N - 1);
+    u64 rest = idx >> logN;
+    const int i = (int)(rest % nl);
+    rest /= nl;
+    const int k = (int)(rest % nk);
+    const u64 bb = rest / nk;
+    const u64 q = primes[i].q, off = ((u64)i << logN) + t;
+    const u64 x = a.p[bb * a.sb + k * a.sk + off];
+    const u64 y = b.p ? b.p[bb * b.sb + k * b.sk + off] : 0;
+    u64 r;
+    if (mode == 0) r = addmod(x, y, q);
+    else if (mode == 1) r = submod(x, y, q);
+    else r = y ? q - y : 0;  // mode 2: out = -b (sub with a missing left operand)
+    out.p[bb * out.sb + k * out.sk + off] = r;
+}
+
+void ew_add(Ctx &c, PolyArr a, PolyArr b, PolyArr out, int B, int nk, int nl, int mode)
+{
+    const u64 total = (u64)B * nk * nl * c.N;
+    if (!total) return;
+    k_ew_add<<<(unsigned)((total + 255) / 256), 256, 0, c.stream>>>(a, b, out, nk, nl, c.logN, total, mode,
+                                                                     c.primes);
+    HEC_HIP(hipGetLastError());
+}
+
+__global__ void __launch_bounds__(256) k_negate(u64 *p, int nl, int logN, u64 total, const DevPrime *primes)
+{
+    const u64 idx = (u64)blockIdx.x * 256 + threadIdx.x;
+    if (idx >= total) return;
+    const int i = (int)((idx >> logN) % nl);
+    const u64 v = p[idx];
+    p[idx] = v ? primes[i].q - v : 0;
+}
+
+void ew_negate(Ctx &c, PolyArr a, int B, int nk, int nl)
+{
+    // contiguous [k][i][N] per entry (sb == nk * sk)
+    for (int b = 0; b < B; ++b) {
+        const u64 total = (u64)nk * nl * c.N;
+        k_negate<<<(unsigned)((total + 255) / 256), 256, 0, c.stream>>>(a.p + b * a.sb, nl, c.logN, total,
+                                                                        c.primes);
+    }
+    HEC_HIP(hipGetLastError());
+}
+
+__global__ void __launch_bounds__(256) k_mul_plain(u64 *a, const u64 *__restrict__ pt, int nl, int logN,
+                                                    u64 total, const DevPrime *__restrict__ primes)
+{
+    const u64 idx = (u64)blockIdx.x * 256 + threadIdx.x;
+    if (idx >= total) return;
+    const u64 per = (u64)nl << logN;
+    const u64 off = idx % per;
+    const int i = (int)(off >> logN);
+    a[idx] = mulmod(a[idx], pt[off], primes[i]);
+}
+
+void ew_mul_plain(Ctx &c, PolyArr a, const u64 *pt, int nk, int nl)
+{
+    const u64 total = (u64)nk * nl * c.N;
+    k_mul_plain<<<(unsigned)((total + 255) / 256), 256, 0, c.stream>>>(a.p, pt, nl, c.logN, total, c.primes);
+    HEC_HIP(hipGetLastError());
+}
+
+__global__ void __launch_bounds__(256) k_dyadic(const u64 *__restrict__ a, const u64 *__restrict__ b, u64 *out,
+                                                 int limb0, int nl, int logN, u64 total,
+                                                 const DevPrime *__restrict__ primes)
+{
+    const u64 idx = (u64)blockIdx.x * 256 + threadIdx.x;
+    if (idx >= total) return;
+    const int i = (int)((idx >> logN) % nl);
+    out[idx] = mulmod(a[idx], b[idx], primes[limb0 + i]);
+}
+
+void ew_dyadic(Ctx &c, const u64 *a, const u64 *b, u64 *out, int limb0, int nl, int npolys)
+{
+    const u64 total = (u64)npolys * nl * c.N;
+    k_dyadic<<<(unsigned)((total + 255) / 256), 256, 0, c.stream>>>(a, b, out, limb0, nl, c.logN, total, c.primes);
+    HEC_HIP(hipGetLastError());
+}
+
+// general ciphertext product (sizes sa x sb -> sa + sb - 1), out must not alias the inputs
+__global__ void __launch_bounds__(256) k_ct_mul(const u64 *__restrict__ a, int sa, const u64 *__restrict__ b,
+                                                 int sb, u64 *__restrict__ out, int nl, int logN, u64 total,
+                                                 const DevPrime *__restrict__ primes)
+{
+    const u64 idx = (u64)blockIdx.x * 256 + threadIdx.x;  // (i, t) within one poly
+    if (idx >= total) return;
+    const int i = (int)(idx >> logN);
+    const DevPrime pr = primes[i];
+    const u64 ps = total;  // words per poly
+    for (int k = 0; k < sa + sb - 1; ++k) {
+        U128 acc{0, 0};
+        const int x0 = k - (sb - 1) > 0 ? k - (sb - 1) : 0, x1 = k < sa - 1 ? k : sa - 1;
+        for (int x = x0; x <= x1; ++x) mac128(acc, a[x * ps + idx], b[(k - x) * ps + idx]);
+        out[k * ps + idx] = barrett128(acc.lo, acc.hi, pr.q, pr.r0, pr.r1);
+    }
+}
+
+void ct_multiply(Ctx &c, const u64 *a, int sa, const u64 *b, int sb, u64 *out, int nl)
+{
+    const u64 total = (u64)nl * c.N;
+    k_ct_mul<<<(unsigned)((total + 255) / 256), 256, 0, c.stream>>>(a, sa, b, sb, out, nl, c.logN, total, c.primes);
+    HEC_HIP(hipGetLastError());
+}
+
+__global__ void __launch_bounds__(256) k_reduce(u64 *p, int nl, int logN, u64 total, const DevPrime *primes)
+{
+    const u64 idx = (u64)blockIdx.x * 256 + threadIdx.x;
+    if (idx >= total) return;
+    const DevPrime pr = primes[(idx >> logN) % nl];
+    p[idx] = barrett64(p[idx], pr.q, pr.r1);
+}
+
+void ew_reduce(Ctx &c, u64 *p, int npoly, int nl)
+{
+    const u64 total = (u64)npoly * nl * c.N;
+    k_reduce<<<(unsigned)((total + 255) / 256), 256, 0, c.stream>>>(p, nl, c.logN, total, c.primes);
+    HEC_HIP(hipGetLastError());
+}
+
+__device__ __forceinline__ u64 mix64(u64 z)
+{
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+__global__ void __launch_bounds__(256) k_fill(u64 *p, int nl, int logN, u64 total, u64 seed, int prime0,
+                                               const DevPrime *primes)
+{
+    const u64 idx = (u64)blockIdx.x * 256 + threadIdx.x;
+    if (idx >= total) return;
+    const DevPrime pr = primes[prime0 + (int)((idx >> logN) % nl)];
+    p[idx] = barrett64(mix64(seed + 0x9E3779B97F4A7C15ull * (idx + 1)), pr.q, pr.r1);
+}
+
+void fill_uniform(Ctx &c, u64 *p, int npoly, int nl, int limb_prime0, int, u64 seed)
+{
+    const u64 total = (u64)npoly * nl * c.N;
+    k_fill<<<(unsigned)((total + 255) / 256), 256, 0, c.stream>>>(p, nl, c.logN, total, seed, limb_prime0,
+                                                                   c.primes);
+    HEC_HIP(hipGetLastError());
+}
+
+}  // namespace hec

@@ -1,0 +1,170 @@
+/*
+ * hecdna.h — C-ABI of the MI355X-native CKKS homomorphic linear-algebra engine.
+ *
+ * This is the drop-in boundary for the reference's hot path
+ * (isteiakakis/Homomorphic-Encryption-Algorithms-Diploma-Thesis):
+ * every arithmetic step of he::linalg / he::operators goes through a seal::Evaluator member call;
+ * each entry point below replaces one of those calls (reference file:line cited per function) and
+ * keeps its argument meaning, data layout and error behaviour:
+ *
+ *   - data layout = SEAL layout: a ciphertext is u64[size][level][N] in NTT form, a plaintext
+ *     u64[level][N] in NTT form, a key-switching key (one RelinKeys / GaloisKeys entry, i.e. SEAL's
+ *     vector<PublicKey>) u64[L][2][K][N], where K = #coeff_modulus, L = K-1 data primes and
+ *     "level" = number of data primes a ciphertext currently has (SEAL chain index + 1);
+ *   - all residues canonical in [0, q); results are bit-identical to SEAL 4.1's Evaluator;
+ *   - errors: SEAL throws std::invalid_argument / std::logic_error; here every call returns a
+ *     status (HEC_OK, HEC_EINVAL for invalid_argument, HEC_ELOGIC for logic_error, HEC_EDEVICE for a
+ *     HIP failure) and hec_last_error() returns SEAL's message text ("scale mismatch",
+ *     "Galois key not present", "end of modulus switching chain reached", ...).
+ *
+ * Objects are device-resident on the context's GPU; every call is ordered on the context's HIP
+ * stream (hec_context_set_stream), downloads synchronise.  One context per device, one host
+ * thread per context.  No torch types cross this boundary.
+ */
+#ifndef HECDNA_H
+#define HECDNA_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HEC_OK 0
+#define HEC_EINVAL 1
+#define HEC_ELOGIC 2
+#define HEC_EDEVICE 3
+
+typedef struct hec_context hec_context;
+typedef struct hec_ciphertext hec_ciphertext;
+typedef struct hec_plaintext hec_plaintext;
+typedef struct hec_kswitch_key hec_kswitch_key; /* one KSwitchKeys entry: RelinKeys[0] */
+typedef struct hec_galois_keys hec_galois_keys; /* GaloisKeys: galois_elt -> key */
+
+const char *hec_last_error(void);
+int hec_version(void);
+
+/* ---------------------------------------------------------------- parameters / context ---- */
+/* seal::CoeffModulus::Create(N, bit_sizes) — used at reference matrix_operations.cpp:1050 */
+int hec_create_coeff_modulus(uint64_t poly_modulus_degree, const int *bit_sizes, uint64_t count, uint64_t *out);
+/* seal::SEALContext(EncryptionParameters{ckks, N, coeff_modulus}) — matrix_operations.cpp:1047-1051.
+ * coeff_modulus[K-1] is the special (key) prime.  device = HIP device ordinal. */
+int hec_context_create(uint64_t poly_modulus_degree, const uint64_t *coeff_modulus, uint64_t K, int device,
+                       hec_context **out);
+int hec_context_destroy(hec_context *ctx);
+int hec_context_set_stream(hec_context *ctx, void *hip_stream); /* NULL = context-owned stream */
+int hec_context_synchronize(hec_context *ctx);
+uint64_t hec_context_poly_degree(const hec_context *ctx);
+uint64_t hec_context_key_moduli(const hec_context *ctx); /* K */
+/* seal::GaloisTool::get_elt_from_step (rotation step -> Galois element); 0 on error */
+uint32_t hec_galois_elt_from_step(const hec_context *ctx, int step);
+/* seal::GaloisTool::get_elts_all — the set KeyGenerator::create_galois_keys() makes
+ * (matrix_operations.cpp:1063-1064).  Returns the count; writes it when out != NULL. */
+uint64_t hec_default_galois_elts(const hec_context *ctx, uint32_t *out);
+
+/* ---------------------------------------------------------------- ciphertext / plaintext -- */
+int hec_ciphertext_create(hec_context *ctx, hec_ciphertext **out);
+int hec_ciphertext_destroy(hec_ciphertext *ct);
+/* host SEAL-layout buffer u64[size][level][N] -> device */
+int hec_ciphertext_upload(hec_ciphertext *ct, const uint64_t *host, uint64_t size, uint64_t level, double scale);
+/* device -> host (synchronises); host must hold size*level*N words */
+int hec_ciphertext_download(const hec_ciphertext *ct, uint64_t *host);
+int hec_ciphertext_info(const hec_ciphertext *ct, uint64_t *size, uint64_t *level, double *scale);
+int hec_ciphertext_copy(hec_ciphertext *dst, const hec_ciphertext *src); /* value semantics, deep copy */
+/* device-to-device import/export of the raw u64 words (for RCCL exchanges done by the caller) */
+int hec_ciphertext_export_device(const hec_ciphertext *ct, void *dev_dst);
+int hec_ciphertext_import_device(hec_ciphertext *ct, const void *dev_src, uint64_t size, uint64_t level,
+                                 double scale);
+/* canonicalise every word mod its prime (after an integer sum of partial accumulators) */
+int hec_ciphertext_reduce(hec_context *ctx, hec_ciphertext *ct);
+/* synthetic input: uniformly random residues (RLWE ciphertexts are pseudo-uniform) */
+int hec_ciphertext_fill_uniform(hec_ciphertext *ct, uint64_t size, uint64_t level, double scale, uint64_t seed);
+
+int hec_plaintext_create(hec_context *ctx, hec_plaintext **out);
+int hec_plaintext_destroy(hec_plaintext *pt);
+int hec_plaintext_upload(hec_plaintext *pt, const uint64_t *host, uint64_t level, double scale);
+
+/* ---------------------------------------------------------------- keys -------------------- */
+/* RelinKeys (KeyGenerator::create_relin_keys, matrix_operations.cpp:1061-1062): data u64[L][2][K][N] */
+int hec_kswitch_key_upload(hec_context *ctx, const uint64_t *host, hec_kswitch_key **out);
+int hec_kswitch_key_fill_uniform(hec_context *ctx, uint64_t seed, hec_kswitch_key **out);
+int hec_kswitch_key_destroy(hec_kswitch_key *key);
+/* GaloisKeys (KeyGenerator::create_galois_keys, matrix_operations.cpp:1063-1064) */
+int hec_galois_keys_create(hec_context *ctx, hec_galois_keys **out);
+int hec_galois_keys_add(hec_galois_keys *gk, uint32_t galois_elt, const uint64_t *host);
+int hec_galois_keys_add_uniform(hec_galois_keys *gk, uint32_t galois_elt, uint64_t seed);
+int hec_galois_keys_has(const hec_galois_keys *gk, uint32_t galois_elt);
+int hec_galois_keys_destroy(hec_galois_keys *gk);
+
+/* ---------------------------------------------------------------- evaluator --------------- */
+/* Each replaces the seal::Evaluator call behind one he::operators operator
+ * (reference include/he_operators.h:44-159, src/core/he_operators.cpp:14-237). */
+int hec_negate_inplace(hec_context *ctx, hec_ciphertext *a);                                  /* op -= eval     */
+int hec_add_inplace(hec_context *ctx, hec_ciphertext *a, const hec_ciphertext *b);           /* a += eval % b  */
+int hec_sub_inplace(hec_context *ctx, hec_ciphertext *a, const hec_ciphertext *b);           /* a -= eval % b  */
+int hec_add_plain_inplace(hec_context *ctx, hec_ciphertext *a, const hec_plaintext *p);      /* a += eval % pt */
+int hec_sub_plain_inplace(hec_context *ctx, hec_ciphertext *a, const hec_plaintext *p);      /* a -= eval % pt */
+int hec_multiply_inplace(hec_context *ctx, hec_ciphertext *a, const hec_ciphertext *b);      /* a *= eval % b  */
+int hec_multiply_plain_inplace(hec_context *ctx, hec_ciphertext *a, const hec_plaintext *p); /* a *= eval % pt */
+int hec_square_inplace(hec_context *ctx, hec_ciphertext *a);                                  /* he_linalg.cpp:647 */
+int hec_relinearize_inplace(hec_context *ctx, hec_ciphertext *a, const hec_kswitch_key *rk); /* a &= eval % rk */
+int hec_rescale_to_next_inplace(hec_context *ctx, hec_ciphertext *a);                         /* a ^= eval      */
+int hec_mod_switch_to_next_inplace(hec_context *ctx, hec_ciphertext *a);                      /* a |= eval      */
+/* a <<= eval % gk % steps (left); right rotation = negative steps (he_operators.cpp:204-235) */
+int hec_rotate_vector_inplace(hec_context *ctx, hec_ciphertext *a, int steps, const hec_galois_keys *gk);
+int hec_apply_galois_inplace(hec_context *ctx, hec_ciphertext *a, uint32_t galois_elt, const hec_galois_keys *gk);
+
+/* ---------------------------------------------------------------- he::linalg hot path ----- */
+/* BatchedMatrix::matmul(eval, rk, gk, other), diag(this) x col(other) (he_linalg.cpp:943-1006):
+ *   out[i] = rescale(relin( sum_{j<n} rot(cols[i], j) (*) diags[j] )),  i < p
+ * n diagonal ciphertexts, p column ciphertexts (the p independent input vectors of a matvec batch).
+ * out[i] may be fresh ciphertexts; they receive level = input level - 1. */
+int hec_matmul_diag_col(hec_context *ctx, const hec_ciphertext *const *diags, uint64_t n,
+                        const hec_ciphertext *const *cols, uint64_t p, const hec_kswitch_key *rk,
+                        const hec_galois_keys *gk, hec_ciphertext *const *out);
+/* Sharded form: size-3 partial sums over diagonals [j_begin, j_end) (no relin / rescale). */
+int hec_matmul_diag_col_partial(hec_context *ctx, const hec_ciphertext *const *diags, uint64_t n,
+                                uint64_t j_begin, uint64_t j_end, const hec_ciphertext *const *cols, uint64_t p,
+                                const hec_galois_keys *gk, hec_ciphertext *const *acc_out);
+/* relinearize + rescale a batch of size-3 accumulators (he_linalg.cpp:999-1002) */
+int hec_matmul_finish(hec_context *ctx, hec_ciphertext *const *acc, uint64_t p, const hec_kswitch_key *rk,
+                      hec_ciphertext *const *out);
+/* BatchedMatrix::matmul, col(this) x col(other)^T -> diag output:
+ *   out[i] = rescale(relin( sum_{j<n} rot(B[j], i) (*) A[j] )), i < p */
+int hec_matmul_col_colT(hec_context *ctx, const hec_ciphertext *const *A, uint64_t n,
+                        const hec_ciphertext *const *B, uint64_t p, const hec_kswitch_key *rk,
+                        const hec_galois_keys *gk, hec_ciphertext *const *out);
+/* Matrix::matmul (he_linalg.cpp:202-236): column-major element-wise ciphertext matrices
+ * (index i + rows*j, swapped when *_transposed); out has r1*c2 entries, column-major. */
+int hec_matrix_matmul(hec_context *ctx, const hec_ciphertext *const *A, uint64_t a_rows, uint64_t a_cols,
+                      int a_transposed, const hec_ciphertext *const *B, uint64_t b_rows, uint64_t b_cols,
+                      int b_transposed, const hec_kswitch_key *rk, hec_ciphertext *const *out);
+
+/* ---------------------------------------------------------------- primitives (cfg2) ------- */
+/* In-place batched negacyclic NTT over device data u64[npolys][nlimbs][N]; limb j uses prime
+ * limb0 + j (SEAL ntt_negacyclic_harvey / inverse_ntt_negacyclic_harvey, canonical in/out). */
+int hec_ntt_forward(hec_context *ctx, uint64_t *dev_data, uint64_t limb0, uint64_t nlimbs, uint64_t npolys);
+int hec_ntt_inverse(hec_context *ctx, uint64_t *dev_data, uint64_t limb0, uint64_t nlimbs, uint64_t npolys);
+/* out = a (*) b (dyadic_product_coeffmod), same layout */
+int hec_dyadic_multiply(hec_context *ctx, const uint64_t *a, const uint64_t *b, uint64_t *out, uint64_t limb0,
+                        uint64_t nlimbs, uint64_t npolys);
+/* device memory helpers for the primitive API and tests */
+int hec_device_alloc(hec_context *ctx, uint64_t bytes, void **out);
+int hec_device_free(hec_context *ctx, void *p);
+int hec_memcpy_h2d(hec_context *ctx, void *dst, const void *src, uint64_t bytes);
+int hec_memcpy_d2h(hec_context *ctx, void *dst, const void *src, uint64_t bytes);
+
+/* ---------------------------------------------------------------- measurement ------------- */
+/* Time `reps` launches of the batched forward NTT on the context stream with HIP events
+ * (average ms per launch written to *ms). */
+int hec_time_ntt_forward(hec_context *ctx, uint64_t *dev_data, uint64_t nlimbs, uint64_t npolys, int reps,
+                         double *ms);
+/* Per-kernel-class event timing of the matvec (enable, then read cumulative ms and launch counts). */
+int hec_profile_enable(hec_context *ctx, int on);
+int hec_profile_read(hec_context *ctx, const char *kernel_class, double *total_ms, uint64_t *launches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HECDNA_H */

@@ -49,6 +49,7 @@ def lib():
         L.orc_ntt_root.argtypes = [C.c_void_p, C.c_uint64]
         L.orc_barrett128.restype = C.c_uint64
         L.orc_barrett128.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64]
+        L.orc_is_prime.argtypes = [C.c_uint64]
         L.orc_elt_from_step.restype = C.c_uint32
         L.orc_elt_from_step.argtypes = [C.c_void_p, C.c_int]
         L.orc_default_galois_elts.restype = C.c_uint64

@@ -1,0 +1,78 @@
+"""Shared test helpers.  Tests are the only place (with smoke() and bench's cpu_baseline leg) that
+load the oracle, and only as the checker."""
+import importlib.util
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG_DIR = os.path.join(ROOT, "homomorphic-encryption-algorithms-diploma-thesis_amd")
+
+
+def load_hecdna():
+    if "hecdna" in sys.modules:
+        return sys.modules["hecdna"]
+    spec = importlib.util.spec_from_file_location("hecdna", os.path.join(PKG_DIR, "__init__.py"))
+    mod = importlib.util.module_from_spec(spec)
+    sys.modules["hecdna"] = mod
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def load_oracle():
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle_py
+    return oracle_py
+
+
+def ks_count(N, n, elts=None):
+    """Number of key switches SEAL's rotate_internal performs for rotations j = 1..n-1 with the
+    default Galois key set."""
+    def elt(step):
+        m = 2 * N
+        if step < 0:
+            step = N // 2 + step
+        return pow(3, step, m)
+    keys = set()
+    m = 2 * N
+    pos, neg = 3, pow(3, -1, m)
+    keys.add(m - 1)
+    for _ in range(N.bit_length() - 2):
+        keys.add(pos); keys.add(neg)
+        pos = pos * pos % m; neg = neg * neg % m
+
+    def naf(v):
+        res, sign, v, i = [], v < 0, abs(v), 0
+        while v:
+            z = (2 - (v & 3)) if v & 1 else 0
+            v = (v - z) >> 1
+            if z:
+                res.append((-z if sign else z) << i)
+            i += 1
+        return res
+
+    def count(step):
+        if step == 0:
+            return 0
+        if elt(step) in keys:
+            return 1
+        return sum(count(s) for s in naf(step) if abs(s) != N // 2)
+    return sum(count(j) for j in range(1, n))
+
+
+def reference_matrix(n):
+    """The reference's demo data (src/demos/matrix_operations.cpp:1079-1087): column c, row r ->
+    2 + n*c + r.  Returned as M[r][c]."""
+    return np.array([[2 + n * c + r for c in range(n)] for r in range(n)], dtype=np.float64)
+
+
+def diag_vectors(M, slots):
+    """Diagonal j of M (slot r = M[r][(r+j) mod n]) replicated cyclically over all slots."""
+    n = M.shape[0]
+    return [np.array([M[r % n][(r % n + j) % n] for r in range(slots)]) for j in range(n)]
+
+
+def col_vector(x, slots):
+    n = len(x)
+    return np.array([x[r % n] for r in range(slots)])

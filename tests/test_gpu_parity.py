@@ -1,0 +1,273 @@
+"""GPU parity: every HIP path through the C-ABI vs the CPU oracle on the same seeded inputs, bit-exact
+(integer work: SURVEY §8(c)).  Run on the MI355X box with `pytest -m gpu`."""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def sha(a, scale=None):
+    h = hashlib.sha256(np.ascontiguousarray(a, dtype=np.uint64).tobytes())
+    if scale is not None:
+        h.update(np.float64(scale).tobytes())
+    return h.hexdigest()
+
+
+class Env:
+    """Oracle + GPU context over the same parameters and the same keys."""
+
+    def __init__(self, orc, hecdna, N, bits, seed=7, elts=None):
+        self.orc, self.hec = orc, hecdna
+        self.m = orc.Oracle.create_coeff_modulus(N, bits)
+        self.o = orc.Oracle(N, self.m)
+        self.N = N
+        self.ctx = hecdna.Context(N, self.m)
+        self.sk = self.o.secret_key(seed)
+        self.rk_h = self.o.relin_key(self.sk, seed + 1)
+        self.elts = elts if elts is not None else self.o.default_galois_elts()
+        self.gk_h = self.o.galois_keys(self.sk, self.elts, seed + 2)
+        self.rk = self.ctx.relin_key(self.rk_h)
+        self.gk = self.ctx.galois_keys(self.gk_h)
+        self.rng = np.random.default_rng(seed)
+
+    def enc(self, vals=None, level=None, scale=2.0**40, seed=0):
+        level = level or len(self.m) - 1
+        if vals is None:
+            vals = self.rng.uniform(-1, 1, self.N // 2)
+        pt = self.o.encode(vals, scale, level)
+        return self.o.encrypt(self.sk, pt, scale, 1000 + seed)
+
+    def rand_ct(self, size, level, scale=2.0**40):
+        d = np.stack([np.stack([self.rng.integers(0, self.m[i], self.N, dtype=np.uint64) for i in range(level)])
+                      for _ in range(size)])
+        return self.orc.Ct(d, scale)
+
+    def up(self, ct):
+        return self.ctx.ciphertext(ct.data, ct.scale)
+
+    def same(self, g, ct):
+        s, l, sc = g.info()
+        assert (s, l) == (ct.size, ct.level)
+        assert sc == ct.scale
+        assert np.array_equal(g.download(), ct.data)
+
+
+@pytest.fixture(scope="module")
+def env11(orc, hecdna):
+    return Env(orc, hecdna, 1 << 11, [50, 36, 36, 50])
+
+
+@pytest.fixture(scope="module")
+def env15(orc, hecdna):
+    # BASELINE cfg2/cfg3 parameters: N = 2^15, {60, 40 x 9, 60}; keys only for what the tests rotate by
+    return Env(orc, hecdna, 1 << 15, [60] + [40] * 9 + [60], seed=99, elts=None)
+
+
+# ------------------------------------------------------------------------------- NTT ----
+@pytest.mark.parametrize("logN", [10, 11, 12, 13, 14, 15, 16])
+def test_ntt_bitexact(orc, hecdna, logN):
+    N = 1 << logN
+    bits = [60, 40, 50, 60] if logN < 16 else [60, 40, 60]
+    m = orc.Oracle.create_coeff_modulus(N, bits)
+    o = orc.Oracle(N, m)
+    ctx = hecdna.Context(N, m)
+    rng = np.random.default_rng(logN)
+    K = len(m)
+    a = np.stack([np.stack([rng.integers(0, q, N, dtype=np.uint64) for q in m]) for _ in range(3)])
+    fwd = ctx.ntt(a)
+    exp = np.stack([np.stack([o.ntt_fwd(i, a[p, i]) for i in range(K)]) for p in range(3)])
+    assert np.array_equal(fwd, exp)
+    assert np.array_equal(ctx.ntt(fwd, inverse=True), a)
+    # limb offset: limbs 1..K-1 only
+    sub = np.ascontiguousarray(a[:, 1:])
+    assert np.array_equal(ctx.ntt(sub, limb0=1), exp[:, 1:])
+
+
+def test_ntt_cfg2_golden(orc, hecdna):
+    fx = json.load(open(os.path.join(GOLD, "cfg2_ntt.json")))
+    N, m = fx["N"], fx["moduli"]
+    rng = np.random.default_rng(fx["rng_seed"])
+    data = np.stack([rng.integers(0, q, N, dtype=np.uint64) for q in m])
+    assert sha(data) == fx["input_sha256"]
+    ctx = hecdna.Context(N, m)
+    out = ctx.ntt(data[None])[0]
+    assert [sha(out[i]) for i in range(len(m))] == fx["forward_sha256"]
+
+
+# ------------------------------------------------------------------------------- ops -----
+def test_add_sub_negate(env11):
+    e = env11
+    a, b = e.rand_ct(2, 3), e.rand_ct(2, 3)
+    e.same(e.ctx.add(e.up(a), e.up(b)), e.o.add(a, b))
+    e.same(e.ctx.sub(e.up(a), e.up(b)), e.o.sub(a, b))
+    e.same(e.ctx.negate(e.up(a)), e.o.negate(a))
+    c3 = e.rand_ct(3, 3)
+    e.same(e.ctx.add(e.up(a), e.up(c3)), e.o.add(a, c3))   # size grows 2 -> 3 (copy extra poly)
+    e.same(e.ctx.sub(e.up(a), e.up(c3)), e.o.sub(a, c3))   # extra poly negated
+    e.same(e.ctx.add(e.up(c3), e.up(a)), e.o.add(c3, a))
+
+
+def test_multiply_square_plain(env11):
+    e = env11
+    a, b = e.rand_ct(2, 3), e.rand_ct(2, 3)
+    e.same(e.ctx.multiply(e.up(a), e.up(b)), e.o.multiply(a, b))
+    e.same(e.ctx.square(e.up(a)), e.o.square(a))
+    c3 = e.rand_ct(3, 3)
+    e.same(e.ctx.multiply(e.up(c3), e.up(a)), e.o.multiply(c3, a))
+    pt = e.rand_ct(1, 3).data[0]
+    p = e.ctx.plaintext(pt, 2.0**40)
+    e.same(e.ctx.multiply_plain(e.up(a), p), e.o.multiply_plain(a, pt, 2.0**40))
+    e.same(e.ctx.add_plain(e.up(a), p), e.o.add_plain(a, pt, 2.0**40))
+    e.same(e.ctx.sub_plain(e.up(a), p), e.o.sub_plain(a, pt, 2.0**40))
+
+
+def test_relinearize_rescale_modswitch(env11):
+    e = env11
+    for level in (3, 2):
+        c3 = e.rand_ct(3, level, 2.0**60)
+        e.same(e.ctx.relinearize(e.up(c3), e.rk), e.o.relinearize(c3, e.rk_h))
+        e.same(e.ctx.rescale_to_next(e.up(c3)), e.o.rescale(c3))
+        c2 = e.rand_ct(2, level, 2.0**40)
+        e.same(e.ctx.rescale_to_next(e.up(c2)), e.o.rescale(c2))
+        e.same(e.ctx.mod_switch_to_next(e.up(c2)), e.o.mod_switch(c2))
+
+
+@pytest.mark.parametrize("steps", [1, 2, 3, 5, 7, -1, -6, 100, 255, 511, -511, 333])
+def test_rotate(env11, steps):
+    e = env11
+    a = e.rand_ct(2, 3)
+    e.same(e.ctx.rotate_vector(e.up(a), steps, e.gk), e.o.rotate(a, steps, e.gk_h))
+
+
+def test_apply_galois_conjugate(env11):
+    e = env11
+    a = e.rand_ct(2, 2)
+    elt = 2 * e.N - 1
+    e.same(e.ctx.apply_galois(e.up(a), elt, e.gk), e.o.apply_galois(a, elt, e.gk_h))
+
+
+def test_rotation_decrypts(env11):
+    e = env11
+    v = e.rng.uniform(-1, 1, e.N // 2)
+    g = e.up(e.enc(v))
+    e.ctx.rotate_vector(g, 37, e.gk)
+    ct = e.orc.Ct(g.download(), g.scale)
+    d = e.o.decode(e.o.decrypt(e.sk, ct), ct.scale).real
+    assert np.max(np.abs(d - np.roll(v, -37))) < 1e-5
+
+
+def test_errors_follow_seal(env11, hecdna):
+    e = env11
+    a = e.up(e.rand_ct(2, 3, 2.0**40))
+    b = e.up(e.rand_ct(2, 3, 2.0**41))
+    with pytest.raises(hecdna.InvalidArgument, match="scale mismatch"):
+        e.ctx.add(a, b)
+    with pytest.raises(hecdna.InvalidArgument, match="parameter mismatch"):
+        e.ctx.add(a, e.up(e.rand_ct(2, 2)))
+    with pytest.raises(hecdna.InvalidArgument, match="end of modulus switching chain reached"):
+        e.ctx.rescale_to_next(e.up(e.rand_ct(2, 1)))
+    empty = e.ctx.galois_keys({})
+    with pytest.raises(hecdna.InvalidArgument, match="Galois key not present"):
+        e.ctx.rotate_vector(a, 1, empty)
+    with pytest.raises(hecdna.InvalidArgument, match="step count too large"):
+        e.ctx.rotate_vector(a, e.N // 2, e.gk)
+    with pytest.raises(hecdna.InvalidArgument, match="scale out of bounds"):
+        e.ctx.multiply(e.up(e.rand_ct(2, 3, 2.0**70)), e.up(e.rand_ct(2, 3, 2.0**70)))
+    with pytest.raises(hecdna.InvalidArgument, match="encrypted size must be 2"):
+        e.ctx.rotate_vector(e.up(e.rand_ct(3, 3)), 1, e.gk)
+
+
+# ------------------------------------------------------------------------------- linalg --
+def test_matvec_cfg1_golden(orc, hecdna):
+    """The reference demo (matrix_operations.cpp:1042-1175, COL_OR_DIAG=1): all 64 output
+    ciphertexts of the 64x64 diag x col product byte-identical to the oracle's golden hashes."""
+    import sys
+    sys.path.insert(0, GOLD)
+    from make_golden import cfg1_inputs, sha as gsha
+    fx = json.load(open(os.path.join(GOLD, "cfg1_matvec.json")))
+    o, m, sk, rk, gk, cts = cfg1_inputs(orc)
+    assert [gsha(c.data, c.scale) for c in cts] == fx["input_sha256"]
+    ctx = hecdna.Context(fx["N"], m)
+    g = [ctx.ciphertext(c.data, c.scale) for c in cts]
+    out = ctx.matmul_diag_col(g, g, ctx.relin_key(rk), ctx.galois_keys(gk))
+    hashes = [gsha(x.download(), x.scale) for x in out]
+    assert hashes == fx["output_sha256"]
+
+
+def test_matvec_batched_equals_single_and_oracle(env11):
+    e = env11
+    n = 12
+    A = [e.enc(seed=j) for j in range(n)]
+    X = [e.enc(seed=100 + i) for i in range(3)]
+    exp = e.o.matmul_diag_col(A, X, e.rk_h, e.gk_h)
+    gA = [e.up(a) for a in A]
+    gX = [e.up(x) for x in X]
+    got = e.ctx.matmul_diag_col(gA, gX, e.rk, e.gk)
+    for g, c in zip(got, exp):
+        e.same(g, c)
+    one = e.ctx.matmul_diag_col(gA, gX[1:2], e.rk, e.gk)[0]
+    e.same(one, exp[1])
+
+
+def test_matvec_partial_finish_equals_full(env11):
+    e = env11
+    n = 10
+    A = [e.up(e.enc(seed=j)) for j in range(n)]
+    X = [e.up(e.enc(seed=50 + i)) for i in range(2)]
+    full = e.ctx.matmul_diag_col(A, X, e.rk, e.gk)
+    p1 = e.ctx.matmul_diag_col_partial(A, 0, 4, X, e.gk)
+    p2 = e.ctx.matmul_diag_col_partial(A, 4, n, X, e.gk)
+    for a, b in zip(p1, p2):
+        e.ctx.add(a, b)
+    fin = e.ctx.matmul_finish(p1, e.rk)
+    for f, g in zip(fin, full):
+        assert np.array_equal(f.download(), g.download()) and f.scale == g.scale
+
+
+def test_matmul_col_colT(env11):
+    e = env11
+    n, p = 6, 5
+    A = [e.enc(seed=j) for j in range(n)]
+    B = [e.enc(seed=30 + j) for j in range(n)]
+    exp = e.o.matmul_col_colT(A, B, p, e.rk_h, e.gk_h)
+    got = e.ctx.matmul_col_colT([e.up(a) for a in A], [e.up(b) for b in B], p, e.rk, e.gk)
+    for g, c in zip(got, exp):
+        e.same(g, c)
+
+
+def test_matrix_matmul(env11):
+    e = env11
+    A = [e.enc(seed=j) for j in range(6)]   # 2x3 column-major
+    B = [e.enc(seed=20 + j) for j in range(6)]  # 3x2
+    for atr, btr, dims in [(0, 0, (2, 3, 3, 2)), (1, 1, (3, 2, 2, 3))]:
+        ar, ac, br, bc = dims
+        exp = e.o.matrix_matmul(A, ar, ac, atr, B, br, bc, btr, e.rk_h)
+        got = e.ctx.matrix_matmul([e.up(a) for a in A], ar, ac, atr, [e.up(b) for b in B], br, bc, btr, e.rk)
+        assert len(got) == len(exp)
+        for g, c in zip(got, exp):
+            e.same(g, c)
+
+
+# ------------------------------------------------------------------------------- full size
+def test_cfg3_rotations_bitexact(env15):
+    """N = 2^15, L = 10 (BASELINE cfg3 parameters): rotations with 1..7 NAF key switches."""
+    e = env15
+    a = e.enc(seed=1)
+    for steps in (1, 3, 4095, -77):
+        e.same(e.ctx.rotate_vector(e.up(a), steps, e.gk), e.o.rotate(a, steps, e.gk_h))
+
+
+def test_cfg3_matvec_small_n_bitexact(env15):
+    e = env15
+    n = 6
+    A = [e.enc(seed=10 + j) for j in range(n)]
+    X = [e.enc(seed=40 + i) for i in range(2)]
+    exp = e.o.matmul_diag_col(A, X, e.rk_h, e.gk_h, nthreads=8)
+    got = e.ctx.matmul_diag_col([e.up(a) for a in A], [e.up(x) for x in X], e.rk, e.gk)
+    for g, c in zip(got, exp):
+        e.same(g, c)
