@@ -347,10 +347,61 @@ struct MatvecPlan {
     std::vector<std::vector<u32>> elts;  // per diagonal j
 };
 
+// Rotation prefix trie.  SEAL's rotate_internal turns rot(x, j) into a fixed sequence of key
+// switches (one per NAF term, least significant first).  Rotations of the SAME input by different
+// j share prefixes of that sequence (rot by 5 = KS_4(KS_1(x)) starts with rot by 1), so a
+// depth-first walk over the trie of sequences computes every distinct prefix once: each rot(x, j)
+// is still produced by exactly SEAL's sequence of key switches applied to exactly the same
+// intermediate ciphertexts, so the bits are unchanged (cfg3: 18,204 -> 5,460 key switches).
+struct RotTrie {
+    struct Node {
+        u32 elt = 0;
+        std::vector<int> children;
+        std::vector<std::size_t> terminals;  // rotation amounts ending at this node
+    };
+    std::vector<Node> nodes{Node{}};
+    int depth = 0;
+    void insert(const std::vector<u32> &seq, std::size_t tag)
+    {
+        int cur = 0;
+        for (u32 e : seq) {
+            int nxt = -1;
+            for (int c : nodes[cur].children)
+                if (nodes[c].elt == e) { nxt = c; break; }
+            if (nxt < 0) {
+                nodes.push_back(Node{e, {}, {}});
+                nxt = (int)nodes.size() - 1;
+                nodes[cur].children.push_back(nxt);
+            }
+            cur = nxt;
+        }
+        nodes[cur].terminals.push_back(tag);
+        depth = std::max(depth, (int)seq.size());
+    }
+    std::size_t key_switches() const { return nodes.size() - 1; }
+};
+
+// Depth-first walk: visit(tag, src) for every terminal of `node`, then for each child compute the
+// child's rotation into bufs[depth + 1] and recurse.  A buffer at depth d is only overwritten after
+// the subtree that read it has been enqueued (stream order makes that safe).
+template <class F>
+void walk_trie(Ctx &c, Scratch &s, const RotTrie &t, int node, PolyArr src, int depth, int B, int l,
+               const hec_galois_keys &gk, u64 *const *bufs, u64 stride, F &visit)
+{
+    for (std::size_t tag : t.nodes[node].terminals) visit(tag, src);
+    for (int ch : t.nodes[node].children) {
+        const u32 e = t.nodes[ch].elt;
+        const PolyArr dst{bufs[depth + 1], stride, (u64)l * c.N};
+        galois_ks(c, s, src, dst, B, l, e, gk.keys.at(e));
+        walk_trie(c, s, t, ch, dst, depth + 1, B, l, gk, bufs, stride, visit);
+    }
+}
+
 // BatchedMatrix::matmul diag x col (he_linalg.cpp:943-1006) for the p columns at once, diagonals
 // [jb, je).  The loop over i (output column) is interchanged with the loop over j so that one
-// rotation launch sequence and one key read serve all p columns; every out[i] still sums the same
-// terms in the same order, and modular addition is exact, so the bits equal the reference loop's.
+// rotation launch sequence and one key read serve all p columns, and the rotations run over the
+// prefix trie; every out[i] still sums the same terms (modular addition is exact and order free),
+// so the bits equal the reference loop's.
 void matvec_core(hec_context *ctx, const hec_ciphertext *const *diags, std::size_t n, std::size_t jb, std::size_t je,
                  const hec_ciphertext *const *cols, std::size_t p, const hec_kswitch_key *rk,
                  const hec_galois_keys *gk, bool finish, hec_ciphertext *const *out)
@@ -378,25 +429,32 @@ void matvec_core(hec_context *ctx, const hec_ciphertext *const *diags, std::size
         }
     }
     if (finish && l < 2) throw std::invalid_argument("end of modulus switching chain reached");
-    std::vector<std::vector<u32>> elts(je - jb);
-    for (std::size_t j = jb; j < je; ++j) rotation_elts(c, (int)j, *gk, elts[j - jb]);
-
+    RotTrie trie;
+    {
+        std::vector<u32> seq;
+        for (std::size_t j = jb; j < je; ++j) {
+            seq.clear();
+            rotation_elts(c, (int)j, *gk, seq);
+            trie.insert(seq, j);
+        }
+    }
     const u64 S2 = 2 * l * N, S3 = 3 * l * N;
-    std::size_t words = p * (S2 + S3 + S2) + 2 * p * l * N + ks_words(c, p, l) + 64 * 64;
+    const int D = trie.depth;
+    std::size_t words = p * (S2 * (D + 1) + S3) + 2 * p * l * N + ks_words(c, p, l) + (D + 80) * 64;
     if (finish) words += rescale_words(c, p, 2, l) + p * 2 * (l - 1) * N;
     Scratch s(c, words);
-    u64 *Xw = s.take(p * S2), *ACC3 = s.take(p * S3), *Rb = s.take(p * S2);
-    for (std::size_t i = 0; i < p; ++i) d2d(c, Xw + i * S2, cols[i]->d, S2);
-    const PolyArr Xa{Xw, S2, l * N}, Ra{Rb, S2, l * N}, Aa{ACC3, S3, l * N};
-    for (std::size_t j = jb; j < je; ++j) {
-        PolyArr src = Xa;
-        for (u32 e : elts[j - jb]) {
-            galois_ks(c, s, src, Ra, (int)p, (int)l, e, gk->keys.at(e));
-            src = Ra;
-        }
+    std::vector<u64 *> bufs(D + 1);
+    for (int d = 0; d <= D; ++d) bufs[d] = s.take(p * S2);
+    u64 *ACC3 = s.take(p * S3);
+    for (std::size_t i = 0; i < p; ++i) d2d(c, bufs[0] + i * S2, cols[i]->d, S2);
+    const PolyArr Xa{bufs[0], S2, l * N}, Aa{ACC3, S3, l * N};
+    bool first = true;
+    auto visit = [&](std::size_t j, PolyArr src) {
         ProfScope pr(c, "tensor");
-        tensor_acc(c, src, diags[j]->d, l * N, Aa, (int)p, (int)l, j == jb);
-    }
+        tensor_acc(c, src, diags[j]->d, l * N, Aa, (int)p, (int)l, first);
+        first = false;
+    };
+    walk_trie(c, s, trie, 0, Xa, 0, (int)p, (int)l, *gk, bufs.data(), S2, visit);
     if (!finish) {
         for (std::size_t i = 0; i < p; ++i) {
             ensure(out[i], S3);
@@ -517,6 +575,23 @@ int hec_context_create(uint64_t N, const uint64_t *mod, uint64_t K, int device, 
                 ipw = (u64)((u128)ipw * iroot % q);
             }
         }
+        // pass-B re-laid tables: entry (s, i, r) = tw[(R + r) 2^s + i] at R (2^s - 1) + i R + r
+        c.logR = (c.logN + 1) / 2;
+        const uint64_t R = 1ull << c.logR, C = N / R;
+        std::vector<ulonglong2> twb(K * N), itwb(K * N);
+        for (uint64_t i = 0; i < K; ++i)
+            for (uint64_t s = 0; (1ull << s) < C; ++s)
+                for (uint64_t ii = 0; ii < (1ull << s); ++ii)
+                    for (uint64_t r = 0; r < R; ++r) {
+                        const uint64_t dst = i * N + R * ((1ull << s) - 1) + ii * R + r;
+                        const uint64_t src = i * N + (R + r) * (1ull << s) + ii;
+                        twb[dst] = tw[src];
+                        itwb[dst] = itw[src];
+                    }
+        HEC_HIP(hipMalloc(&c.twb, K * N * sizeof(ulonglong2)));
+        HEC_HIP(hipMalloc(&c.itwb, K * N * sizeof(ulonglong2)));
+        HEC_HIP(hipMemcpy(c.twb, twb.data(), K * N * sizeof(ulonglong2), hipMemcpyHostToDevice));
+        HEC_HIP(hipMemcpy(c.itwb, itwb.data(), K * N * sizeof(ulonglong2), hipMemcpyHostToDevice));
         HEC_HIP(hipMalloc(&c.primes, K * sizeof(DevPrime)));
         HEC_HIP(hipMemcpy(c.primes, c.hprimes.data(), K * sizeof(DevPrime), hipMemcpyHostToDevice));
         HEC_HIP(hipMalloc(&c.tw, K * N * sizeof(ulonglong2)));
@@ -555,6 +630,8 @@ int hec_context_destroy(hec_context *ctx)
         (void)hipFree(c.primes);
         (void)hipFree(c.tw);
         (void)hipFree(c.itw);
+        (void)hipFree(c.twb);
+        (void)hipFree(c.itwb);
         if (c.own_stream) (void)hipStreamDestroy(c.stream);
         delete ctx;
     });
@@ -1123,25 +1200,30 @@ int hec_matmul_col_colT(hec_context *ctx, const hec_ciphertext *const *A, uint64
             else need(are_close(sc, s), "scale mismatch");
         }
         if (l < 2) throw std::invalid_argument("end of modulus switching chain reached");
-        std::vector<std::vector<u32>> elts(p);
-        for (uint64_t i = 0; i < p; ++i) rotation_elts(c, (int)i, *gk, elts[i]);
-        Scratch s(c, n * S2 * 3 + p * (S3 + So) + ks_words(c, std::max<uint64_t>(n, p), l) + 2 * n * l * N +
-                         rescale_words(c, p, 2, l) + 512);
-        u64 *Aw = s.take(n * S2), *Bw = s.take(n * S2), *Rb = s.take(n * S2), *AC = s.take(p * S3),
-            *O = s.take(p * So);
+        RotTrie trie;  // rotations rot(B[j], i) for all j share the trie over i
+        {
+            std::vector<u32> seq;
+            for (uint64_t i = 0; i < p; ++i) {
+                seq.clear();
+                rotation_elts(c, (int)i, *gk, seq);
+                trie.insert(seq, i);
+            }
+        }
+        const int D = trie.depth;
+        Scratch s(c, n * S2 * (D + 2) + p * (S3 + So) + ks_words(c, std::max<uint64_t>(n, p), l) + 2 * n * l * N +
+                         rescale_words(c, p, 2, l) + (D + 80) * 64);
+        std::vector<u64 *> bufs(D + 1);
+        for (int d = 0; d <= D; ++d) bufs[d] = s.take(n * S2);
+        u64 *Aw = s.take(n * S2), *AC = s.take(p * S3), *O = s.take(p * So);
         for (uint64_t j = 0; j < n; ++j) {
             d2d(c, Aw + j * S2, A[j]->d, S2);
-            d2d(c, Bw + j * S2, B[j]->d, S2);
+            d2d(c, bufs[0] + j * S2, B[j]->d, S2);
         }
-        const PolyArr Ba{Bw, S2, l * N}, Ra{Rb, S2, l * N}, Aa{Aw, S2, l * N};
-        for (uint64_t i = 0; i < p; ++i) {
-            PolyArr src = Ba;
-            for (u32 e : elts[i]) {
-                galois_ks(c, s, src, Ra, (int)n, (int)l, e, gk->keys.at(e));
-                src = Ra;
-            }
+        const PolyArr Ba{bufs[0], S2, l * N}, Aa{Aw, S2, l * N};
+        auto visit = [&](std::size_t i, PolyArr src) {  // out[i] = sum_j rot(B[j], i) (x) A[j]
             tensor_sum(c, src, Aa, AC + i * S3, l * N, (int)n, (int)l);
-        }
+        };
+        walk_trie(c, s, trie, 0, Ba, 0, (int)n, (int)l, *gk, bufs.data(), S2, visit);
         const PolyArr Ca{AC, S3, l * N};
         keyswitch(c, s, PolyArr{AC + 2 * l * N, S3, 0}, rk->d, Ca, 2, Ca, (int)p, (int)l);
         rescale_batch(c, s, Ca, (int)p, 2, (int)l, PolyArr{O, So, (l - 1) * N});

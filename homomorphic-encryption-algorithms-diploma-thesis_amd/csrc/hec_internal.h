@@ -51,6 +51,9 @@ struct Ctx {
     DevPrime *primes = nullptr;     // device [K]
     ulonglong2 *tw = nullptr;       // device [K][N] {w, w_shoup}, w = psi^bitrev(idx)
     ulonglong2 *itw = nullptr;      // device [K][N] inverse twiddles psi^-bitrev(idx)
+    ulonglong2 *twb = nullptr;      // device [K][N] pass-B layout of tw: [s][i][chunk] (see hec_kernels.hip)
+    ulonglong2 *itwb = nullptr;     // same for itw
+    int logR = 0;                   // pass split N = R x C, R = 2^ceil(logN/2)
     Workspace ws;
     // host-side constants
     std::vector<u64> p_inv, p_inv_q, p_half_mod;            // key switch mod-down (per data prime)

@@ -160,8 +160,8 @@ struct DivRoundIO_B {
 // =============================================================================== NTT core ==
 // One round: stages [S0, S1) of a P = 2^LOGP point sub-transform.  Thread `ts` of its segment owns
 // 16 elements = 2^(4-D) groups of 2^D elements (D = S1 - S0).
-template <int LOGP, int RND, bool INV, class AddrF>
-__device__ __forceinline__ void ntt_round(u64 *lds, const AddrF &addr, int ts, u64 base, const ulonglong2 *tw,
+template <int LOGP, int RND, bool INV, class AddrF, class TwF>
+__device__ __forceinline__ void ntt_round(u64 *lds, const AddrF &addr, int ts, const TwF &twidx, const ulonglong2 *tw,
                                           u64 q, u64 two_q)
 {
     constexpr int S0 = RND * 4;
@@ -184,7 +184,7 @@ __device__ __forceinline__ void ntt_round(u64 *lds, const AddrF &addr, int ts, u
                 for (int a = 0; a < NQ; ++a) {
                     if (a & bit) continue;
                     const int xu = xb | (a << (LOGP - S1));
-                    const ulonglong2 w = tw[(base << s) + (u64)(xu >> (LOGP - s))];
+                    const ulonglong2 w = tw[twidx(s, xu >> (LOGP - s))];
                     ct_bfly(v[a], v[a | bit], w.x, w.y, q, two_q);
                 }
             }
@@ -196,7 +196,7 @@ __device__ __forceinline__ void ntt_round(u64 *lds, const AddrF &addr, int ts, u
                 for (int a = 0; a < NQ; ++a) {
                     if (a & bit) continue;
                     const int xu = xb | (a << (LOGP - S1));
-                    const ulonglong2 w = tw[(base << s) + (u64)(xu >> (LOGP - s))];
+                    const ulonglong2 w = tw[twidx(s, xu >> (LOGP - s))];
                     gs_bfly(v[a], v[a | bit], w.x, w.y, q, two_q);
                 }
             }
@@ -235,16 +235,24 @@ __global__ void __launch_bounds__(NSEG *(1 << LOGP) / 16)
     __syncthreads();
 
     const int ts = threadIdx.x / NSEG, sg = threadIdx.x % NSEG;
-    const u64 base = PASS_A ? 1ull : ((1ull << (logN - LOGP)) + seg0 + sg);
     auto addr = [sg](int x) { return PASS_A ? x * LD + sg : sg * LD + x; };
+    // pass A: SEAL table index 2^s + i (shared by all columns: broadcast reads).
+    // pass B: the per-chunk index (R + r) 2^s + i is served from the re-laid table
+    //         twb[s][i][r] = tw[(R + r) 2^s + i] at R (2^s - 1) + i R + r, so lanes (consecutive
+    //         chunks r) read consecutive 16-B entries.
+    const u64 R = 1ull << (logN - LOGP), chunk = (u64)(seg0 + sg);
+    auto twidx = [=](int s, int i) -> u64 {
+        if constexpr (PASS_A) return (1ull << s) + (u64)i;
+        else return R * ((1ull << s) - 1) + (u64)i * R + chunk;
+    };
     if constexpr (!INV) {
-        ntt_round<LOGP, 0, false>(lds, addr, ts, base, tw, q, two_q);
+        ntt_round<LOGP, 0, false>(lds, addr, ts, twidx, tw, q, two_q);
         __syncthreads();
-        ntt_round<LOGP, 1, false>(lds, addr, ts, base, tw, q, two_q);
+        ntt_round<LOGP, 1, false>(lds, addr, ts, twidx, tw, q, two_q);
     } else {
-        ntt_round<LOGP, 1, true>(lds, addr, ts, base, tw, q, two_q);
+        ntt_round<LOGP, 1, true>(lds, addr, ts, twidx, tw, q, two_q);
         __syncthreads();
-        ntt_round<LOGP, 0, true>(lds, addr, ts, base, tw, q, two_q);
+        ntt_round<LOGP, 0, true>(lds, addr, ts, twidx, tw, q, two_q);
     }
     __syncthreads();
 
@@ -276,9 +284,9 @@ static void run_ntt2(Ctx &c, int njobs, const IO1 &first, const IO2 &second)
     constexpr int TA = NA * R / 16, TB = NB * C / 16;
     if constexpr (!INV) {
         k_ntt<LOGR, NA, false, true, false><<<gA, TA, 0, c.stream>>>(first, c.tw, c.primes, c.logN);
-        k_ntt<LOGC, NB, false, false, true><<<gB, TB, 0, c.stream>>>(second, c.tw, c.primes, c.logN);
+        k_ntt<LOGC, NB, false, false, true><<<gB, TB, 0, c.stream>>>(second, c.twb, c.primes, c.logN);
     } else {
-        k_ntt<LOGC, NB, true, false, false><<<gB, TB, 0, c.stream>>>(first, c.itw, c.primes, c.logN);
+        k_ntt<LOGC, NB, true, false, false><<<gB, TB, 0, c.stream>>>(first, c.itwb, c.primes, c.logN);
         k_ntt<LOGR, NA, true, true, true><<<gA, TA, 0, c.stream>>>(second, c.itw, c.primes, c.logN);
     }
     HEC_HIP(hipGetLastError());
