@@ -159,7 +159,8 @@ def main():
         ctx.profile(True)
         step()
         ctx.synchronize()
-        for cls in ("ks_intt", "ks_modup", "ks_mac", "ks_moddown", "galois", "tensor", "relin", "rescale"):
+        for cls in ("ks_intt", "ks_modup", "ks_mac", "ks_modup_mac", "ks_moddown", "galois", "tensor", "relin",
+                    "rescale"):
             ms, cnt = ctx.profile_read(cls)
             breakdown[cls] = {"ms": round(ms, 3), "launch_groups": cnt}
         ctx.profile(False)

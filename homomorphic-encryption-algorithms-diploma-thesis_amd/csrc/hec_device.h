@@ -19,6 +19,8 @@ struct DevPrime {
     u64 q;
     u64 r0, r1;         // floor(2^128 / q) = r1:r0 (SEAL Modulus::const_ratio)
     u64 ninv, ninv_q;   // N^-1 mod q and its Shoup quotient
+    double qd, qinv, ninv_d;  // FP64 path (q < 2^42 only): q, 1/q, N^-1 as doubles
+    int fp;                   // 1 -> NTT kernels use the exact FP64 arithmetic below
 };
 
 __device__ __forceinline__ u64 mulhi64(u64 a, u64 b) { return __umul64hi(a, b); }
@@ -80,3 +82,52 @@ __device__ __forceinline__ void gs_bfly(u64 &X, u64 &Y, u64 w, u64 wq, u64 q, u6
 }
 
 __device__ __forceinline__ u32 bitrev(u32 x, int bits) { return __brev(x) >> (32 - bits); }
+
+// ------------------------------------------------------------------ exact FP64 modular arithmetic
+// For q < 2^42 (fp = 1) residues are carried as integer-valued doubles.  gfx950 issues an FP64
+// FMA in 4 cycles per wave vs 8 for a 32-bit integer multiply, and a 64x64->128 product needs
+// 9 such multiplies, so this path is several times cheaper than Shoup on u64.
+// fp_mulmod(y, w): TwoProduct  h + l = y*w exactly (h = fl(y*w), l = fma(y, w, -h));
+// k = rint(h * (1/q)) is within 0.5 + 3|y| 2^-53 of y*w/q (w < q), so for |y| <= 10 q < 2^45.4
+// r = (h - k q) + l is computed exactly (every intermediate is an integer below 2^53) and
+// r = y*w - k q lies in [-0.53q, 0.53q].
+// The result is congruent to y*w mod q; canonical residues are taken only at kernel outputs, so the
+// final bits equal any other exact implementation's.
+#pragma clang fp contract(off)
+__device__ __forceinline__ double fp_mulmod(double y, double w, double q, double qinv)
+{
+    const double h = y * w;
+    const double l = __fma_rn(y, w, -h);
+    const double k = rint(h * qinv);
+    const double r = __fma_rn(-k, q, h);
+    return r + l;
+}
+__device__ __forceinline__ double fp_reduce(double x, double q, double qinv)  // -> [-0.53q, 0.53q]
+{
+    return __fma_rn(-rint(x * qinv), q, x);
+}
+// forward CT: |X| grows by <= 0.53q per stage (< 10q after 16 stages from inputs < 2q)
+__device__ __forceinline__ void ct_bfly_fp(double &X, double &Y, double w, double q, double qinv)
+{
+    const double t = fp_mulmod(Y, w, q, qinv);
+    Y = X - t;
+    X = X + t;
+}
+// inverse GS: sums are re-centred every stage so magnitudes stay below q
+__device__ __forceinline__ void gs_bfly_fp(double &X, double &Y, double w, double q, double qinv)
+{
+    const double s = X + Y, dlt = X - Y;
+    X = fp_reduce(s, q, qinv);
+    Y = fp_mulmod(dlt, w, q, qinv);
+}
+#pragma clang fp contract(on)
+// exact u64 <-> double for 0 <= x < 2^52 through the 2^52 magic number
+__device__ __forceinline__ double u2d(u64 x) { return __longlong_as_double((long long)(x | 0x4330000000000000ull)) - 4503599627370496.0; }
+__device__ __forceinline__ u64 d2u(double x) { return (u64)__double_as_longlong(x + 4503599627370496.0) - 0x4330000000000000ull; }
+// integer-valued double with |x| < 2^52 -> canonical residue as u64
+__device__ __forceinline__ u64 fp_canon(double x, double q, double qinv)
+{
+    double r = fp_reduce(x, q, qinv);
+    r = r < 0 ? r + q : r;
+    return d2u(r);
+}

@@ -15,6 +15,7 @@
 //   (5) OUT[b][k][i] = IN[b][k][i] + (ACC[b][k][i] - NTT_i(round(y))) * P^-1     divide_round
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
 
@@ -272,13 +273,18 @@ void keyswitch(Ctx &c, Scratch &s, PolyArr T, const u64 *key, PolyArr IN, int in
         ProfScope ps(c, "ks_intt");
         ntt_strided(c, true, T.p, T.sb, D, l * N, l, pmap, B * l);
     }
-    {
-        ProfScope ps(c, "ks_modup");
-        ks_modup(c, D, E, B, l);
-    }
-    {
-        ProfScope ps(c, "ks_mac");
-        ks_mac(c, T, E, key, ACC, B, l);
+    if (c.fused_modup_mac) {  // experimental: latency-bound at small batch
+        ProfScope ps(c, "ks_modup_mac");
+        ks_modup_mac(c, D, E, T, key, ACC, B, l);
+    } else {
+        {
+            ProfScope ps(c, "ks_modup");
+            ks_modup(c, D, E, B, l);
+        }
+        {
+            ProfScope ps(c, "ks_mac");
+            ks_mac(c, T, E, key, ACC, B, l);
+        }
     }
     {
         ProfScope ps(c, "ks_moddown");
@@ -545,6 +551,7 @@ int hec_context_create(uint64_t N, const uint64_t *mod, uint64_t K, int device, 
         auto *ctx = new hec_context();
         Ctx &c = ctx->c;
         c.device = device;
+        if (const char *f = std::getenv("HEC_FUSED_MODUP_MAC")) c.fused_modup_mac = f[0] == '1';
         c.N = N;
         c.logN = __builtin_ctzll(N);
         c.K = K;
@@ -564,6 +571,10 @@ int hec_context_create(uint64_t N, const uint64_t *mod, uint64_t K, int device, 
             p.r1 = (u64)(r >> 64);
             p.ninv = invm(N % q, q);
             p.ninv_q = shoupq(p.ninv, q);
+            p.fp = q < (1ull << 42) ? 1 : 0;  // exact FP64 NTT arithmetic (hec_device.h)
+            p.qd = (double)q;
+            p.qinv = 1.0 / (double)q;
+            p.ninv_d = (double)p.ninv;
             c.hprimes.push_back(p);
             const u64 root = minimal_root(2 * N, q), iroot = invm(root, q);
             u64 pw = 1, ipw = 1;
@@ -588,10 +599,22 @@ int hec_context_create(uint64_t N, const uint64_t *mod, uint64_t K, int device, 
                         twb[dst] = tw[src];
                         itwb[dst] = itw[src];
                     }
+        auto to_d = [](const std::vector<ulonglong2> &v) {
+            std::vector<double> r(v.size());
+            for (std::size_t k = 0; k < v.size(); ++k) r[k] = (double)v[k].x;  // exact when q < 2^42
+            return r;
+        };
+        const std::vector<double> twf = to_d(tw), itwf = to_d(itw), twbf = to_d(twb), itwbf = to_d(itwb);
+        for (auto [dst, src] : {std::pair{&c.twf, &twf}, std::pair{&c.itwf, &itwf}, std::pair{&c.twbf, &twbf},
+                                std::pair{&c.itwbf, &itwbf}}) {
+            HEC_HIP(hipMalloc(dst, K * N * sizeof(double)));
+            HEC_HIP(hipMemcpy(*dst, src->data(), K * N * sizeof(double), hipMemcpyHostToDevice));
+        }
         HEC_HIP(hipMalloc(&c.twb, K * N * sizeof(ulonglong2)));
         HEC_HIP(hipMalloc(&c.itwb, K * N * sizeof(ulonglong2)));
         HEC_HIP(hipMemcpy(c.twb, twb.data(), K * N * sizeof(ulonglong2), hipMemcpyHostToDevice));
         HEC_HIP(hipMemcpy(c.itwb, itwb.data(), K * N * sizeof(ulonglong2), hipMemcpyHostToDevice));
+        HEC_HIP(hipMalloc(&c.imap, (HEC_MAXL + 2) * sizeof(int)));
         HEC_HIP(hipMalloc(&c.primes, K * sizeof(DevPrime)));
         HEC_HIP(hipMemcpy(c.primes, c.hprimes.data(), K * sizeof(DevPrime), hipMemcpyHostToDevice));
         HEC_HIP(hipMalloc(&c.tw, K * N * sizeof(ulonglong2)));
@@ -628,10 +651,12 @@ int hec_context_destroy(hec_context *ctx)
         (void)hipStreamSynchronize(c.stream);
         c.ws.release();
         (void)hipFree(c.primes);
+        (void)hipFree(c.imap);
         (void)hipFree(c.tw);
         (void)hipFree(c.itw);
         (void)hipFree(c.twb);
         (void)hipFree(c.itwb);
+        for (double *p : {c.twf, c.itwf, c.twbf, c.itwbf}) (void)hipFree(p);
         if (c.own_stream) (void)hipStreamDestroy(c.stream);
         delete ctx;
     });

@@ -53,11 +53,15 @@ struct Ctx {
     ulonglong2 *itw = nullptr;      // device [K][N] inverse twiddles psi^-bitrev(idx)
     ulonglong2 *twb = nullptr;      // device [K][N] pass-B layout of tw: [s][i][chunk] (see hec_kernels.hip)
     ulonglong2 *itwb = nullptr;     // same for itw
+    double *twf = nullptr, *itwf = nullptr, *twbf = nullptr, *itwbf = nullptr;  // FP64 twins (q < 2^42)
+    int *imap = nullptr;                    // device scratch: target-prime order for fused kernels
+    std::vector<int> imap_host = std::vector<int>(HEC_MAXL + 2);
     int logR = 0;                   // pass split N = R x C, R = 2^ceil(logN/2)
     Workspace ws;
     // host-side constants
     std::vector<u64> p_inv, p_inv_q, p_half_mod;            // key switch mod-down (per data prime)
     std::vector<std::vector<u64>> ql_inv, ql_inv_q, ql_half_mod;  // rescale at level l (drop prime l-1)
+    bool fused_modup_mac = false;  // HEC_FUSED_MODUP_MAC=1 selects the fused mod-up/MAC kernels
     // profiling
     bool prof = false;
     struct ProfRec { double ms = 0; uint64_t n = 0; };
@@ -78,6 +82,8 @@ void ntt_strided(Ctx &c, bool inverse, const u64 *src, u64 ps_src, u64 *dst, u64
 // Key-switch phases (B targets at level l; see hec_engine.hip for the dataflow)
 void ks_modup(Ctx &c, const u64 *D, u64 *E, int B, int l);
 void ks_mac(Ctx &c, PolyArr T, const u64 *E, const u64 *key, u64 *ACC, int B, int l);
+// fused: pass A of the mod-up NTTs, then (pass B + key MAC) per target prime -> ACC[b][k][I]
+void ks_modup_mac(Ctx &c, const u64 *D, u64 *E, PolyArr T, const u64 *key, u64 *ACC, int B, int l);
 // divide-and-round by `last_idx` prime: Y = coefficient-form last limb per (b,k) (address Y + b*ysb + k*ysk),
 // X / IN / OUT addressed (b,k,i), nk polys per batch entry, nl output limbs.
 //   OUT = IN + (X - NTT(corr)) * inv   (IN optional; inv = last^-1 mod q_i)

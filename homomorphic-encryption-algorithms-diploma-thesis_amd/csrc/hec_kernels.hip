@@ -158,15 +158,24 @@ struct DivRoundIO_B {
 };
 
 // =============================================================================== NTT core ==
+// Twiddle tables per prime: integer {w, w_shoup} pairs (60-bit primes) and integer-valued doubles
+// (primes < 2^42, FP64 arithmetic), each in SEAL order for pass A and re-laid for pass B.
+struct TwTables {
+    const ulonglong2 *a, *b;  // integer: pass A (SEAL order), pass B ([s][i][chunk])
+    const double *fa, *fb;    // FP64 twins
+};
+
 // One round: stages [S0, S1) of a P = 2^LOGP point sub-transform.  Thread `ts` of its segment owns
-// 16 elements = 2^(4-D) groups of 2^D elements (D = S1 - S0).
-template <int LOGP, int RND, bool INV, class AddrF, class TwF>
+// 16 elements = 2^(4-D) groups of 2^D elements (D = S1 - S0).  FP selects the arithmetic: the LDS
+// words then hold the bits of integer-valued doubles.
+template <int LOGP, int RND, bool INV, bool FP, class AddrF, class TwF>
 __device__ __forceinline__ void ntt_round(u64 *lds, const AddrF &addr, int ts, const TwF &twidx, const ulonglong2 *tw,
-                                          u64 q, u64 two_q)
+                                          const double *twf, const DevPrime &pr)
 {
     constexpr int S0 = RND * 4;
     constexpr int S1 = (S0 + 4 < LOGP) ? S0 + 4 : LOGP;
     constexpr int D = S1 - S0, G = 1 << (4 - D), NQ = 1 << D;
+    const u64 q = pr.q, two_q = 2 * q;
 #pragma unroll
     for (int gi = 0; gi < G; ++gi) {
         const int g = ts * G + gi;
@@ -176,28 +185,25 @@ __device__ __forceinline__ void ntt_round(u64 *lds, const AddrF &addr, int ts, c
         u64 v[NQ];
 #pragma unroll
         for (int a = 0; a < NQ; ++a) v[a] = lds[addr(xb | (a << (LOGP - S1)))];
-        if constexpr (!INV) {
 #pragma unroll
-            for (int s = S0; s < S1; ++s) {
-                const int bit = 1 << (S1 - s - 1);
+        for (int st = 0; st < D; ++st) {
+            const int s = INV ? S1 - 1 - st : S0 + st;
+            const int bit = 1 << (S1 - s - 1);
 #pragma unroll
-                for (int a = 0; a < NQ; ++a) {
-                    if (a & bit) continue;
-                    const int xu = xb | (a << (LOGP - S1));
-                    const ulonglong2 w = tw[twidx(s, xu >> (LOGP - s))];
-                    ct_bfly(v[a], v[a | bit], w.x, w.y, q, two_q);
-                }
-            }
-        } else {
-#pragma unroll
-            for (int s = S1 - 1; s >= S0; --s) {
-                const int bit = 1 << (S1 - s - 1);
-#pragma unroll
-                for (int a = 0; a < NQ; ++a) {
-                    if (a & bit) continue;
-                    const int xu = xb | (a << (LOGP - S1));
-                    const ulonglong2 w = tw[twidx(s, xu >> (LOGP - s))];
-                    gs_bfly(v[a], v[a | bit], w.x, w.y, q, two_q);
+            for (int a = 0; a < NQ; ++a) {
+                if (a & bit) continue;
+                const int xu = xb | (a << (LOGP - S1));
+                const u64 ti = twidx(s, xu >> (LOGP - s));
+                if constexpr (FP) {
+                    double X = __longlong_as_double((long long)v[a]), Y = __longlong_as_double((long long)v[a | bit]);
+                    if constexpr (!INV) ct_bfly_fp(X, Y, twf[ti], pr.qd, pr.qinv);
+                    else gs_bfly_fp(X, Y, twf[ti], pr.qd, pr.qinv);
+                    v[a] = (u64)__double_as_longlong(X);
+                    v[a | bit] = (u64)__double_as_longlong(Y);
+                } else {
+                    const ulonglong2 w = tw[ti];
+                    if constexpr (!INV) ct_bfly(v[a], v[a | bit], w.x, w.y, q, two_q);
+                    else gs_bfly(v[a], v[a | bit], w.x, w.y, q, two_q);
                 }
             }
         }
@@ -206,31 +212,29 @@ __device__ __forceinline__ void ntt_round(u64 *lds, const AddrF &addr, int ts, c
     }
 }
 
-template <int LOGP, int NSEG, bool INV, bool PASS_A, bool FINAL, class IO>
-__global__ void __launch_bounds__(NSEG *(1 << LOGP) / 16)
-    k_ntt(const IO io, const ulonglong2 *__restrict__ twt, const DevPrime *__restrict__ primes, int logN)
+template <int LOGP, int NSEG, bool INV, bool PASS_A, bool FINAL, bool FP, class Bound>
+__device__ __forceinline__ void ntt_pass_body(u64 *lds, const Bound &bio, const DevPrime &pr, const TwTables &tt,
+                                              int logN)
 {
     constexpr int P = 1 << LOGP, TPS = P / 16, THREADS = NSEG * TPS;
     constexpr int LD = PASS_A ? (NSEG + 1) : (P + 1);
-    __shared__ u64 lds[PASS_A ? P * (NSEG + 1) : NSEG * (P + 1)];
-    static_assert(LOGP >= 5 && LOGP <= 8, "two rounds of 4 stages");
-
-    const auto bio = io.bind(blockIdx.y);
-    const DevPrime pr = primes[bio.prime];
+    constexpr bool FIRST = !FINAL;  // forward: A then B; inverse: B then A
+    (void)TPS;
     const u64 q = pr.q, two_q = 2 * q;
-    const ulonglong2 *tw = twt + ((u64)bio.prime << logN);
     const int seg0 = blockIdx.x * NSEG;
     const int lc = logN - LOGP;  // pass A: log2(#columns)
+    const ulonglong2 *tw = (PASS_A ? tt.a : tt.b) + ((u64)bio.prime << logN);
+    const double *twf = (PASS_A ? tt.fa : tt.fb) + ((u64)bio.prime << logN);
 
 #pragma unroll 4
     for (int li = threadIdx.x; li < P * NSEG; li += THREADS) {
-        if constexpr (PASS_A) {
-            const int x = li / NSEG, sg = li % NSEG;
-            lds[x * LD + sg] = bio.load(((u64)x << lc) + seg0 + sg);
-        } else {
-            const int sg = li / P, x = li % P;
-            lds[sg * LD + x] = bio.load(((u64)(seg0 + sg) << LOGP) + x);
-        }
+        int x, sg;
+        u64 g;
+        if constexpr (PASS_A) { x = li / NSEG; sg = li % NSEG; g = ((u64)x << lc) + seg0 + sg; }
+        else { sg = li / P; x = li % P; g = ((u64)(seg0 + sg) << LOGP) + x; }
+        u64 v = bio.load(g);
+        if constexpr (FP && FIRST) v = (u64)__double_as_longlong(u2d(v));  // integer input -> double bits
+        lds[PASS_A ? x * LD + sg : sg * LD + x] = v;
     }
     __syncthreads();
 
@@ -239,20 +243,20 @@ __global__ void __launch_bounds__(NSEG *(1 << LOGP) / 16)
     // pass A: SEAL table index 2^s + i (shared by all columns: broadcast reads).
     // pass B: the per-chunk index (R + r) 2^s + i is served from the re-laid table
     //         twb[s][i][r] = tw[(R + r) 2^s + i] at R (2^s - 1) + i R + r, so lanes (consecutive
-    //         chunks r) read consecutive 16-B entries.
+    //         chunks r) read consecutive entries.
     const u64 R = 1ull << (logN - LOGP), chunk = (u64)(seg0 + sg);
     auto twidx = [=](int s, int i) -> u64 {
         if constexpr (PASS_A) return (1ull << s) + (u64)i;
         else return R * ((1ull << s) - 1) + (u64)i * R + chunk;
     };
     if constexpr (!INV) {
-        ntt_round<LOGP, 0, false>(lds, addr, ts, twidx, tw, q, two_q);
+        ntt_round<LOGP, 0, false, FP>(lds, addr, ts, twidx, tw, twf, pr);
         __syncthreads();
-        ntt_round<LOGP, 1, false>(lds, addr, ts, twidx, tw, q, two_q);
+        ntt_round<LOGP, 1, false, FP>(lds, addr, ts, twidx, tw, twf, pr);
     } else {
-        ntt_round<LOGP, 1, true>(lds, addr, ts, twidx, tw, q, two_q);
+        ntt_round<LOGP, 1, true, FP>(lds, addr, ts, twidx, tw, twf, pr);
         __syncthreads();
-        ntt_round<LOGP, 0, true>(lds, addr, ts, twidx, tw, q, two_q);
+        ntt_round<LOGP, 0, true, FP>(lds, addr, ts, twidx, tw, twf, pr);
     }
     __syncthreads();
 
@@ -269,11 +273,29 @@ __global__ void __launch_bounds__(NSEG *(1 << LOGP) / 16)
             g = ((u64)(seg0 + s2) << LOGP) + x;
         }
         if constexpr (FINAL) {
-            if constexpr (!INV) v = csub(csub(v, two_q), q);
-            else v = shoup(v, pr.ninv, pr.ninv_q, q);
+            if constexpr (FP) {
+                double d = __longlong_as_double((long long)v);
+                if constexpr (INV) d = fp_mulmod(d, pr.ninv_d, pr.qd, pr.qinv);
+                v = fp_canon(d, pr.qd, pr.qinv);
+            } else {
+                if constexpr (!INV) v = csub(csub(v, two_q), q);
+                else v = shoup(v, pr.ninv, pr.ninv_q, q);
+            }
         }
         bio.store(g, v);
     }
+}
+
+template <int LOGP, int NSEG, bool INV, bool PASS_A, bool FINAL, class IO>
+__global__ void __launch_bounds__(NSEG *(1 << LOGP) / 16)
+    k_ntt(const IO io, TwTables tt, const DevPrime *__restrict__ primes, int logN)
+{
+    static_assert(LOGP >= 5 && LOGP <= 8, "two rounds of 4 stages");
+    __shared__ u64 lds[PASS_A ? (1 << LOGP) * (NSEG + 1) : NSEG * ((1 << LOGP) + 1)];
+    const auto bio = io.bind(blockIdx.y);
+    const DevPrime pr = primes[bio.prime];
+    if (pr.fp) ntt_pass_body<LOGP, NSEG, INV, PASS_A, FINAL, true>(lds, bio, pr, tt, logN);
+    else ntt_pass_body<LOGP, NSEG, INV, PASS_A, FINAL, false>(lds, bio, pr, tt, logN);
 }
 
 template <int LOGR, int LOGC, int NA, int NB, bool INV, class IO1, class IO2>
@@ -282,12 +304,13 @@ static void run_ntt2(Ctx &c, int njobs, const IO1 &first, const IO2 &second)
     constexpr int R = 1 << LOGR, C = 1 << LOGC;
     const dim3 gA(C / NA, njobs), gB(R / NB, njobs);
     constexpr int TA = NA * R / 16, TB = NB * C / 16;
+    const TwTables fwd{c.tw, c.twb, c.twf, c.twbf}, inv{c.itw, c.itwb, c.itwf, c.itwbf};
     if constexpr (!INV) {
-        k_ntt<LOGR, NA, false, true, false><<<gA, TA, 0, c.stream>>>(first, c.tw, c.primes, c.logN);
-        k_ntt<LOGC, NB, false, false, true><<<gB, TB, 0, c.stream>>>(second, c.twb, c.primes, c.logN);
+        k_ntt<LOGR, NA, false, true, false><<<gA, TA, 0, c.stream>>>(first, fwd, c.primes, c.logN);
+        k_ntt<LOGC, NB, false, false, true><<<gB, TB, 0, c.stream>>>(second, fwd, c.primes, c.logN);
     } else {
-        k_ntt<LOGC, NB, true, false, false><<<gB, TB, 0, c.stream>>>(first, c.itwb, c.primes, c.logN);
-        k_ntt<LOGR, NA, true, true, true><<<gA, TA, 0, c.stream>>>(second, c.itw, c.primes, c.logN);
+        k_ntt<LOGC, NB, true, false, false><<<gB, TB, 0, c.stream>>>(first, inv, c.primes, c.logN);
+        k_ntt<LOGR, NA, true, true, true><<<gA, TA, 0, c.stream>>>(second, inv, c.primes, c.logN);
     }
     HEC_HIP(hipGetLastError());
 }
@@ -349,6 +372,147 @@ void divide_round(Ctx &c, const u64 *Y, u64 ysb, u64 ysk, PolyArr X, PolyArr IN,
     b.primes = c.primes;
     for (int i = 0; i < nl; ++i) { b.inv[i] = inv[i]; b.inv_q[i] = inv_q[i]; }
     ntt_dispatch<false>(c, B * nk * nl, a, b);
+}
+
+// ====================================================================== fused mod-up B + MAC ==
+// Key-switch steps (2b)+(3) in one kernel: a block owns NSEG chunks (NSEG * C coefficients) of one
+// target prime I for one batch entry b and loops over the digits J: it finishes the NTT of digit J
+// (pass B stages, from the pass-A output E[b][I][J]; J == I reuses the NTT-form target T[b][I])
+// in LDS/registers and multiply-accumulates it with key[J][k][I] into per-thread accumulators, so
+// the NTT-form digits never go back to HBM.  FP primes (< 2^42) accumulate exact FP64 modular
+// products (|acc| <= 0.53 q l, canonicalised once), 60-bit primes fold each 128-bit product with one
+// Barrett reduction (64-bit accumulators keep the register footprint at 2 waves/SIMD).
+// Blocks of the same (I, chunk block) for different b land on the same XCD (grid x = chunk blocks,
+// a multiple of 8), so the key chunk they share is served from that XCD's L2.
+template <int LOGP, int NSEG, bool FP>
+__global__ void __launch_bounds__(NSEG *(1 << LOGP) / 16, 2)
+    k_modup_b_mac(PolyArr T, const u64 *__restrict__ E, const u64 *__restrict__ key, u64 *__restrict__ ACC,
+                  TwTables tt, const DevPrime *__restrict__ primes, const int *__restrict__ Imap, int logN, int l,
+                  int K)
+{
+    constexpr int P = 1 << LOGP, THREADS = NSEG * P / 16, LD = P + 1, EPT = 16;
+    __shared__ u64 lds[NSEG * (P + 1)];
+    const int I = Imap[blockIdx.y], b = blockIdx.z;
+    const int kI = I == l ? K - 1 : I;
+    const DevPrime pr = primes[kI];
+    const u64 N = 1ull << logN;
+    const int seg0 = blockIdx.x * NSEG;
+    const u64 base = (u64)seg0 << LOGP;  // first coefficient of the block (contiguous range)
+    const ulonglong2 *tw = tt.b + ((u64)kI << logN);
+    const double *twf = tt.fb + ((u64)kI << logN);
+    const int ts = threadIdx.x / NSEG, sg = threadIdx.x % NSEG;
+    auto addr = [sg](int x) { return sg * LD + x; };
+    const u64 R = 1ull << (logN - LOGP), chunk = (u64)(seg0 + sg);
+    auto twidx = [=](int s, int i) -> u64 { return R * ((1ull << s) - 1) + (u64)i * R + chunk; };
+
+    // accumulators: FP -> integer-valued doubles; int -> canonical u64 folded by Barrett per digit
+    u64 a0[EPT], a1[EPT];
+#pragma unroll
+    for (int e = 0; e < EPT; ++e) {
+        if constexpr (FP) a0[e] = a1[e] = (u64)__double_as_longlong(0.0);
+        else a0[e] = a1[e] = 0;
+    }
+    for (int J = 0; J < l; ++J) {
+        const u64 *src = (J == I) ? T.p + b * T.sb + (u64)J * N
+                                  : E + (((u64)((b * (l + 1) + I) * l + J)) << logN);
+        const bool ntt = (J != I);
+#pragma unroll 4
+        for (int li = threadIdx.x; li < P * NSEG; li += THREADS) {
+            u64 v = src[base + li];
+            if constexpr (FP) {
+                if (!ntt) v = (u64)__double_as_longlong(u2d(v));  // canonical integer target
+            }
+            lds[(li / P) * LD + (li % P)] = v;
+        }
+        __syncthreads();
+        if (ntt) {
+            ntt_round<LOGP, 0, false, FP>(lds, addr, ts, twidx, tw, twf, pr);
+            __syncthreads();
+            ntt_round<LOGP, 1, false, FP>(lds, addr, ts, twidx, tw, twf, pr);
+            __syncthreads();
+        }
+        const u64 *k0p = key + (((u64)(J * 2 + 0) * K + kI) << logN) + base;
+        const u64 *k1p = key + (((u64)(J * 2 + 1) * K + kI) << logN) + base;
+#pragma unroll
+        for (int e = 0; e < EPT; ++e) {
+            if ((e & 3) == 0) __builtin_amdgcn_sched_barrier(0);  // bound the loads in flight (VGPRs)
+            const int li = threadIdx.x + e * THREADS;
+            const u64 v = lds[(li / P) * LD + (li % P)];
+            const u64 k0 = k0p[li], k1 = k1p[li];
+            if constexpr (FP) {
+                const double dv = __longlong_as_double((long long)v);
+                a0[e] = (u64)__double_as_longlong(__longlong_as_double((long long)a0[e]) +
+                                                  fp_mulmod(dv, u2d(k0), pr.qd, pr.qinv));
+                a1[e] = (u64)__double_as_longlong(__longlong_as_double((long long)a1[e]) +
+                                                  fp_mulmod(dv, u2d(k1), pr.qd, pr.qinv));
+            } else {  // acc + v*k < 2^61 + 2^124: one Barrett keeps the accumulator canonical
+                U128 t0{a0[e], 0}, t1{a1[e], 0};
+                mac128(t0, v, k0);
+                mac128(t1, v, k1);
+                a0[e] = barrett128(t0.lo, t0.hi, pr.q, pr.r0, pr.r1);
+                a1[e] = barrett128(t1.lo, t1.hi, pr.q, pr.r0, pr.r1);
+            }
+        }
+        __syncthreads();
+    }
+    u64 *o0 = ACC + (((u64)((b * 2 + 0) * (l + 1) + I)) << logN) + base;
+    u64 *o1 = ACC + (((u64)((b * 2 + 1) * (l + 1) + I)) << logN) + base;
+#pragma unroll
+    for (int e = 0; e < EPT; ++e) {
+        const int li = threadIdx.x + e * THREADS;
+        if constexpr (FP) {
+            o0[li] = fp_canon(__longlong_as_double((long long)a0[e]), pr.qd, pr.qinv);
+            o1[li] = fp_canon(__longlong_as_double((long long)a1[e]), pr.qd, pr.qinv);
+        } else {
+            o0[li] = a0[e];
+            o1[li] = a1[e];
+        }
+    }
+}
+
+template <int LOGR, int LOGC, int NA, int NB>
+static void run_modup_fused(Ctx &c, const u64 *D, u64 *E, PolyArr T, const u64 *key, u64 *ACC, int B, int l)
+{
+    constexpr int R = 1 << LOGR, C = 1 << LOGC;
+    ModUpMap m{l, c.logN, (int)c.K - 1};
+    ModUpIO_A a{m, D, E, c.primes};
+    const TwTables fwd{c.tw, c.twb, c.twf, c.twbf};
+    // (2a) pass A of every mod-up NTT (B * l * l jobs), output E[b][I][J] (lazy, pass-A domain)
+    k_ntt<LOGR, NA, false, true, false><<<dim3(C / NA, B * l * l), NA * R / 16, 0, c.stream>>>(a, fwd, c.primes, c.logN);
+    // (2b)+(3) fused, split by arithmetic path
+    int nfp = 0, nint = 0;
+    int *hm = c.imap_host.data();
+    for (int I = 0; I <= l; ++I) {
+        const int kI = I == l ? (int)c.K - 1 : I;
+        if (c.hprimes[kI].fp) hm[nfp++] = I;
+    }
+    for (int I = 0; I <= l; ++I) {
+        const int kI = I == l ? (int)c.K - 1 : I;
+        if (!c.hprimes[kI].fp) hm[nfp + nint++] = I;
+    }
+    HEC_HIP(hipMemcpyAsync(c.imap, hm, (l + 1) * sizeof(int), hipMemcpyHostToDevice, c.stream));
+    constexpr int TB = NB * C / 16;
+    if (nfp)
+        k_modup_b_mac<LOGC, NB, true><<<dim3(R / NB, nfp, B), TB, 0, c.stream>>>(T, E, key, ACC, fwd, c.primes, c.imap,
+                                                                                 c.logN, l, (int)c.K);
+    if (nint)
+        k_modup_b_mac<LOGC, NB, false><<<dim3(R / NB, nint, B), TB, 0, c.stream>>>(T, E, key, ACC, fwd, c.primes,
+                                                                                    c.imap + nfp, c.logN, l, (int)c.K);
+    HEC_HIP(hipGetLastError());
+}
+
+void ks_modup_mac(Ctx &c, const u64 *D, u64 *E, PolyArr T, const u64 *key, u64 *ACC, int B, int l)
+{
+    switch (c.logN) {
+    case 10: run_modup_fused<5, 5, 32, 32>(c, D, E, T, key, ACC, B, l); break;
+    case 11: run_modup_fused<6, 5, 32, 64>(c, D, E, T, key, ACC, B, l); break;
+    case 12: run_modup_fused<6, 6, 64, 64>(c, D, E, T, key, ACC, B, l); break;
+    case 13: run_modup_fused<7, 6, 32, 64>(c, D, E, T, key, ACC, B, l); break;
+    case 14: run_modup_fused<7, 7, 32, 32>(c, D, E, T, key, ACC, B, l); break;
+    case 15: run_modup_fused<8, 7, 16, 32>(c, D, E, T, key, ACC, B, l); break;
+    case 16: run_modup_fused<8, 8, 16, 16>(c, D, E, T, key, ACC, B, l); break;
+    default: throw std::invalid_argument("poly_modulus_degree must be 2^10 .. 2^16");
+    }
 }
 
 // =============================================================================== key MAC ===
