@@ -614,7 +614,7 @@ int hec_context_create(uint64_t N, const uint64_t *mod, uint64_t K, int device, 
         HEC_HIP(hipMalloc(&c.itwb, K * N * sizeof(ulonglong2)));
         HEC_HIP(hipMemcpy(c.twb, twb.data(), K * N * sizeof(ulonglong2), hipMemcpyHostToDevice));
         HEC_HIP(hipMemcpy(c.itwb, itwb.data(), K * N * sizeof(ulonglong2), hipMemcpyHostToDevice));
-        HEC_HIP(hipMalloc(&c.imap, (HEC_MAXL + 2) * sizeof(int)));
+        HEC_HIP(hipMalloc(&c.imap, 64 * (HEC_MAXL + 2) * sizeof(int)));
         HEC_HIP(hipMalloc(&c.primes, K * sizeof(DevPrime)));
         HEC_HIP(hipMemcpy(c.primes, c.hprimes.data(), K * sizeof(DevPrime), hipMemcpyHostToDevice));
         HEC_HIP(hipMalloc(&c.tw, K * N * sizeof(ulonglong2)));

@@ -54,7 +54,8 @@ struct Ctx {
     ulonglong2 *twb = nullptr;      // device [K][N] pass-B layout of tw: [s][i][chunk] (see hec_kernels.hip)
     ulonglong2 *itwb = nullptr;     // same for itw
     double *twf = nullptr, *itwf = nullptr, *twbf = nullptr, *itwbf = nullptr;  // FP64 twins (q < 2^42)
-    int *imap = nullptr;                    // device scratch: target-prime order for fused kernels
+    int *imap = nullptr;                    // device ring of 64 target-prime order tables (kernel args)
+    unsigned imap_slot = 0;
     std::vector<int> imap_host = std::vector<int>(HEC_MAXL + 2);
     int logR = 0;                   // pass split N = R x C, R = 2^ceil(logN/2)
     Workspace ws;

@@ -28,8 +28,10 @@ struct StridedIO {  // job -> (poly = job / nl, limb = job % nl); src/dst may al
         const u64 *s;
         u64 *d;
         int prime;
+        struct Pre {};
+        __device__ Pre pre(u64) const { return {}; }
         __device__ u64 load(u64 g) const { return s[g]; }
-        __device__ void store(u64 g, u64 v) const { d[g] = v; }
+        __device__ void store(u64 g, u64 v, Pre) const { d[g] = v; }
     };
     __device__ Bound bind(int job) const
     {
@@ -69,8 +71,10 @@ struct ModUpIO_A {  // load digit J (coefficient form, canonical mod q_J) reduce
         u64 *d;
         u64 q, r1;
         int prime;
+        struct Pre {};
+        __device__ Pre pre(u64) const { return {}; }
         __device__ u64 load(u64 g) const { return barrett64(s[g], q, r1); }
-        __device__ void store(u64 g, u64 v) const { d[g] = v; }
+        __device__ void store(u64 g, u64 v, Pre) const { d[g] = v; }
     };
     __device__ Bound bind(int job) const
     {
@@ -86,8 +90,10 @@ struct ModUpIO_B {
     struct Bound {
         u64 *p;
         int prime;
+        struct Pre {};
+        __device__ Pre pre(u64) const { return {}; }
         __device__ u64 load(u64 g) const { return p[g]; }
-        __device__ void store(u64 g, u64 v) const { p[g] = v; }
+        __device__ void store(u64 g, u64 v, Pre) const { p[g] = v; }
     };
     __device__ Bound bind(int job) const
     {
@@ -114,13 +120,15 @@ struct DivRoundIO_A {
         u64 *z;
         u64 last, half, q, r1, fix;
         int prime;
+        struct Pre {};
+        __device__ Pre pre(u64) const { return {}; }
         __device__ u64 load(u64 g) const
         {
             u64 v = y[g] + half;
             v = v >= last ? v - last : v;
             return barrett64(v, q, r1) + fix;
         }
-        __device__ void store(u64 g, u64 v) const { z[g] = v; }
+        __device__ void store(u64 g, u64 v, Pre) const { z[g] = v; }
     };
     __device__ Bound bind(int job) const
     {
@@ -139,11 +147,15 @@ struct DivRoundIO_B {
         u64 *out;
         u64 q, w, wq;
         int prime;
+        struct Pre {  // operands of the post-op, loaded before the butterfly rounds
+            u64 x, in;
+        };
+        __device__ Pre pre(u64 g) const { return Pre{x[g], in ? in[g] : 0}; }
         __device__ u64 load(u64 g) const { return z[g]; }
-        __device__ void store(u64 g, u64 v) const
+        __device__ void store(u64 g, u64 v, Pre p) const
         {
-            u64 r = shoup(x[g] + q - v, w, wq, q);
-            if (in) r = addmod(r, in[g], q);
+            u64 r = shoup(p.x + q - v, w, wq, q);
+            if (in) r = addmod(r, p.in, q);
             out[g] = r;
         }
     };
@@ -182,28 +194,39 @@ __device__ __forceinline__ void ntt_round(u64 *lds, const AddrF &addr, int ts, c
         const int lo = g & ((1 << (LOGP - S1)) - 1);
         const int hi = g >> (LOGP - S1);
         const int xb = (hi << (LOGP - S0)) | lo;
+        // the group's 2^D - 1 twiddles do not depend on data: issue their loads before the LDS
+        // reads so their latency overlaps.  Round-stage st uses index twidx(S0+st, hi 2^st + m),
+        // m = a >> (D - st) the top st bits of the element slot a.
+        double wf[FP ? NQ - 1 : 1];
+        ulonglong2 wi[FP ? 1 : NQ - 1];
+#pragma unroll
+        for (int st = 0; st < D; ++st)
+#pragma unroll
+            for (int m = 0; m < (1 << st); ++m) {
+                const u64 ti = twidx(S0 + st, (hi << st) | m);
+                if constexpr (FP) wf[(1 << st) - 1 + m] = twf[ti];
+                else wi[(1 << st) - 1 + m] = tw[ti];
+            }
         u64 v[NQ];
 #pragma unroll
         for (int a = 0; a < NQ; ++a) v[a] = lds[addr(xb | (a << (LOGP - S1)))];
 #pragma unroll
-        for (int st = 0; st < D; ++st) {
-            const int s = INV ? S1 - 1 - st : S0 + st;
-            const int bit = 1 << (S1 - s - 1);
+        for (int k = 0; k < D; ++k) {
+            const int st = INV ? D - 1 - k : k;
+            const int bit = 1 << (D - 1 - st);
 #pragma unroll
             for (int a = 0; a < NQ; ++a) {
                 if (a & bit) continue;
-                const int xu = xb | (a << (LOGP - S1));
-                const u64 ti = twidx(s, xu >> (LOGP - s));
+                const int wk = (1 << st) - 1 + (a >> (D - st));
                 if constexpr (FP) {
                     double X = __longlong_as_double((long long)v[a]), Y = __longlong_as_double((long long)v[a | bit]);
-                    if constexpr (!INV) ct_bfly_fp(X, Y, twf[ti], pr.qd, pr.qinv);
-                    else gs_bfly_fp(X, Y, twf[ti], pr.qd, pr.qinv);
+                    if constexpr (!INV) ct_bfly_fp(X, Y, wf[wk], pr.qd, pr.qinv);
+                    else gs_bfly_fp(X, Y, wf[wk], pr.qd, pr.qinv);
                     v[a] = (u64)__double_as_longlong(X);
                     v[a | bit] = (u64)__double_as_longlong(Y);
                 } else {
-                    const ulonglong2 w = tw[ti];
-                    if constexpr (!INV) ct_bfly(v[a], v[a | bit], w.x, w.y, q, two_q);
-                    else gs_bfly(v[a], v[a | bit], w.x, w.y, q, two_q);
+                    if constexpr (!INV) ct_bfly(v[a], v[a | bit], wi[wk].x, wi[wk].y, q, two_q);
+                    else gs_bfly(v[a], v[a | bit], wi[wk].x, wi[wk].y, q, two_q);
                 }
             }
         }
@@ -226,8 +249,9 @@ __device__ __forceinline__ void ntt_pass_body(u64 *lds, const Bound &bio, const 
     const ulonglong2 *tw = (PASS_A ? tt.a : tt.b) + ((u64)bio.prime << logN);
     const double *twf = (PASS_A ? tt.fa : tt.fb) + ((u64)bio.prime << logN);
 
-#pragma unroll 4
-    for (int li = threadIdx.x; li < P * NSEG; li += THREADS) {
+#pragma unroll
+    for (int it = 0; it < P * NSEG / THREADS; ++it) {
+        const int li = threadIdx.x + it * THREADS;
         int x, sg;
         u64 g;
         if constexpr (PASS_A) { x = li / NSEG; sg = li % NSEG; g = ((u64)x << lc) + seg0 + sg; }
@@ -238,6 +262,19 @@ __device__ __forceinline__ void ntt_pass_body(u64 *lds, const Bound &bio, const 
     }
     __syncthreads();
 
+    // post-op operands of this thread's output words: issue their loads now so they overlap the rounds
+    constexpr int ITS = P * NSEG / THREADS;
+    typename Bound::Pre pre[FINAL ? ITS : 1];
+    if constexpr (FINAL) {
+#pragma unroll
+        for (int it = 0; it < ITS; ++it) {
+            const int li = threadIdx.x + it * THREADS;
+            u64 g;
+            if constexpr (PASS_A) g = ((u64)(li / NSEG) << lc) + seg0 + li % NSEG;
+            else g = ((u64)(seg0 + li / P) << LOGP) + li % P;
+            pre[it] = bio.pre(g);
+        }
+    }
     const int ts = threadIdx.x / NSEG, sg = threadIdx.x % NSEG;
     auto addr = [sg](int x) { return PASS_A ? x * LD + sg : sg * LD + x; };
     // pass A: SEAL table index 2^s + i (shared by all columns: broadcast reads).
@@ -260,8 +297,9 @@ __device__ __forceinline__ void ntt_pass_body(u64 *lds, const Bound &bio, const 
     }
     __syncthreads();
 
-#pragma unroll 4
-    for (int li = threadIdx.x; li < P * NSEG; li += THREADS) {
+#pragma unroll
+    for (int it = 0; it < P * NSEG / THREADS; ++it) {
+        const int li = threadIdx.x + it * THREADS;
         u64 v, g;
         if constexpr (PASS_A) {
             const int x = li / NSEG, s2 = li % NSEG;
@@ -281,8 +319,10 @@ __device__ __forceinline__ void ntt_pass_body(u64 *lds, const Bound &bio, const 
                 if constexpr (!INV) v = csub(csub(v, two_q), q);
                 else v = shoup(v, pr.ninv, pr.ninv_q, q);
             }
+            bio.store(g, v, pre[it]);
+        } else {
+            bio.store(g, v, typename Bound::Pre{});
         }
-        bio.store(g, v);
     }
 }
 
@@ -490,14 +530,15 @@ static void run_modup_fused(Ctx &c, const u64 *D, u64 *E, PolyArr T, const u64 *
         const int kI = I == l ? (int)c.K - 1 : I;
         if (!c.hprimes[kI].fp) hm[nfp + nint++] = I;
     }
-    HEC_HIP(hipMemcpyAsync(c.imap, hm, (l + 1) * sizeof(int), hipMemcpyHostToDevice, c.stream));
+    int *dm = c.imap + (HEC_MAXL + 2) * (c.imap_slot++ % 64);
+    HEC_HIP(hipMemcpyAsync(dm, hm, (l + 1) * sizeof(int), hipMemcpyHostToDevice, c.stream));
     constexpr int TB = NB * C / 16;
     if (nfp)
-        k_modup_b_mac<LOGC, NB, true><<<dim3(R / NB, nfp, B), TB, 0, c.stream>>>(T, E, key, ACC, fwd, c.primes, c.imap,
+        k_modup_b_mac<LOGC, NB, true><<<dim3(R / NB, nfp, B), TB, 0, c.stream>>>(T, E, key, ACC, fwd, c.primes, dm,
                                                                                  c.logN, l, (int)c.K);
     if (nint)
         k_modup_b_mac<LOGC, NB, false><<<dim3(R / NB, nint, B), TB, 0, c.stream>>>(T, E, key, ACC, fwd, c.primes,
-                                                                                    c.imap + nfp, c.logN, l, (int)c.K);
+                                                                                    dm + nfp, c.logN, l, (int)c.K);
     HEC_HIP(hipGetLastError());
 }
 
@@ -520,13 +561,12 @@ void ks_modup_mac(Ctx &c, const u64 *D, u64 *E, PolyArr T, const u64 *key, u64 *
 // 128-bit lazy accumulation then one Barrett reduction (SEAL switch_key_inplace step 3).
 // A thread owns one coefficient for BT batch entries, so each key word is read once per BT targets.
 template <int BT>
-__global__ void __launch_bounds__(256)
-    k_ks_mac(PolyArr T, const u64 *__restrict__ E, const u64 *__restrict__ key, u64 *__restrict__ ACC, int B,
-             int l, int K, int logN, const DevPrime *__restrict__ primes)
+__device__ __forceinline__ void ks_mac_int(PolyArr T, const u64 *__restrict__ E, const u64 *__restrict__ key,
+                                           u64 *__restrict__ ACC, int B, int l, int K, int logN,
+                                           const DevPrime *__restrict__ primes, int I)
 {
     const u64 N = 1ull << logN;
     const u64 g = (u64)blockIdx.x * 256 + threadIdx.x;
-    const int I = blockIdx.y;
     const int b0 = blockIdx.z * BT;
     const int kI = I == l ? K - 1 : I;
     const DevPrime pr = primes[kI];
@@ -557,11 +597,80 @@ __global__ void __launch_bounds__(256)
     }
 }
 
+// FP64 variant for target primes < 2^42: each thread owns two adjacent coefficients (16-B loads),
+// products by fp_mulmod (exact, |r| <= 0.53 q), sums kept as integer-valued doubles (|acc| <= 0.53 q l).
+template <int BT>
+__device__ __forceinline__ void ks_mac_fp(PolyArr T, const u64 *__restrict__ E, const u64 *__restrict__ key,
+                                          u64 *__restrict__ ACC, int B, int l, int K, int logN,
+                                          const DevPrime *__restrict__ primes, int I)
+{
+    const u64 N = 1ull << logN;
+    if ((u64)blockIdx.x * 512 >= N) return;  // FP blocks own two coefficients per thread
+    const u64 g = 2 * ((u64)blockIdx.x * 256 + threadIdx.x);
+    const int b0 = blockIdx.z * BT;
+    const int kI = I == l ? K - 1 : I;
+    const DevPrime pr = primes[kI];
+    double a0[BT][2], a1[BT][2];
+#pragma unroll
+    for (int t = 0; t < BT; ++t) a0[t][0] = a0[t][1] = a1[t][0] = a1[t][1] = 0.0;
+    for (int J = 0; J < l; ++J) {
+        const ulonglong2 k0 = *(const ulonglong2 *)(key + ((u64)(J * 2 + 0) * K + kI) * N + g);
+        const ulonglong2 k1 = *(const ulonglong2 *)(key + ((u64)(J * 2 + 1) * K + kI) * N + g);
+        const double k00 = u2d(k0.x), k01 = u2d(k0.y), k10 = u2d(k1.x), k11 = u2d(k1.y);
+#pragma unroll
+        for (int t = 0; t < BT; ++t) {
+            const int b = b0 + t;
+            if (b < B) {
+                const ulonglong2 e = (I == J) ? *(const ulonglong2 *)(T.p + b * T.sb + (u64)J * N + g)
+                                              : *(const ulonglong2 *)(E + (((u64)((b * (l + 1) + I) * l + J)) << logN) + g);
+                const double e0 = u2d(e.x), e1 = u2d(e.y);
+                a0[t][0] += fp_mulmod(e0, k00, pr.qd, pr.qinv);
+                a0[t][1] += fp_mulmod(e1, k01, pr.qd, pr.qinv);
+                a1[t][0] += fp_mulmod(e0, k10, pr.qd, pr.qinv);
+                a1[t][1] += fp_mulmod(e1, k11, pr.qd, pr.qinv);
+            }
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < BT; ++t) {
+        const int b = b0 + t;
+        if (b < B) {
+            *(ulonglong2 *)(ACC + (((u64)((b * 2 + 0) * (l + 1) + I)) << logN) + g) =
+                ulonglong2{fp_canon(a0[t][0], pr.qd, pr.qinv), fp_canon(a0[t][1], pr.qd, pr.qinv)};
+            *(ulonglong2 *)(ACC + (((u64)((b * 2 + 1) * (l + 1) + I)) << logN) + g) =
+                ulonglong2{fp_canon(a1[t][0], pr.qd, pr.qinv), fp_canon(a1[t][1], pr.qd, pr.qinv)};
+        }
+    }
+}
+
+// one launch: blockIdx.y < nfp -> FP64 target primes, the rest integer primes (run concurrently)
+template <int BT>
+__global__ void __launch_bounds__(256)
+    k_ks_mac(PolyArr T, const u64 *__restrict__ E, const u64 *__restrict__ key, u64 *__restrict__ ACC, int B, int l,
+             int K, int logN, const DevPrime *__restrict__ primes, const int *__restrict__ Imap, int nfp)
+{
+    const int I = Imap[blockIdx.y];
+    if ((int)blockIdx.y < nfp) ks_mac_fp<BT>(T, E, key, ACC, B, l, K, logN, primes, I);
+    else ks_mac_int<BT>(T, E, key, ACC, B, l, K, logN, primes, I);
+}
+
 void ks_mac(Ctx &c, PolyArr T, const u64 *E, const u64 *key, u64 *ACC, int B, int l)
 {
     constexpr int BT = 8;
-    const dim3 grid((unsigned)(c.N / 256), l + 1, (B + BT - 1) / BT);
-    k_ks_mac<BT><<<grid, 256, 0, c.stream>>>(T, E, key, ACC, B, l, (int)c.K, c.logN, c.primes);
+    int nfp = 0, nint = 0;
+    int *hm = c.imap_host.data();
+    for (int pass = 0; pass < 2; ++pass)
+        for (int I = 0; I <= l; ++I) {
+            const int kI = I == l ? (int)c.K - 1 : I;
+            const bool fp = c.hprimes[kI].fp != 0;
+            if (pass == 0 && fp) hm[nfp++] = I;
+            if (pass == 1 && !fp) hm[nfp + nint++] = I;
+        }
+    int *dm = c.imap + (HEC_MAXL + 2) * (c.imap_slot++ % 64);  // per-call slot: no host/device race
+    HEC_HIP(hipMemcpyAsync(dm, hm, (l + 1) * sizeof(int), hipMemcpyHostToDevice, c.stream));
+    const unsigned bz = (B + BT - 1) / BT;
+    k_ks_mac<BT><<<dim3((unsigned)(c.N / 256), nfp + nint, bz), 256, 0, c.stream>>>(T, E, key, ACC, B, l, (int)c.K,
+                                                                                   c.logN, c.primes, dm, nfp);
     HEC_HIP(hipGetLastError());
 }
 
