@@ -1,0 +1,171 @@
+// he_demo — the reference's `demo matrix_operations batched_matmul_ckks` flow
+// (src/demos/matrix_operations.cpp:1042-1175) written against the hecdna drop-in headers:
+// identical he::operators / he::linalg code, with seal:: types replaced by hecdna:: types.
+// Key generation / encryption / decryption stay with the caller (SEAL in a real deployment); this
+// program reads SEAL-layout keys and ciphertexts from a file and writes the result ciphertexts.
+//
+// usage: he_demo <mode> <in.bin> <out.bin>
+//   mode = batched_diag   (COL_OR_DIAG = 1: A diag-batched x B col-batched)
+//          batched_col    (COL_OR_DIAG = 0: A col-batched x A^T)
+//          ops            (operator expressions: ((eval%gk%c0) << 5) * c1, relin, rescale, + c2 ...)
+//          matrix         (Matrix 2x2 elementwise-ciphertext matmul, he_linalg.cpp:202-236)
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <iostream>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "he_linalg.h"
+#include "he_operators.h"
+
+using namespace he::operators;
+using namespace he::linalg;
+using hecdna::Ciphertext;
+
+namespace {
+struct Input {
+    std::uint64_t N = 0;
+    std::vector<std::uint64_t> moduli;
+    struct Ct { std::uint64_t size, level; double scale; std::vector<std::uint64_t> data; };
+    std::vector<Ct> cts;
+    std::vector<std::uint64_t> rk;
+    std::map<std::uint32_t, std::vector<std::uint64_t>> gk;
+};
+
+template <class T>
+void rd(std::ifstream &f, T *p, std::size_t n)
+{
+    f.read(reinterpret_cast<char *>(p), sizeof(T) * n);
+    if (!f) throw std::runtime_error("truncated input");
+}
+
+Input read_input(const char *path)
+{
+    std::ifstream f(path, std::ios::binary);
+    char magic[8];
+    rd(f, magic, 8);
+    if (std::memcmp(magic, "HECDNA01", 8)) throw std::runtime_error("bad magic");
+    Input in;
+    std::uint64_t K, n;
+    rd(f, &in.N, 1);
+    rd(f, &K, 1);
+    in.moduli.resize(K);
+    rd(f, in.moduli.data(), K);
+    rd(f, &n, 1);
+    for (std::uint64_t i = 0; i < n; ++i) {
+        Input::Ct c;
+        rd(f, &c.size, 1);
+        rd(f, &c.level, 1);
+        rd(f, &c.scale, 1);
+        c.data.resize(c.size * c.level * in.N);
+        rd(f, c.data.data(), c.data.size());
+        in.cts.push_back(std::move(c));
+    }
+    const std::size_t kw = (K - 1) * 2 * K * in.N;
+    std::uint64_t has_rk, ngk;
+    rd(f, &has_rk, 1);
+    if (has_rk) {
+        in.rk.resize(kw);
+        rd(f, in.rk.data(), kw);
+    }
+    rd(f, &ngk, 1);
+    for (std::uint64_t i = 0; i < ngk; ++i) {
+        std::uint64_t elt;
+        rd(f, &elt, 1);
+        auto &v = in.gk[(std::uint32_t)elt];
+        v.resize(kw);
+        rd(f, v.data(), kw);
+    }
+    return in;
+}
+
+void write_output(const char *path, const std::vector<const Ciphertext *> &cts)
+{
+    std::ofstream f(path, std::ios::binary);
+    const std::uint64_t n = cts.size();
+    f.write(reinterpret_cast<const char *>(&n), 8);
+    for (const Ciphertext *c : cts) {
+        const std::uint64_t s = c->size(), l = c->level();
+        const double sc = c->scale();
+        const auto d = c->download();
+        f.write(reinterpret_cast<const char *>(&s), 8);
+        f.write(reinterpret_cast<const char *>(&l), 8);
+        f.write(reinterpret_cast<const char *>(&sc), 8);
+        f.write(reinterpret_cast<const char *>(d.data()), d.size() * 8);
+    }
+}
+}  // namespace
+
+int main(int argc, char **argv)
+{
+    if (argc != 4) {
+        std::cout << "usage: he_demo <batched_diag|batched_col|ops|matrix> <in.bin> <out.bin>\n";
+        return 1;
+    }
+    const std::string mode = argv[1];
+    const Input in = read_input(argv[2]);
+
+    hecdna::Context ctx(in.N, in.moduli);  // SEALContext ctx(parms)
+    hecdna::Evaluator eval(ctx);           // Evaluator eval(ctx)
+    hecdna::RelinKeys rk;
+    if (!in.rk.empty()) rk = hecdna::RelinKeys(ctx, in.rk.data());
+    hecdna::GaloisKeys gk(ctx);
+    for (const auto &[elt, data] : in.gk) gk.add(elt, data.data());
+    std::vector<Ciphertext> cts;
+    for (const auto &c : in.cts) {
+        cts.emplace_back(ctx);
+        cts.back().upload(c.data.data(), c.size, c.level, c.scale);
+    }
+
+    std::vector<const Ciphertext *> outs;
+    std::vector<Ciphertext> keep;
+    if (mode == "batched_diag" || mode == "batched_col") {
+        // matrix_operations.cpp:1112-1141 — the same code the reference runs over seal:: types
+        const std::size_t dim = cts.size();
+        std::vector<BatchedVector> mat1_cols_bvec;
+        mat1_cols_bvec.reserve(dim);
+        for (std::size_t i = 0; i < dim; ++i) mat1_cols_bvec.emplace_back(dim, cts[i]);
+        std::vector<BatchedVector> res;
+        if (mode == "batched_diag") {
+            BatchedMatrix mat1_bmat(BatchedMatrix::BatchingType::diag, mat1_cols_bvec);
+            BatchedMatrix mat2_bmat(BatchedMatrix::BatchingType::col, std::move(mat1_cols_bvec));
+            BatchedMatrix mat3_bmat = mat1_bmat.matmul(eval, rk, gk, mat2_bmat);
+            res = mat3_bmat.get_bvecs();
+        } else {
+            BatchedMatrix mat1_bmat(BatchedMatrix::BatchingType::col, std::move(mat1_cols_bvec));
+            BatchedMatrix mat2_bmat = mat1_bmat;
+            mat2_bmat.transp();
+            BatchedMatrix mat3_bmat = mat1_bmat.matmul(eval, rk, gk, mat2_bmat);
+            res = mat3_bmat.get_bvecs();
+        }
+        for (auto &b : res) keep.push_back(b.get_bvec());
+    } else if (mode == "ops") {
+        // operator surface of he_operators.h on three ciphertexts
+        Ciphertext r = eval % gk % cts[0] << 5;  // rotate left
+        r *= eval % cts[1];                       // ct x ct
+        r &= eval % rk;                           // relinearize
+        r ^= eval;                                // rescale
+        Ciphertext s = eval % gk % cts[2] >> 3;   // rotate right (out of place)
+        s |= eval;                                // mod switch to next
+        keep.push_back(r);
+        keep.push_back(s);
+        Ciphertext t = eval % cts[0] - cts[1];
+        t -= eval;                                // negate
+        keep.push_back(t);
+    } else if (mode == "matrix") {
+        // Matrix::matmul on 2x2 element-wise ciphertext matrices (column-major elems)
+        Matrix A(2, 2, std::vector<Ciphertext>(cts.begin(), cts.begin() + 4));
+        Matrix B(2, 2, std::vector<Ciphertext>(cts.begin() + 4, cts.begin() + 8));
+        Matrix C = A.matmul(eval, rk, B);
+        for (const auto &c : C.get_elems()) keep.push_back(c);
+    } else {
+        std::cout << "No such demo for " << mode << ".\n";
+        return 1;
+    }
+    for (auto &c : keep) outs.push_back(&c);
+    write_output(argv[3], outs);
+    std::cout << "he_demo " << mode << ": wrote " << outs.size() << " ciphertexts\n";
+    return 0;
+}

@@ -1,0 +1,271 @@
+// hecdna C++ host API: RAII value types over the C-ABI (include/hecdna.h) that stand in for the
+// seal:: types the reference's he_operators / he_linalg layer is written against
+// (reference include/he_operators.h:3, include/he_linalg.h:4 include "seal/seal.h").
+//
+//   seal::SEALContext + EncryptionParameters  -> hecdna::Context
+//   seal::Evaluator                           -> hecdna::Evaluator  (same member names, const)
+//   seal::Ciphertext / Plaintext              -> hecdna::Ciphertext / Plaintext (value semantics,
+//                                                copy = deep device copy, like SEAL)
+//   seal::RelinKeys / GaloisKeys              -> hecdna::RelinKeys / GaloisKeys
+//   seal::CoeffModulus::Create                -> hecdna::CoeffModulus::Create
+//
+// Errors are rethrown with SEAL's exception types and messages (std::invalid_argument,
+// std::logic_error); HIP failures as std::runtime_error.  Objects live on the context's GPU.
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "hecdna.h"
+
+namespace hecdna {
+
+inline void check(int rc)
+{
+    if (rc == HEC_OK) return;
+    const std::string msg = hec_last_error();
+    if (rc == HEC_EINVAL) throw std::invalid_argument(msg);
+    if (rc == HEC_ELOGIC) throw std::logic_error(msg);
+    throw std::runtime_error(msg);
+}
+
+struct CoeffModulus {
+    static std::vector<std::uint64_t> Create(std::size_t poly_modulus_degree, const std::vector<int> &bit_sizes)
+    {
+        std::vector<std::uint64_t> out(bit_sizes.size());
+        check(hec_create_coeff_modulus(poly_modulus_degree, bit_sizes.data(), bit_sizes.size(), out.data()));
+        return out;
+    }
+};
+
+class Context {
+public:
+    Context(std::size_t poly_modulus_degree, const std::vector<std::uint64_t> &coeff_modulus, int device = 0)
+    {
+        hec_context *c = nullptr;
+        check(hec_context_create(poly_modulus_degree, coeff_modulus.data(), coeff_modulus.size(), device, &c));
+        h_.reset(c, [](hec_context *p) { hec_context_destroy(p); });
+        moduli_ = coeff_modulus;
+    }
+    hec_context *get() const { return h_.get(); }
+    std::size_t poly_modulus_degree() const { return hec_context_poly_degree(h_.get()); }
+    std::size_t slot_count() const { return poly_modulus_degree() / 2; }
+    const std::vector<std::uint64_t> &coeff_modulus() const { return moduli_; }
+    std::uint32_t galois_elt_from_step(int step) const
+    {
+        const std::uint32_t e = hec_galois_elt_from_step(h_.get(), step);
+        if (!e) check(HEC_EINVAL);
+        return e;
+    }
+    std::vector<std::uint32_t> default_galois_elts() const
+    {
+        std::vector<std::uint32_t> v(hec_default_galois_elts(h_.get(), nullptr));
+        hec_default_galois_elts(h_.get(), v.data());
+        return v;
+    }
+    void set_stream(void *hip_stream) const { check(hec_context_set_stream(h_.get(), hip_stream)); }
+    void synchronize() const { check(hec_context_synchronize(h_.get())); }
+
+private:
+    std::shared_ptr<hec_context> h_;
+    std::vector<std::uint64_t> moduli_;
+};
+
+class Ciphertext {
+public:
+    Ciphertext() = default;
+    explicit Ciphertext(const Context &ctx) : ctx_(&ctx) { create(); }
+    Ciphertext(const Ciphertext &o) : ctx_(o.ctx_)
+    {
+        if (o.h_) {
+            create();
+            check(hec_ciphertext_copy(h_, o.h_));
+        }
+    }
+    Ciphertext(Ciphertext &&o) noexcept : ctx_(o.ctx_), h_(o.h_) { o.h_ = nullptr; }
+    Ciphertext &operator=(const Ciphertext &o)
+    {
+        if (this == &o) return *this;
+        if (!o.h_) { reset(); ctx_ = o.ctx_; return *this; }
+        if (!h_ || ctx_ != o.ctx_) { reset(); ctx_ = o.ctx_; create(); }
+        check(hec_ciphertext_copy(h_, o.h_));
+        return *this;
+    }
+    Ciphertext &operator=(Ciphertext &&o) noexcept
+    {
+        if (this != &o) {
+            reset();
+            ctx_ = o.ctx_;
+            h_ = o.h_;
+            o.h_ = nullptr;
+        }
+        return *this;
+    }
+    ~Ciphertext() { reset(); }
+
+    // SEAL layout host buffer u64[size][level][N] (e.g. seal::Ciphertext::data())
+    void upload(const std::uint64_t *data, std::size_t size, std::size_t level, double scale)
+    {
+        ensure();
+        check(hec_ciphertext_upload(h_, data, size, level, scale));
+    }
+    std::vector<std::uint64_t> download() const
+    {
+        std::vector<std::uint64_t> v(size() * level() * ctx_->poly_modulus_degree());
+        check(hec_ciphertext_download(h_, v.data()));
+        return v;
+    }
+    std::size_t size() const { return info().size; }
+    std::size_t level() const { return info().level; }
+    double scale() const { return info().scale; }
+    const Context &context() const { return *ctx_; }
+    hec_ciphertext *get() const { return h_; }
+    // bind a default-constructed ciphertext to a context (used by out-of-place operations)
+    void bind(const Context &ctx)
+    {
+        if (!h_ || ctx_ != &ctx) { reset(); ctx_ = &ctx; create(); }
+    }
+
+private:
+    struct Info { std::size_t size, level; double scale; };
+    Info info() const
+    {
+        if (!h_) return {0, 0, 1.0};
+        std::uint64_t s = 0, l = 0;
+        double sc = 0;
+        check(hec_ciphertext_info(h_, &s, &l, &sc));
+        return {s, l, sc};
+    }
+    void create()
+    {
+        hec_ciphertext *c = nullptr;
+        check(hec_ciphertext_create(ctx_->get(), &c));
+        h_ = c;
+    }
+    void ensure()
+    {
+        if (!ctx_) throw std::logic_error("ciphertext has no context");
+        if (!h_) create();
+    }
+    void reset()
+    {
+        if (h_) hec_ciphertext_destroy(h_);
+        h_ = nullptr;
+    }
+    const Context *ctx_ = nullptr;
+    hec_ciphertext *h_ = nullptr;
+};
+
+class Plaintext {
+public:
+    Plaintext() = default;
+    Plaintext(const Context &ctx, const std::uint64_t *data, std::size_t level, double scale)
+    {
+        hec_plaintext *p = nullptr;
+        check(hec_plaintext_create(ctx.get(), &p));
+        h_.reset(p, [](hec_plaintext *x) { hec_plaintext_destroy(x); });
+        check(hec_plaintext_upload(p, data, level, scale));
+    }
+    hec_plaintext *get() const { return h_.get(); }
+
+private:
+    std::shared_ptr<hec_plaintext> h_;
+};
+
+class RelinKeys {
+public:
+    RelinKeys() = default;
+    // SEAL layout u64[L][2][K][N] (KSwitchKeys::data()[0], one PublicKey per data prime)
+    RelinKeys(const Context &ctx, const std::uint64_t *data)
+    {
+        hec_kswitch_key *k = nullptr;
+        check(hec_kswitch_key_upload(ctx.get(), data, &k));
+        h_.reset(k, [](hec_kswitch_key *x) { hec_kswitch_key_destroy(x); });
+    }
+    hec_kswitch_key *get() const { return h_.get(); }
+
+private:
+    std::shared_ptr<hec_kswitch_key> h_;
+};
+
+class GaloisKeys {
+public:
+    GaloisKeys() = default;
+    explicit GaloisKeys(const Context &ctx)
+    {
+        hec_galois_keys *g = nullptr;
+        check(hec_galois_keys_create(ctx.get(), &g));
+        h_.reset(g, [](hec_galois_keys *x) { hec_galois_keys_destroy(x); });
+    }
+    void add(std::uint32_t galois_elt, const std::uint64_t *data) { check(hec_galois_keys_add(h_.get(), galois_elt, data)); }
+    bool has_key(std::uint32_t galois_elt) const { return hec_galois_keys_has(h_.get(), galois_elt) != 0; }
+    hec_galois_keys *get() const { return h_.get(); }
+
+private:
+    std::shared_ptr<hec_galois_keys> h_;
+};
+
+// seal::Evaluator: const member functions, in-place and out-of-place forms
+class Evaluator {
+public:
+    explicit Evaluator(const Context &ctx) : ctx_(&ctx) {}
+    const Context &context() const { return *ctx_; }
+
+    void negate_inplace(Ciphertext &a) const { check(hec_negate_inplace(c(), a.get())); }
+    void add_inplace(Ciphertext &a, const Ciphertext &b) const { check(hec_add_inplace(c(), a.get(), b.get())); }
+    void sub_inplace(Ciphertext &a, const Ciphertext &b) const { check(hec_sub_inplace(c(), a.get(), b.get())); }
+    void add_plain_inplace(Ciphertext &a, const Plaintext &p) const { check(hec_add_plain_inplace(c(), a.get(), p.get())); }
+    void sub_plain_inplace(Ciphertext &a, const Plaintext &p) const { check(hec_sub_plain_inplace(c(), a.get(), p.get())); }
+    void multiply_inplace(Ciphertext &a, const Ciphertext &b) const { check(hec_multiply_inplace(c(), a.get(), b.get())); }
+    void multiply_plain_inplace(Ciphertext &a, const Plaintext &p) const
+    {
+        check(hec_multiply_plain_inplace(c(), a.get(), p.get()));
+    }
+    void square_inplace(Ciphertext &a) const { check(hec_square_inplace(c(), a.get())); }
+    void relinearize_inplace(Ciphertext &a, const RelinKeys &rk) const
+    {
+        check(hec_relinearize_inplace(c(), a.get(), rk.get()));
+    }
+    void rescale_to_next_inplace(Ciphertext &a) const { check(hec_rescale_to_next_inplace(c(), a.get())); }
+    void mod_switch_to_next_inplace(Ciphertext &a) const { check(hec_mod_switch_to_next_inplace(c(), a.get())); }
+    void rotate_vector_inplace(Ciphertext &a, int steps, const GaloisKeys &gk) const
+    {
+        check(hec_rotate_vector_inplace(c(), a.get(), steps, gk.get()));
+    }
+    void apply_galois_inplace(Ciphertext &a, std::uint32_t elt, const GaloisKeys &gk) const
+    {
+        check(hec_apply_galois_inplace(c(), a.get(), elt, gk.get()));
+    }
+
+    // out-of-place forms: destination = copy, then the in-place operation (SEAL's own pattern)
+    void negate(const Ciphertext &a, Ciphertext &d) const { d = a; negate_inplace(d); }
+    void add(const Ciphertext &a, const Ciphertext &b, Ciphertext &d) const { d = a; add_inplace(d, b); }
+    void sub(const Ciphertext &a, const Ciphertext &b, Ciphertext &d) const { d = a; sub_inplace(d, b); }
+    void add_plain(const Ciphertext &a, const Plaintext &p, Ciphertext &d) const { d = a; add_plain_inplace(d, p); }
+    void sub_plain(const Ciphertext &a, const Plaintext &p, Ciphertext &d) const { d = a; sub_plain_inplace(d, p); }
+    void multiply(const Ciphertext &a, const Ciphertext &b, Ciphertext &d) const { d = a; multiply_inplace(d, b); }
+    void multiply_plain(const Ciphertext &a, const Plaintext &p, Ciphertext &d) const
+    {
+        d = a;
+        multiply_plain_inplace(d, p);
+    }
+    void square(const Ciphertext &a, Ciphertext &d) const { d = a; square_inplace(d); }
+    void relinearize(const Ciphertext &a, const RelinKeys &rk, Ciphertext &d) const { d = a; relinearize_inplace(d, rk); }
+    void rescale_to_next(const Ciphertext &a, Ciphertext &d) const { d = a; rescale_to_next_inplace(d); }
+    void mod_switch_to_next(const Ciphertext &a, Ciphertext &d) const { d = a; mod_switch_to_next_inplace(d); }
+    void rotate_vector(const Ciphertext &a, int steps, const GaloisKeys &gk, Ciphertext &d) const
+    {
+        d = a;
+        rotate_vector_inplace(d, steps, gk);
+    }
+
+private:
+    hec_context *c() const { return ctx_->get(); }
+    const Context *ctx_;
+};
+
+}  // namespace hecdna

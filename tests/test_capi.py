@@ -44,3 +44,19 @@ def test_host_logic_without_gpu(hecdna):
     with __import__("pytest").raises(hecdna.InvalidArgument):
         hecdna.create_coeff_modulus(1000, [60])
     assert ctypes.sizeof(ctypes.c_void_p) == 8
+
+
+def test_cpp_facade_links_against_boundary(hecdna, tmp_path):
+    """The C++ drop-in headers (he_operators.h / he_linalg.h over hecdna types) compile and the
+    demo links against libhecdna.so using only the C-ABI."""
+    import os
+    pkg = os.path.dirname(hecdna.LIB_PATH)
+    exe = str(tmp_path / "he_demo")
+    subprocess.check_call(["g++", "-std=c++20", "-O0", "-I" + os.path.join(pkg, "cpp", "include"),
+                           "-I" + os.path.join(pkg, "..", "include"),
+                           os.path.join(pkg, "cpp", "demo", "he_demo.cpp"),
+                           os.path.join(pkg, "cpp", "src", "he_operators.cpp"),
+                           os.path.join(pkg, "cpp", "src", "he_linalg.cpp"),
+                           "-L" + pkg, "-lhecdna", "-o", exe])
+    out = subprocess.run([exe], capture_output=True, text=True, env=dict(os.environ, LD_LIBRARY_PATH=pkg))
+    assert out.returncode == 1 and "usage" in out.stdout

@@ -1,0 +1,119 @@
+"""The C++ drop-in surface (cpp/include/he_operators.h, he_linalg.h over hecdna types) runs the
+reference's demo code path on the GPU and reproduces the oracle bit for bit.  The demo program
+(cpp/demo/he_demo.cpp) is the reference's bench_he_batched_matmul_ckks flow
+(src/demos/matrix_operations.cpp:1042-1175) with seal:: replaced by hecdna::."""
+import hashlib
+import json
+import os
+import struct
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "homomorphic-encryption-algorithms-diploma-thesis_amd")
+GOLD = os.path.join(ROOT, "tests", "golden")
+DEMO = os.path.join(PKG, "bin", "he_demo")
+
+
+@pytest.fixture(scope="module")
+def demo():
+    subprocess.check_call(["make", "-s", "-C", PKG, "bin/he_demo"])
+    return DEMO
+
+
+def write_input(path, N, moduli, cts, rk, gk):
+    with open(path, "wb") as f:
+        f.write(b"HECDNA01")
+        f.write(struct.pack("<QQ", N, len(moduli)))
+        f.write(np.array(moduli, dtype=np.uint64).tobytes())
+        f.write(struct.pack("<Q", len(cts)))
+        for c in cts:
+            f.write(struct.pack("<QQd", c.size, c.level, c.scale))
+            f.write(np.ascontiguousarray(c.data, dtype=np.uint64).tobytes())
+        f.write(struct.pack("<Q", 1 if rk is not None else 0))
+        if rk is not None:
+            f.write(np.ascontiguousarray(rk).tobytes())
+        f.write(struct.pack("<Q", len(gk)))
+        for e, k in gk.items():
+            f.write(struct.pack("<Q", e))
+            f.write(np.ascontiguousarray(k).tobytes())
+
+
+def read_output(path, N):
+    out = []
+    with open(path, "rb") as f:
+        (n,) = struct.unpack("<Q", f.read(8))
+        for _ in range(n):
+            s, l, sc = struct.unpack("<QQd", f.read(24))
+            d = np.frombuffer(f.read(s * l * N * 8), dtype=np.uint64).reshape(s, l, N)
+            out.append((d, sc))
+    return out
+
+
+def run(demo, mode, tmp_path, N, moduli, cts, rk, gk):
+    inp, outp = str(tmp_path / f"{mode}.in"), str(tmp_path / f"{mode}.out")
+    write_input(inp, N, moduli, cts, rk, gk)
+    subprocess.check_call([demo, mode, inp, outp])
+    return read_output(outp, N)
+
+
+def test_demo_batched_diag_matches_golden(demo, orc, tmp_path):
+    sys.path.insert(0, GOLD)
+    from make_golden import cfg1_inputs, sha
+    fx = json.load(open(os.path.join(GOLD, "cfg1_matvec.json")))
+    o, m, sk, rk, gk, cts = cfg1_inputs(orc)
+    out = run(demo, "batched_diag", tmp_path, fx["N"], m, cts, rk, gk)
+    assert [sha(d, sc) for d, sc in out] == fx["output_sha256"]
+
+
+@pytest.fixture(scope="module")
+def small(orc):
+    N = 1 << 11
+    m = orc.Oracle.create_coeff_modulus(N, [50, 36, 36, 50])
+    o = orc.Oracle(N, m)
+    sk = o.secret_key(21)
+    rk = o.relin_key(sk, 22)
+    gk = o.galois_keys(sk, o.default_galois_elts(), 23)
+    rng = np.random.default_rng(4)
+    cts = [o.encrypt(sk, o.encode(rng.uniform(-1, 1, N // 2), 2.0**40, 3), 2.0**40, 30 + i) for i in range(8)]
+    return N, m, o, rk, gk, cts
+
+
+def same(got, exp):
+    d, sc = got
+    assert d.shape == exp.data.shape and sc == exp.scale
+    assert np.array_equal(d, exp.data)
+
+
+def test_demo_batched_col(demo, small, tmp_path):
+    N, m, o, rk, gk, cts = small
+    A = cts[:6]
+    out = run(demo, "batched_col", tmp_path, N, m, A, rk, gk)
+    # col x col^T with B = A^T: p = dim of the bvecs (= 6 here), out[i] = sum_j rot(A[j], i) * A[j]
+    exp = o.matmul_col_colT(A, A, 6, rk, gk)
+    assert len(out) == 6
+    for g, e in zip(out, exp):
+        same(g, e)
+
+
+def test_demo_operator_surface(demo, small, tmp_path):
+    N, m, o, rk, gk, cts = small
+    out = run(demo, "ops", tmp_path, N, m, cts[:3], rk, gk)
+    r = o.rescale(o.relinearize(o.multiply(o.rotate(cts[0], 5, gk), cts[1]), rk))
+    s = o.mod_switch(o.rotate(cts[2], -3, gk))
+    t = o.negate(o.sub(cts[0], cts[1]))
+    for g, e in zip(out, [r, s, t]):
+        same(g, e)
+
+
+def test_demo_matrix_matmul(demo, small, tmp_path):
+    N, m, o, rk, gk, cts = small
+    out = run(demo, "matrix", tmp_path, N, m, cts[:8], rk, gk)
+    exp = o.matrix_matmul(cts[:4], 2, 2, False, cts[4:8], 2, 2, False, rk)
+    assert len(out) == 4
+    for g, e in zip(out, exp):
+        same(g, e)
