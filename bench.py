@@ -31,7 +31,8 @@ S_CT = lambda N, l: 2 * l * N * 8  # noqa: E731
 
 def load_hecdna():
     import importlib.util
-    spec = importlib.util.spec_from_file_location("hecdna", os.path.join(PKG, "__init__.py"))
+    spec = importlib.util.spec_from_file_location("hecdna", os.path.join(PKG, "__init__.py"),
+                                                  submodule_search_locations=[PKG])
     mod = importlib.util.module_from_spec(spec)
     sys.modules["hecdna"] = mod
     spec.loader.exec_module(mod)
@@ -96,16 +97,22 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-diags", type=int, default=48)
     ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--mode", choices=["throughput", "sharded"], default="throughput",
+                    help="throughput: replicas, own vectors per rank (the metric, weak scaling); sharded: one "
+                         "batch split over ranks by trie subtrees of the diagonals + one RCCL reduce-scatter "
+                         "(cfg4 curve, strong scaling)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # torch first, at every N: libhecdna then binds to torch's HIP runtime, so the RCCL buffers and
+    # the engine share one runtime and the 1-GPU and N-GPU runs execute the same code
+    import torch
+    torch.cuda.set_device(local)
     dist = None
     if world > 1:
-        import torch
         import torch.distributed as dist
-        torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     hec = load_hecdna()
@@ -118,8 +125,18 @@ def main():
     rk = ctx.relin_key(seed=11 + rank)
     gk = ctx.galois_keys(uniform_elts=elts, seed=1000 + 97 * rank)
     scale = 2.0**40
-    diags = [ctx.ciphertext().fill_uniform(2, L, scale, 10_000 + j) for j in range(args.n)]
-    cols = [ctx.ciphertext().fill_uniform(2, L, scale, 90_000 + 100 * rank + i) for i in range(args.batch)]
+    sharded = args.mode == "sharded"
+    plan = None
+    if sharded:
+        import hecdna.shard as shard
+        plan = shard.plan_diagonal_shards(N, args.n, world)
+        held = set(plan[rank])  # a rank only stores the diagonals of its trie subtrees
+    else:
+        held = range(args.n)
+    diags = [ctx.ciphertext().fill_uniform(2, L, scale, 10_000 + j) if j in held else None for j in range(args.n)]
+    # sharded: every rank sees the same input batch (same seeds); throughput: own vectors per rank
+    cseed = 90_000 + (0 if sharded else 100 * rank)
+    cols = [ctx.ciphertext().fill_uniform(2, L, scale, cseed + i) for i in range(args.batch)]
     outs = [hec.Ciphertext(ctx) for _ in range(args.batch)]
     ctx.synchronize()
 
@@ -130,7 +147,10 @@ def main():
             dist.barrier()
 
     def step():
-        ctx.matmul_diag_col(diags, cols, rk, gk, out=outs)
+        if sharded:
+            shard.sharded_matvec(ctx, diags, cols, rk, gk, rank, world, plan=plan)
+        else:
+            ctx.matmul_diag_col(diags, cols, rk, gk, out=outs)
 
     for _ in range(args.warmup):
         step()
@@ -149,7 +169,7 @@ def main():
         dt = float(t.item())
 
     ms_per_step = dt / args.steps * 1e3
-    total = args.batch * world * args.steps
+    total = args.batch * (1 if sharded else world) * args.steps
     value = total / dt
     ks = ks_total(N, args.n)
 
@@ -193,11 +213,14 @@ def main():
             "metric": "CKKS matvec ciphertexts/sec (N=2^15, L=10)",
             "value": round(value, 6), "unit": "matvec/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "u64", "data": "synthetic",
+            "scaling": "strong" if sharded else "weak", "vs_baseline": None, "dtype": "u64", "data": "synthetic",
             "config": {"workload": f"he_linalg BatchedMatrix::matmul diag x col, {args.n}x{args.n} ct x ct "
                                    f"matvec, N=2^{args.logn}, L={L}, default Galois keys",
                        "batch_per_gpu": args.batch, "n": args.n, "key_switches_per_matvec": ks,
-                       "parallelism": f"replicated matrix+keys, dp{world} over input vectors"},
+                       "parallelism": (f"sharded{world}: diagonals split by rotation-trie subtrees, one RCCL "
+                                       f"reduce-scatter of size-3 partials" if sharded else
+                                       f"replicated matrix+keys, dp{world} over input vectors"),
+                       "batch_global": args.batch * (1 if sharded else world)},
             "roofline": roof,
             "cpu_baseline": cpu,
             "whole_step_algorithmic_GBps": round(algo_mv * total / dt / 1e9, 2),

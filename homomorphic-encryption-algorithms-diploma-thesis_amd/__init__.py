@@ -93,6 +93,7 @@ def lib():
             "hec_apply_galois_inplace": [vp, vp, C.c_uint32, vp],
             "hec_matmul_diag_col": [vp, vp, C.c_uint64, vp, C.c_uint64, vp, vp, vp],
             "hec_matmul_diag_col_partial": [vp, vp, C.c_uint64, C.c_uint64, C.c_uint64, vp, C.c_uint64, vp, vp],
+            "hec_matmul_diag_col_partial_set": [vp, vp, C.c_uint64, vp, C.c_uint64, vp, C.c_uint64, vp, vp],
             "hec_matmul_finish": [vp, vp, C.c_uint64, vp, vp],
             "hec_matmul_col_colT": [vp, vp, C.c_uint64, vp, C.c_uint64, vp, vp, vp],
             "hec_matrix_matmul": [vp, vp, C.c_uint64, C.c_uint64, C.c_int, vp, C.c_uint64, C.c_uint64, C.c_int,
@@ -159,6 +160,7 @@ class Context:
         self.moduli = [int(x) for x in coeff_modulus]
         self.K = len(self.moduli)
         self.L = self.K - 1
+        self.device = int(device)
         m = np.array(self.moduli, dtype=np.uint64)
         h = C.c_void_p()
         _check(lib().hec_context_create(self.N, _p(m), self.K, int(device), C.byref(h)))
@@ -257,7 +259,8 @@ class Context:
     # -------------------------------------------------------------- linalg
     @staticmethod
     def _arr(cts):
-        return (C.c_void_p * len(cts))(*[c.h for c in cts])
+        # None entries pass a null handle (diagonals a sharded rank does not hold; never dereferenced)
+        return (C.c_void_p * len(cts))(*[(c.h if c is not None else None) for c in cts])
 
     def matmul_diag_col(self, diags, cols, rk, gk, out=None):
         out = out or [Ciphertext(self) for _ in cols]
@@ -271,10 +274,21 @@ class Context:
                                                  self._arr(cols), len(cols), gk.h, self._arr(out)))
         return out
 
+    def matmul_diag_col_partial_set(self, diags, js, cols, gk, out=None):
+        out = out or [Ciphertext(self) for _ in cols]
+        idx = np.ascontiguousarray(js, dtype=np.uint64)
+        _check(lib().hec_matmul_diag_col_partial_set(self.h, self._arr(diags), len(diags), _p(idx), len(idx),
+                                                     self._arr(cols), len(cols), gk.h, self._arr(out)))
+        return out
+
     def matmul_finish(self, accs, rk, out=None):
         out = out or [Ciphertext(self) for _ in accs]
         _check(lib().hec_matmul_finish(self.h, self._arr(accs), len(accs), rk.h, self._arr(out)))
         return out
+
+    def reduce(self, ct):
+        """Reduce every word of ct mod its prime (after a partial-sum exchange)."""
+        _check(lib().hec_ciphertext_reduce(self.h, ct.h)); return ct
 
     def matmul_col_colT(self, A, B, p, rk, gk):
         out = [Ciphertext(self) for _ in range(p)]
@@ -375,6 +389,14 @@ class Ciphertext:
         out = np.empty((s, l, self.ctx.N), dtype=np.uint64)
         _check(lib().hec_ciphertext_download(self.h, _p(out)))
         return out
+
+    def export_device(self, dev_ptr):
+        """Copy the u64[size][level][N] words into device memory at dev_ptr (stream ordered)."""
+        _check(lib().hec_ciphertext_export_device(self.h, C.c_void_p(dev_ptr)))
+
+    def import_device(self, dev_ptr, size, level, scale):
+        _check(lib().hec_ciphertext_import_device(self.h, C.c_void_p(dev_ptr), size, level, float(scale)))
+        return self
 
     def copy(self):
         c = Ciphertext(self.ctx)

@@ -408,29 +408,29 @@ void walk_trie(Ctx &c, Scratch &s, const RotTrie &t, int node, PolyArr src, int 
 // rotation launch sequence and one key read serve all p columns, and the rotations run over the
 // prefix trie; every out[i] still sums the same terms (modular addition is exact and order free),
 // so the bits equal the reference loop's.
-void matvec_core(hec_context *ctx, const hec_ciphertext *const *diags, std::size_t n, std::size_t jb, std::size_t je,
-                 const hec_ciphertext *const *cols, std::size_t p, const hec_kswitch_key *rk,
-                 const hec_galois_keys *gk, bool finish, hec_ciphertext *const *out)
+void matvec_core(hec_context *ctx, const hec_ciphertext *const *diags, std::size_t n,
+                 const std::vector<std::size_t> &js, const hec_ciphertext *const *cols, std::size_t p,
+                 const hec_kswitch_key *rk, const hec_galois_keys *gk, bool finish, hec_ciphertext *const *out)
 {
     Ctx &c = ctx->c;
-    need(n >= 1 && p >= 1 && jb < je && je <= n, "empty matrix operand");
+    need(n >= 1 && p >= 1 && !js.empty(), "empty matrix operand");
+    for (std::size_t j : js) need(j < n, "diagonal index out of range");
     need(gk && gk->ctx == ctx, "galois_keys is not valid for encryption parameters");
     if (finish) need(rk && rk->ctx == ctx, "relin_keys is not valid for encryption parameters");
     const std::size_t l = cols[0]->level, N = c.N;
-    for (std::size_t j = jb; j < je; ++j) check_ct(ctx, diags[j]);
+    for (std::size_t j : js) check_ct(ctx, diags[j]);
     for (std::size_t i = 0; i < p; ++i) check_ct(ctx, cols[i]);
     for (std::size_t i = 0; i < p; ++i) need(cols[i]->size == 2, "encrypted size must be 2");
-    for (std::size_t j = jb; j < je; ++j) need(diags[j]->size == 2, "encrypted size must be 2");
-    for (std::size_t j = jb; j < je; ++j)
-        need(diags[j]->level == l, "encrypted1 and encrypted2 parameter mismatch");
+    for (std::size_t j : js) need(diags[j]->size == 2, "encrypted size must be 2");
+    for (std::size_t j : js) need(diags[j]->level == l, "encrypted1 and encrypted2 parameter mismatch");
     for (std::size_t i = 0; i < p; ++i) need(cols[i]->level == l, "encrypted1 and encrypted2 parameter mismatch");
     // scale bookkeeping exactly as multiply_inplace (bound) + add_inplace (are_close) would see it
     std::vector<double> ps(p);
     for (std::size_t i = 0; i < p; ++i) {
-        for (std::size_t j = jb; j < je; ++j) {
-            const double sc = cols[i]->scale * diags[j]->scale;
+        for (std::size_t k = 0; k < js.size(); ++k) {
+            const double sc = cols[i]->scale * diags[js[k]]->scale;
             need(scale_ok(c, sc, l), "scale out of bounds");
-            if (j == jb) ps[i] = sc;
+            if (k == 0) ps[i] = sc;
             else need(are_close(ps[i], sc), "scale mismatch");
         }
     }
@@ -438,7 +438,7 @@ void matvec_core(hec_context *ctx, const hec_ciphertext *const *diags, std::size
     RotTrie trie;
     {
         std::vector<u32> seq;
-        for (std::size_t j = jb; j < je; ++j) {
+        for (std::size_t j : js) {
             seq.clear();
             rotation_elts(c, (int)j, *gk, seq);
             trie.insert(seq, j);
@@ -1156,7 +1156,9 @@ int hec_matmul_diag_col(hec_context *ctx, const hec_ciphertext *const *diags, ui
     return guard([&] {
         set_device(ctx);
         need(diags && cols && out, "null argument");
-        matvec_core(ctx, diags, n, 0, n, cols, p, rk, gk, true, out);
+        std::vector<std::size_t> js(n);
+        for (std::size_t j = 0; j < n; ++j) js[j] = j;
+        matvec_core(ctx, diags, n, js, cols, p, rk, gk, true, out);
     });
 }
 
@@ -1167,7 +1169,24 @@ int hec_matmul_diag_col_partial(hec_context *ctx, const hec_ciphertext *const *d
     return guard([&] {
         set_device(ctx);
         need(diags && cols && acc_out, "null argument");
-        matvec_core(ctx, diags, n, j_begin, j_end, cols, p, nullptr, gk, false, acc_out);
+        need(j_begin < j_end && j_end <= n, "empty matrix operand");
+        std::vector<std::size_t> js;
+        for (uint64_t j = j_begin; j < j_end; ++j) js.push_back(j);
+        matvec_core(ctx, diags, n, js, cols, p, nullptr, gk, false, acc_out);
+    });
+}
+
+int hec_matmul_diag_col_partial_set(hec_context *ctx, const hec_ciphertext *const *diags, uint64_t n,
+                                    const uint64_t *j_idx, uint64_t nj, const hec_ciphertext *const *cols, uint64_t p,
+                                    const hec_galois_keys *gk, hec_ciphertext *const *acc_out)
+{
+    return guard([&] {
+        set_device(ctx);
+        need(diags && cols && acc_out && j_idx, "null argument");
+        std::vector<std::size_t> js(j_idx, j_idx + nj);
+        std::sort(js.begin(), js.end());
+        need(std::adjacent_find(js.begin(), js.end()) == js.end(), "duplicate diagonal index");
+        matvec_core(ctx, diags, n, js, cols, p, nullptr, gk, false, acc_out);
     });
 }
 

@@ -127,6 +127,13 @@ int hec_matmul_diag_col(hec_context *ctx, const hec_ciphertext *const *diags, ui
 int hec_matmul_diag_col_partial(hec_context *ctx, const hec_ciphertext *const *diags, uint64_t n,
                                 uint64_t j_begin, uint64_t j_end, const hec_ciphertext *const *cols, uint64_t p,
                                 const hec_galois_keys *gk, hec_ciphertext *const *acc_out);
+/* Sharded form over an arbitrary set of diagonal indices j_idx[0..nj) (any order, no duplicates): the
+ * multi-GPU planner hands each rank whole subtrees of the rotation prefix trie so that no key switch
+ * is repeated across ranks.  Summing the partials of a partition of [0, n) mod q gives exactly the
+ * accumulator of hec_matmul_diag_col. */
+int hec_matmul_diag_col_partial_set(hec_context *ctx, const hec_ciphertext *const *diags, uint64_t n,
+                                    const uint64_t *j_idx, uint64_t nj, const hec_ciphertext *const *cols, uint64_t p,
+                                    const hec_galois_keys *gk, hec_ciphertext *const *acc_out);
 /* relinearize + rescale a batch of size-3 accumulators (he_linalg.cpp:999-1002) */
 int hec_matmul_finish(hec_context *ctx, hec_ciphertext *const *acc, uint64_t p, const hec_kswitch_key *rk,
                       hec_ciphertext *const *out);

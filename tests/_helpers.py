@@ -13,7 +13,8 @@ PKG_DIR = os.path.join(ROOT, "homomorphic-encryption-algorithms-diploma-thesis_a
 def load_hecdna():
     if "hecdna" in sys.modules:
         return sys.modules["hecdna"]
-    spec = importlib.util.spec_from_file_location("hecdna", os.path.join(PKG_DIR, "__init__.py"))
+    spec = importlib.util.spec_from_file_location("hecdna", os.path.join(PKG_DIR, "__init__.py"),
+                                                  submodule_search_locations=[PKG_DIR])
     mod = importlib.util.module_from_spec(spec)
     sys.modules["hecdna"] = mod
     spec.loader.exec_module(mod)

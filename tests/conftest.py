@@ -14,6 +14,12 @@ def pytest_configure(config):
 
 @pytest.fixture(scope="session")
 def hecdna():
+    # torch ships its own HIP runtime (torch/lib/libamdhip64.so, soname libamdhip64.so.7).  Initialising
+    # torch first lets libhecdna bind to that same runtime; loading libhecdna first would pull in
+    # /opt/rocm's copy and leave torch's second runtime without a device (tests that exchange device
+    # tensors with torch need both on one runtime).
+    import torch
+    torch.cuda.is_available()
     from _helpers import load_hecdna
     return load_hecdna()
 

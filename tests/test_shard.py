@@ -1,0 +1,138 @@
+"""Multi-GPU sharding logic on CPU: the trie-subtree planner, and the one exchange
+step over a world_size-2 gloo process group.  The per-rank partial accumulators come from the
+oracle here (the GPU path for the same step is in test_gpu_shard.py); what is under test is the
+planner, the u64-as-int64 collective and the owner bookkeeping in hecdna.shard."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+
+@pytest.fixture(scope="module")
+def shard(hecdna):
+    import hecdna.shard as s
+    return s
+
+
+def test_rotation_elts_follow_seal_naf(shard, orc):
+    N = 1 << 11
+    m = orc.Oracle.create_coeff_modulus(N, [50, 36, 50])
+    o = orc.Oracle(N, m)
+    assert sorted(shard.default_galois_elts(N)) == sorted(o.default_galois_elts())
+    for v in list(range(-40, 41)) + [N // 2 - 1, 1000, -777]:
+        assert shard._naf(v) == orc.Oracle.naf(v)
+        if 0 < abs(v) < N // 2:
+            assert shard.elt_from_step(N, v) == o.elt_from_step(v)
+
+
+@pytest.mark.parametrize("N,n,total", [(1 << 13, 64, 84), (1 << 15, 4096, 5460), (1 << 16, 1024, 1364)])
+def test_trie_cost_known_counts(shard, N, n, total):
+    # 5460 = key switches of the cfg3 matvec on the trie (SEAL's per-rotation count is 18204)
+    assert shard.trie_cost(N, range(n)) == total
+
+
+@pytest.mark.parametrize("N,n", [(1 << 13, 64), (1 << 15, 4096), (1 << 16, 1024), (1 << 11, 5)])
+@pytest.mark.parametrize("G", [1, 2, 3, 4, 8])
+def test_plan_partitions_and_balances(shard, N, n, G):
+    if G > n:
+        with pytest.raises(ValueError):
+            shard.plan_diagonal_shards(N, n, G)
+        return
+    plan = shard.plan_diagonal_shards(N, n, G)
+    assert len(plan) == G and all(plan)
+    assert sorted(j for p in plan for j in p) == list(range(n))
+    costs = [shard.trie_cost(N, p) for p in plan]
+    total = shard.trie_cost(N, range(n))
+    depth = max(len(shard.rotation_elts(N, j, set(shard.default_galois_elts(N)))) for j in range(n))
+    # subtrees stay whole: at most one shared path repeated per cut
+    assert sum(costs) <= total + (G - 1) * depth
+    if n >= 64:
+        assert max(costs) <= -(-total // G) + 2 * depth
+
+
+def test_owners(shard):
+    assert shard.owners(8, 4) == [0, 0, 1, 1, 2, 2, 3, 3]
+    assert shard.owners(3, 2) == [0, 1, 0]
+    assert shard.owners(1, 1) == [0]
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, p, q):
+    import sys
+    import torch
+    import torch.distributed as dist
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__))))
+    from _helpers import load_hecdna, load_oracle
+    load_hecdna()
+    import hecdna.shard as shard
+    orc = load_oracle()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        N, n = 1 << 11, 8
+        m = orc.Oracle.create_coeff_modulus(N, [50, 36, 36, 50])
+        o = orc.Oracle(N, m)
+        sk = o.secret_key(5)
+        rk = o.relin_key(sk, 6)
+        gk = o.galois_keys(sk, o.default_galois_elts(), 7)
+        rng = np.random.default_rng(11)
+        enc = lambda s: o.encrypt(sk, o.encode(rng.uniform(-1, 1, N // 2), 2.0**30, 3), 2.0**30, s)  # noqa
+        A = [enc(100 + j) for j in range(n)]
+        X = [enc(200 + i) for i in range(p)]
+        plan = shard.plan_diagonal_shards(N, n, world)
+        mine = plan[rank]
+        # this rank's partial = sum over its contiguous runs of oracle range partials (mod q)
+        acc = None
+        runs, start = [], mine[0]
+        for a, b in zip(mine, mine[1:] + [None]):
+            if b != a + 1:
+                runs.append((start, a + 1))
+                start = b
+        qs = np.asarray(m[:3], dtype=np.uint64).reshape(1, 3, 1)
+        for jb, je in runs:
+            part = o.matmul_diag_col(A, X, rk, gk, j_begin=jb, j_end=je, finish=False)
+            d = np.stack([c.data for c in part])
+            acc = d if acc is None else (acc + d) % qs
+        scale = part[0].scale
+        buf = torch.from_numpy(acc.reshape(p, -1).view(np.int64).copy())
+        rows = shard.exchange_partials(buf, world)
+        red = shard.reduce_rows_mod_q(rows.numpy(), m, 3, N)
+        owned = [i for i, w in enumerate(shard.owners(p, world)) if w == rank]
+        assert len(owned) == red.shape[0]
+        full = o.matmul_diag_col(A, X, rk, gk)
+        for k, i in enumerate(owned):
+            c = orc.Ct(red[k].reshape(3, 3, N).copy(), scale)
+            fin = o.rescale(o.relinearize(c, rk))
+            assert fin.scale == full[i].scale
+            assert np.array_equal(fin.data, full[i].data), (rank, i)
+        q.put((rank, "ok", owned))
+    except Exception as e:  # surface the failure to the parent
+        q.put((rank, repr(e), None))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("p", [2, 3])  # 2: reduce-scatter path, 3: all-reduce + round robin
+def test_gloo_world2_exchange_bit_exact(shard, p):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, p, q)) for r in range(2)]
+    for pr in procs:
+        pr.start()
+    res = [q.get(timeout=300) for _ in procs]
+    for pr in procs:
+        pr.join(timeout=60)
+    assert all(r[1] == "ok" for r in res), res
+    owned = sorted(i for r in res for i in r[2])
+    assert owned == list(range(p))
