@@ -179,7 +179,7 @@ def main():
         ctx.profile(True)
         step()
         ctx.synchronize()
-        for cls in ("ks_intt", "ks_modup", "ks_mac", "ks_modup_mac", "ks_moddown", "galois", "tensor", "relin",
+        for cls in ("ks_intt", "ks_modup", "ks_mac", "ks_modup_a", "ks_bmac", "ks_moddown", "galois", "tensor", "relin",
                     "rescale"):
             ms, cnt = ctx.profile_read(cls)
             breakdown[cls] = {"ms": round(ms, 3), "launch_groups": cnt}

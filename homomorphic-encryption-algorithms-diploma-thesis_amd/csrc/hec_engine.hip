@@ -273,9 +273,15 @@ void keyswitch(Ctx &c, Scratch &s, PolyArr T, const u64 *key, PolyArr IN, int in
         ProfScope ps(c, "ks_intt");
         ntt_strided(c, true, T.p, T.sb, D, l * N, l, pmap, B * l);
     }
-    if (c.fused_modup_mac) {  // experimental: latency-bound at small batch
-        ProfScope ps(c, "ks_modup_mac");
-        ks_modup_mac(c, D, E, T, key, ACC, B, l);
+    if (c.fused_modup_mac) {  // mod-up pass A, then pass B fused with the key MAC (no E round trip)
+        {
+            ProfScope ps(c, "ks_modup_a");
+            ks_modup_mac(c, D, E, T, key, ACC, B, l, 1);
+        }
+        {
+            ProfScope ps(c, "ks_bmac");
+            ks_modup_mac(c, D, E, T, key, ACC, B, l, 2);
+        }
     } else {
         {
             ProfScope ps(c, "ks_modup");
@@ -551,7 +557,8 @@ int hec_context_create(uint64_t N, const uint64_t *mod, uint64_t K, int device, 
         auto *ctx = new hec_context();
         Ctx &c = ctx->c;
         c.device = device;
-        if (const char *f = std::getenv("HEC_FUSED_MODUP_MAC")) c.fused_modup_mac = f[0] == '1';
+        if (const char *f = std::getenv("HEC_FUSED_MODUP_MAC")) c.fused_modup_mac = f[0] != '0';
+        if (const char *f = std::getenv("HEC_BMAC_KEYS")) c.bmac_keys = f[0] - '0';
         c.N = N;
         c.logN = __builtin_ctzll(N);
         c.K = K;
@@ -560,6 +567,9 @@ int hec_context_create(uint64_t N, const uint64_t *mod, uint64_t K, int device, 
         for (u64 q : c.q) c.bits.push_back(64 - __builtin_clzll(q));
         HEC_HIP(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
         c.own_stream = true;
+        HEC_HIP(hipStreamCreateWithFlags(&c.side, hipStreamNonBlocking));
+        HEC_HIP(hipEventCreateWithFlags(&c.ev_fork, hipEventDisableTiming));
+        HEC_HIP(hipEventCreateWithFlags(&c.ev_join, hipEventDisableTiming));
         std::vector<ulonglong2> tw(K * N), itw(K * N);
         for (uint64_t i = 0; i < K; ++i) {
             const u64 q = c.q[i];
@@ -658,6 +668,9 @@ int hec_context_destroy(hec_context *ctx)
         (void)hipFree(c.itwb);
         for (double *p : {c.twf, c.itwf, c.twbf, c.itwbf}) (void)hipFree(p);
         if (c.own_stream) (void)hipStreamDestroy(c.stream);
+        (void)hipStreamDestroy(c.side);
+        (void)hipEventDestroy(c.ev_fork);
+        (void)hipEventDestroy(c.ev_join);
         delete ctx;
     });
 }

@@ -42,6 +42,8 @@ struct Ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     bool own_stream = false;
+    hipStream_t side = nullptr;                 // second stream for concurrent kernels inside a call
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     std::size_t N = 0;
     int logN = 0;
     std::size_t K = 0, L = 0;
@@ -62,7 +64,8 @@ struct Ctx {
     // host-side constants
     std::vector<u64> p_inv, p_inv_q, p_half_mod;            // key switch mod-down (per data prime)
     std::vector<std::vector<u64>> ql_inv, ql_inv_q, ql_half_mod;  // rescale at level l (drop prime l-1)
-    bool fused_modup_mac = false;  // HEC_FUSED_MODUP_MAC=1 selects the fused mod-up/MAC kernels
+    int bmac_keys = 1;             // HEC_BMAC_KEYS: k_bmac key loads 0 late / 1 before the rounds / 2 one digit ahead
+    bool fused_modup_mac = true;  // HEC_FUSED_MODUP_MAC=0: separate mod-up pass B and key MAC kernels
     // profiling
     bool prof = false;
     struct ProfRec { double ms = 0; uint64_t n = 0; };
@@ -83,8 +86,9 @@ void ntt_strided(Ctx &c, bool inverse, const u64 *src, u64 ps_src, u64 *dst, u64
 // Key-switch phases (B targets at level l; see hec_engine.hip for the dataflow)
 void ks_modup(Ctx &c, const u64 *D, u64 *E, int B, int l);
 void ks_mac(Ctx &c, PolyArr T, const u64 *E, const u64 *key, u64 *ACC, int B, int l);
-// fused: pass A of the mod-up NTTs, then (pass B + key MAC) per target prime -> ACC[b][k][I]
-void ks_modup_mac(Ctx &c, const u64 *D, u64 *E, PolyArr T, const u64 *key, u64 *ACC, int B, int l);
+// fused: pass A of the mod-up NTTs (part & 1), then (pass B + key MAC) per target prime -> ACC[b][k][I]
+// (part & 2)
+void ks_modup_mac(Ctx &c, const u64 *D, u64 *E, PolyArr T, const u64 *key, u64 *ACC, int B, int l, int part);
 // divide-and-round by `last_idx` prime: Y = coefficient-form last limb per (b,k) (address Y + b*ysb + k*ysk),
 // X / IN / OUT addressed (b,k,i), nk polys per batch entry, nl output limbs.
 //   OUT = IN + (X - NTT(corr)) * inv   (IN optional; inv = last^-1 mod q_i)

@@ -178,15 +178,37 @@ struct TwTables {
 };
 
 // One round: stages [S0, S1) of a P = 2^LOGP point sub-transform.  Thread `ts` of its segment owns
-// 16 elements = 2^(4-D) groups of 2^D elements (D = S1 - S0).  FP selects the arithmetic: the LDS
-// words then hold the bits of integer-valued doubles.
-template <int LOGP, int RND, bool INV, bool FP, class AddrF, class TwF>
-__device__ __forceinline__ void ntt_round(u64 *lds, const AddrF &addr, int ts, const TwF &twidx, const ulonglong2 *tw,
-                                          const double *twf, const DevPrime &pr)
+// EPT elements = EPT / 2^D groups of 2^D elements (D = S1 - S0).  FP selects the arithmetic: the LDS
+// words then hold the bits of integer-valued doubles.  TO_REG keeps the results in `regs` (group
+// order: regs[gi 2^D + a]) instead of writing them back to LDS; in a final round (S1 == LOGP) the
+// thread's EPT elements are then the consecutive slots ts*EPT .. ts*EPT + EPT - 1.
+// Twiddle getters: (global stage s, index i within the stage) -> w.  GlobalTw reads the SEAL-ordered /
+// pass-B re-laid tables in HBM (L2-resident); LdsTw a per-segment copy staged in LDS.
+template <class IdxF>
+struct GlobalTw {
+    IdxF idx;
+    const ulonglong2 *tw;
+    const double *twf;
+    __device__ double f(int s, int i) const { return twf[idx(s, i)]; }
+    __device__ ulonglong2 w(int s, int i) const { return tw[idx(s, i)]; }
+};
+struct LdsTw {  // entry k = 2^s - 1 + i of this segment; FP: one word (double bits), integer: {w, w_shoup}
+    const u64 *row;
+    __device__ double f(int s, int i) const { return __longlong_as_double((long long)row[(1 << s) - 1 + i]); }
+    __device__ ulonglong2 w(int s, int i) const
+    {
+        const u64 *p = row + 2 * ((1 << s) - 1 + i);
+        return ulonglong2{p[0], p[1]};
+    }
+};
+
+template <int LOGP, int S0, int S1, int EPT, bool INV, bool FP, bool TO_REG, class AddrF, class TwG>
+__device__ __forceinline__ void ntt_round_g(u64 *lds, const AddrF &addr, int ts, const TwG &twg, const DevPrime &pr,
+                                            u64 *regs)
 {
-    constexpr int S0 = RND * 4;
-    constexpr int S1 = (S0 + 4 < LOGP) ? S0 + 4 : LOGP;
-    constexpr int D = S1 - S0, G = 1 << (4 - D), NQ = 1 << D;
+    constexpr int LE = EPT == 16 ? 4 : EPT == 8 ? 3 : EPT == 4 ? 2 : 1;
+    constexpr int D = S1 - S0, G = 1 << (LE - D), NQ = 1 << D;
+    static_assert(D >= 1 && D <= LE, "round covers 1..log2(EPT) stages");
     const u64 q = pr.q, two_q = 2 * q;
 #pragma unroll
     for (int gi = 0; gi < G; ++gi) {
@@ -203,9 +225,8 @@ __device__ __forceinline__ void ntt_round(u64 *lds, const AddrF &addr, int ts, c
         for (int st = 0; st < D; ++st)
 #pragma unroll
             for (int m = 0; m < (1 << st); ++m) {
-                const u64 ti = twidx(S0 + st, (hi << st) | m);
-                if constexpr (FP) wf[(1 << st) - 1 + m] = twf[ti];
-                else wi[(1 << st) - 1 + m] = tw[ti];
+                if constexpr (FP) wf[(1 << st) - 1 + m] = twg.f(S0 + st, (hi << st) | m);
+                else wi[(1 << st) - 1 + m] = twg.w(S0 + st, (hi << st) | m);
             }
         u64 v[NQ];
 #pragma unroll
@@ -231,8 +252,22 @@ __device__ __forceinline__ void ntt_round(u64 *lds, const AddrF &addr, int ts, c
             }
         }
 #pragma unroll
-        for (int a = 0; a < NQ; ++a) lds[addr(xb | (a << (LOGP - S1)))] = v[a];
+        for (int a = 0; a < NQ; ++a) {
+            if constexpr (TO_REG) regs[gi * NQ + a] = v[a];
+            else lds[addr(xb | (a << (LOGP - S1)))] = v[a];
+        }
     }
+}
+
+// the two-pass NTT's rounds: 16 elements per thread, stages [4 RND, min(4 RND + 4, LOGP))
+template <int LOGP, int RND, bool INV, bool FP, class AddrF, class TwF>
+__device__ __forceinline__ void ntt_round(u64 *lds, const AddrF &addr, int ts, const TwF &twidx, const ulonglong2 *tw,
+                                          const double *twf, const DevPrime &pr)
+{
+    constexpr int S0 = RND * 4;
+    constexpr int S1 = (S0 + 4 < LOGP) ? S0 + 4 : LOGP;
+    const GlobalTw<TwF> twg{twidx, tw, twf};
+    ntt_round_g<LOGP, S0, S1, 16, INV, FP, false>(lds, addr, ts, twg, pr, nullptr);
 }
 
 template <int LOGP, int NSEG, bool INV, bool PASS_A, bool FINAL, bool FP, class Bound>
@@ -415,143 +450,218 @@ void divide_round(Ctx &c, const u64 *Y, u64 ysb, u64 ysk, PolyArr X, PolyArr IN,
 }
 
 // ====================================================================== fused mod-up B + MAC ==
-// Key-switch steps (2b)+(3) in one kernel: a block owns NSEG chunks (NSEG * C coefficients) of one
-// target prime I for one batch entry b and loops over the digits J: it finishes the NTT of digit J
-// (pass B stages, from the pass-A output E[b][I][J]; J == I reuses the NTT-form target T[b][I])
-// in LDS/registers and multiply-accumulates it with key[J][k][I] into per-thread accumulators, so
-// the NTT-form digits never go back to HBM.  FP primes (< 2^42) accumulate exact FP64 modular
-// products (|acc| <= 0.53 q l, canonicalised once), 60-bit primes fold each 128-bit product with one
-// Barrett reduction (64-bit accumulators keep the register footprint at 2 waves/SIMD).
-// Blocks of the same (I, chunk block) for different b land on the same XCD (grid x = chunk blocks,
-// a multiple of 8), so the key chunk they share is served from that XCD's L2.
-template <int LOGP, int NSEG, bool FP>
-__global__ void __launch_bounds__(NSEG *(1 << LOGP) / 16, 2)
-    k_modup_b_mac(PolyArr T, const u64 *__restrict__ E, const u64 *__restrict__ key, u64 *__restrict__ ACC,
-                  TwTables tt, const DevPrime *__restrict__ primes, const int *__restrict__ Imap, int logN, int l,
-                  int K)
+// Key-switch steps (2b)+(3) in one kernel, so the NTT-form digits never go back to HBM.  A block owns
+// NSEG contiguous chunks (NSEG * P coefficients) of one target prime I for one batch entry b and
+// loops over the digits J:
+//   * the pass-A output E[b][I][J] of digit J (J == I: the NTT-form target T[b][I]) is staged into
+//     LDS from registers that were loaded one iteration earlier (software prefetch), and the key
+//     words key[J][k][I] of the thread's output coefficients are issued before the rounds;
+//   * the pass-B stages run in 8-element rounds (3 + 3 + 1 stages for P = 128); the last round
+//     leaves each thread with 8 consecutive NTT outputs in registers;
+//   * those are multiplied by the key words and accumulated: FP primes (< 2^42) as exact FP64
+//     products (|acc| <= 0.53 q l, canonicalised once), 60-bit primes in 128-bit accumulators
+//     (SEAL's lazy MAC), one Barrett reduction at the end.  (Barrett-reduced 64-bit accumulators
+//     would bring the kernel to 3 waves/SIMD but measured 15 % slower: the integer blocks set the tail.)
+// Grid (R / NSEG, l + 1, B): blocks of one (chunk block, I) for different b are R/NSEG * (l+1) apart,
+// a multiple of 8 for logN >= 14, so they run on one XCD and share its L2 copy of the key chunk.
+// The integer target primes come first in Imap: their blocks are the slowest, so they start first.
+template <int LOGP, int NSEG, int EPT, bool FP, int KEYM>
+__device__ __forceinline__ void bmac_body(u64 *lds, u64 *ltw, PolyArr T, const u64 *__restrict__ E, const u64 *__restrict__ key,
+                                          u64 *__restrict__ ACC, const TwTables &tt, const DevPrime &pr, int I, int kI,
+                                          int b, int logN, int l, int K)
 {
-    constexpr int P = 1 << LOGP, THREADS = NSEG * P / 16, LD = P + 1, EPT = 16;
-    __shared__ u64 lds[NSEG * (P + 1)];
-    const int I = Imap[blockIdx.y], b = blockIdx.z;
-    const int kI = I == l ? K - 1 : I;
-    const DevPrime pr = primes[kI];
+    constexpr int P = 1 << LOGP, THREADS = NSEG * P / EPT, LD = P + 1, TWS = 2 * P + 2;
     const u64 N = 1ull << logN;
     const int seg0 = blockIdx.x * NSEG;
-    const u64 base = (u64)seg0 << LOGP;  // first coefficient of the block (contiguous range)
+    const u64 base = (u64)seg0 << LOGP;
     const ulonglong2 *tw = tt.b + ((u64)kI << logN);
     const double *twf = tt.fb + ((u64)kI << logN);
     const int ts = threadIdx.x / NSEG, sg = threadIdx.x % NSEG;
     auto addr = [sg](int x) { return sg * LD + x; };
-    const u64 R = 1ull << (logN - LOGP), chunk = (u64)(seg0 + sg);
-    auto twidx = [=](int s, int i) -> u64 { return R * ((1ull << s) - 1) + (u64)i * R + chunk; };
+    const u64 R = 1ull << (logN - LOGP);
+    // the pass-B twiddles of a chunk do not depend on the digit J: stage the block's (NSEG chunks x
+    // (P - 1) entries) once into LDS, rows padded to TWS words (bank spread), lanes = consecutive chunks
+    // so the re-laid table reads coalesce
+    for (int t = threadIdx.x; t < NSEG * (P - 1); t += THREADS) {
+        const int sl = t % NSEG, k = t / NSEG;
+        const int st = 31 - __clz(k + 1), i = k + 1 - (1 << st);
+        const u64 gi = R * ((1ull << st) - 1) + (u64)i * R + (u64)(seg0 + sl);
+        if constexpr (FP) ltw[sl * TWS + k] = (u64)__double_as_longlong(twf[gi]);
+        else {
+            const ulonglong2 w = tw[gi];
+            ltw[sl * TWS + 2 * k] = w.x;
+            ltw[sl * TWS + 2 * k + 1] = w.y;
+        }
+    }
+    const LdsTw twg{ltw + sg * TWS};
+    const u64 g0 = ((u64)(seg0 + sg) << LOGP) + (u64)ts * EPT;  // first of this thread's outputs
+    auto src = [&](int J) -> const u64 * {
+        return J == I ? T.p + b * T.sb + (u64)J * N : E + (((u64)((b * (l + 1) + I) * l + J)) << logN);
+    };
 
-    // accumulators: FP -> integer-valued doubles; int -> canonical u64 folded by Barrett per digit
-    u64 a0[EPT], a1[EPT];
+    double f0[FP ? EPT : 1], f1[FP ? EPT : 1];
+    U128 i0[FP ? 1 : EPT], i1[FP ? 1 : EPT];
 #pragma unroll
     for (int e = 0; e < EPT; ++e) {
-        if constexpr (FP) a0[e] = a1[e] = (u64)__double_as_longlong(0.0);
-        else a0[e] = a1[e] = 0;
+        if constexpr (FP) f0[e] = f1[e] = 0.0;
+        else i0[e] = i1[e] = U128{0, 0};
+    }
+    auto load_keys = [&](int J, u64 *k0, u64 *k1) {
+        const u64 *kp0 = key + (((u64)(J * 2 + 0) * K + kI) << logN) + g0;
+        const u64 *kp1 = key + (((u64)(J * 2 + 1) * K + kI) << logN) + g0;
+#pragma unroll
+        for (int e = 0; e < EPT; e += 2) {
+            const ulonglong2 a = *(const ulonglong2 *)(kp0 + e), c = *(const ulonglong2 *)(kp1 + e);
+            k0[e] = a.x; k0[e + 1] = a.y; k1[e] = c.x; k1[e + 1] = c.y;
+        }
+    };
+    u64 kc0[KEYM == 2 ? EPT : 1], kc1[KEYM == 2 ? EPT : 1];
+    if constexpr (KEYM == 2) load_keys(0, kc0, kc1);
+    u64 nx[EPT];
+    {
+        const u64 *s0 = src(0) + base;
+#pragma unroll
+        for (int e = 0; e < EPT; ++e) nx[e] = s0[threadIdx.x + e * THREADS];
     }
     for (int J = 0; J < l; ++J) {
-        const u64 *src = (J == I) ? T.p + b * T.sb + (u64)J * N
-                                  : E + (((u64)((b * (l + 1) + I) * l + J)) << logN);
-        const bool ntt = (J != I);
-#pragma unroll 4
-        for (int li = threadIdx.x; li < P * NSEG; li += THREADS) {
-            u64 v = src[base + li];
+        const bool ntt = J != I;
+#pragma unroll
+        for (int e = 0; e < EPT; ++e) {
+            const int li = threadIdx.x + e * THREADS;
+            u64 v = nx[e];
             if constexpr (FP) {
                 if (!ntt) v = (u64)__double_as_longlong(u2d(v));  // canonical integer target
             }
             lds[(li / P) * LD + (li % P)] = v;
         }
-        __syncthreads();
-        if (ntt) {
-            ntt_round<LOGP, 0, false, FP>(lds, addr, ts, twidx, tw, twf, pr);
-            __syncthreads();
-            ntt_round<LOGP, 1, false, FP>(lds, addr, ts, twidx, tw, twf, pr);
-            __syncthreads();
+        if (J + 1 < l) {
+            const u64 *s1 = src(J + 1) + base;
+#pragma unroll
+            for (int e = 0; e < EPT; ++e) nx[e] = s1[threadIdx.x + e * THREADS];
         }
-        const u64 *k0p = key + (((u64)(J * 2 + 0) * K + kI) << logN) + base;
-        const u64 *k1p = key + (((u64)(J * 2 + 1) * K + kI) << logN) + base;
+        u64 k0[EPT], k1[EPT];
+        if constexpr (KEYM == 2) {  // keys of digit J were loaded one iteration ago; issue J + 1's now
+#pragma unroll
+            for (int e = 0; e < EPT; ++e) { k0[e] = kc0[e]; k1[e] = kc1[e]; }
+            if (J + 1 < l) load_keys(J + 1, kc0, kc1);
+        }
+        if constexpr (KEYM == 1) load_keys(J, k0, k1);
+        __syncthreads();
+        u64 v[EPT];
+        if (ntt) {
+            static_assert(LOGP >= 5 && LOGP <= 8, "pass-B sizes 2^5 .. 2^8");
+            if constexpr (LOGP <= 6) {
+                ntt_round_g<LOGP, 0, 3, EPT, false, FP, false>(lds, addr, ts, twg, pr, nullptr);
+                __syncthreads();
+                ntt_round_g<LOGP, 3, LOGP, EPT, false, FP, true>(lds, addr, ts, twg, pr, v);
+            } else {
+                ntt_round_g<LOGP, 0, 3, EPT, false, FP, false>(lds, addr, ts, twg, pr, nullptr);
+                __syncthreads();
+                ntt_round_g<LOGP, 3, 6, EPT, false, FP, false>(lds, addr, ts, twg, pr, nullptr);
+                __syncthreads();
+                ntt_round_g<LOGP, 6, LOGP, EPT, false, FP, true>(lds, addr, ts, twg, pr, v);
+            }
+        } else {
+#pragma unroll
+            for (int e = 0; e < EPT; ++e) v[e] = lds[addr(ts * EPT + e)];
+        }
+        if constexpr (KEYM == 0) load_keys(J, k0, k1);
 #pragma unroll
         for (int e = 0; e < EPT; ++e) {
-            if ((e & 3) == 0) __builtin_amdgcn_sched_barrier(0);  // bound the loads in flight (VGPRs)
-            const int li = threadIdx.x + e * THREADS;
-            const u64 v = lds[(li / P) * LD + (li % P)];
-            const u64 k0 = k0p[li], k1 = k1p[li];
             if constexpr (FP) {
-                const double dv = __longlong_as_double((long long)v);
-                a0[e] = (u64)__double_as_longlong(__longlong_as_double((long long)a0[e]) +
-                                                  fp_mulmod(dv, u2d(k0), pr.qd, pr.qinv));
-                a1[e] = (u64)__double_as_longlong(__longlong_as_double((long long)a1[e]) +
-                                                  fp_mulmod(dv, u2d(k1), pr.qd, pr.qinv));
-            } else {  // acc + v*k < 2^61 + 2^124: one Barrett keeps the accumulator canonical
-                U128 t0{a0[e], 0}, t1{a1[e], 0};
-                mac128(t0, v, k0);
-                mac128(t1, v, k1);
-                a0[e] = barrett128(t0.lo, t0.hi, pr.q, pr.r0, pr.r1);
-                a1[e] = barrett128(t1.lo, t1.hi, pr.q, pr.r0, pr.r1);
+                const double dv = __longlong_as_double((long long)v[e]);
+                f0[e] += fp_mulmod(dv, u2d(k0[e]), pr.qd, pr.qinv);
+                f1[e] += fp_mulmod(dv, u2d(k1[e]), pr.qd, pr.qinv);
+            } else {
+                mac128(i0[e], v[e], k0[e]);  // v < 4q: sum of l products < 2^126
+                mac128(i1[e], v[e], k1[e]);
             }
         }
         __syncthreads();
     }
-    u64 *o0 = ACC + (((u64)((b * 2 + 0) * (l + 1) + I)) << logN) + base;
-    u64 *o1 = ACC + (((u64)((b * 2 + 1) * (l + 1) + I)) << logN) + base;
+    u64 *o0 = ACC + (((u64)((b * 2 + 0) * (l + 1) + I)) << logN) + g0;
+    u64 *o1 = ACC + (((u64)((b * 2 + 1) * (l + 1) + I)) << logN) + g0;
 #pragma unroll
-    for (int e = 0; e < EPT; ++e) {
-        const int li = threadIdx.x + e * THREADS;
+    for (int e = 0; e < EPT; e += 2) {
         if constexpr (FP) {
-            o0[li] = fp_canon(__longlong_as_double((long long)a0[e]), pr.qd, pr.qinv);
-            o1[li] = fp_canon(__longlong_as_double((long long)a1[e]), pr.qd, pr.qinv);
+            *(ulonglong2 *)(o0 + e) = ulonglong2{fp_canon(f0[e], pr.qd, pr.qinv), fp_canon(f0[e + 1], pr.qd, pr.qinv)};
+            *(ulonglong2 *)(o1 + e) = ulonglong2{fp_canon(f1[e], pr.qd, pr.qinv), fp_canon(f1[e + 1], pr.qd, pr.qinv)};
         } else {
-            o0[li] = a0[e];
-            o1[li] = a1[e];
+            *(ulonglong2 *)(o0 + e) = ulonglong2{barrett128(i0[e].lo, i0[e].hi, pr.q, pr.r0, pr.r1),
+                                                 barrett128(i0[e + 1].lo, i0[e + 1].hi, pr.q, pr.r0, pr.r1)};
+            *(ulonglong2 *)(o1 + e) = ulonglong2{barrett128(i1[e].lo, i1[e].hi, pr.q, pr.r0, pr.r1),
+                                                 barrett128(i1[e + 1].lo, i1[e + 1].hi, pr.q, pr.r0, pr.r1)};
         }
     }
 }
 
-template <int LOGR, int LOGC, int NA, int NB>
-static void run_modup_fused(Ctx &c, const u64 *D, u64 *E, PolyArr T, const u64 *key, u64 *ACC, int B, int l)
+// one launch: blockIdx.y < nint -> integer target primes, the rest FP64 (blocks of both kinds overlap)
+template <int LOGP, int NSEG, int EPT, int KEYM>
+__global__ void __launch_bounds__(NSEG *(1 << LOGP) / EPT)
+    k_bmac(PolyArr T, const u64 *__restrict__ E, const u64 *__restrict__ key, u64 *__restrict__ ACC, TwTables tt,
+           const DevPrime *__restrict__ primes, const int *__restrict__ Imap, int logN, int l, int K, int nint)
 {
-    constexpr int R = 1 << LOGR, C = 1 << LOGC;
-    ModUpMap m{l, c.logN, (int)c.K - 1};
-    ModUpIO_A a{m, D, E, c.primes};
+    __shared__ u64 lds[NSEG * ((1 << LOGP) + 1)];
+    __shared__ u64 ltw[NSEG * (2 * (1 << LOGP) + 2)];
+    const int I = Imap[blockIdx.y], b = blockIdx.z;
+    const int kI = I == l ? K - 1 : I;
+    const DevPrime pr = primes[kI];
+    if ((int)blockIdx.y < nint)
+        bmac_body<LOGP, NSEG, EPT, false, KEYM>(lds, ltw, T, E, key, ACC, tt, pr, I, kI, b, logN, l, K);
+    else
+        bmac_body<LOGP, NSEG, EPT, true, KEYM>(lds, ltw, T, E, key, ACC, tt, pr, I, kI, b, logN, l, K);
+}
+
+template <int LOGR, int LOGC, int NA, int NB2>
+static void run_modup_fused(Ctx &c, const u64 *D, u64 *E, PolyArr T, const u64 *key, u64 *ACC, int B, int l,
+                            int part)
+{
+    constexpr int R = 1 << LOGR, C = 1 << LOGC, EPT = 8;
     const TwTables fwd{c.tw, c.twb, c.twf, c.twbf};
     // (2a) pass A of every mod-up NTT (B * l * l jobs), output E[b][I][J] (lazy, pass-A domain)
-    k_ntt<LOGR, NA, false, true, false><<<dim3(C / NA, B * l * l), NA * R / 16, 0, c.stream>>>(a, fwd, c.primes, c.logN);
-    // (2b)+(3) fused, split by arithmetic path
+    if (part & 1) {
+        ModUpMap m{l, c.logN, (int)c.K - 1};
+        k_ntt<LOGR, NA, false, true, false><<<dim3(C / NA, B * l * l), NA * R / 16, 0, c.stream>>>(
+            ModUpIO_A{m, D, E, c.primes}, fwd, c.primes, c.logN);
+    }
+    if (!(part & 2)) {
+        HEC_HIP(hipGetLastError());
+        return;
+    }
+    // (2b)+(3) fused; integer target primes first (slowest blocks start first)
     int nfp = 0, nint = 0;
     int *hm = c.imap_host.data();
     for (int I = 0; I <= l; ++I) {
         const int kI = I == l ? (int)c.K - 1 : I;
-        if (c.hprimes[kI].fp) hm[nfp++] = I;
+        if (!c.hprimes[kI].fp) hm[nint++] = I;
     }
     for (int I = 0; I <= l; ++I) {
         const int kI = I == l ? (int)c.K - 1 : I;
-        if (!c.hprimes[kI].fp) hm[nfp + nint++] = I;
+        if (c.hprimes[kI].fp) hm[nint + nfp++] = I;
     }
     int *dm = c.imap + (HEC_MAXL + 2) * (c.imap_slot++ % 64);
     HEC_HIP(hipMemcpyAsync(dm, hm, (l + 1) * sizeof(int), hipMemcpyHostToDevice, c.stream));
-    constexpr int TB = NB * C / 16;
-    if (nfp)
-        k_modup_b_mac<LOGC, NB, true><<<dim3(R / NB, nfp, B), TB, 0, c.stream>>>(T, E, key, ACC, fwd, c.primes, dm,
-                                                                                 c.logN, l, (int)c.K);
-    if (nint)
-        k_modup_b_mac<LOGC, NB, false><<<dim3(R / NB, nint, B), TB, 0, c.stream>>>(T, E, key, ACC, fwd, c.primes,
-                                                                                    dm + nfp, c.logN, l, (int)c.K);
+    constexpr int TB = NB2 * C / EPT;
+    const dim3 grid(R / NB2, nint + nfp, B);
+    switch (c.bmac_keys) {  // key loads: 0 after the rounds, 1 before them, 2 one digit ahead
+    case 0: k_bmac<LOGC, NB2, EPT, 0><<<grid, TB, 0, c.stream>>>(T, E, key, ACC, fwd, c.primes, dm, c.logN, l, (int)c.K, nint); break;
+    case 1: k_bmac<LOGC, NB2, EPT, 1><<<grid, TB, 0, c.stream>>>(T, E, key, ACC, fwd, c.primes, dm, c.logN, l, (int)c.K, nint); break;
+    default: k_bmac<LOGC, NB2, EPT, 2><<<grid, TB, 0, c.stream>>>(T, E, key, ACC, fwd, c.primes, dm, c.logN, l, (int)c.K, nint); break;
+    }
     HEC_HIP(hipGetLastError());
 }
 
-void ks_modup_mac(Ctx &c, const u64 *D, u64 *E, PolyArr T, const u64 *key, u64 *ACC, int B, int l)
+void ks_modup_mac(Ctx &c, const u64 *D, u64 *E, PolyArr T, const u64 *key, u64 *ACC, int B, int l, int part)
 {
+    // <LOGR, LOGC, pass-A columns per block, fused pass-B chunks per block (256 threads, 8 elements each)>
     switch (c.logN) {
-    case 10: run_modup_fused<5, 5, 32, 32>(c, D, E, T, key, ACC, B, l); break;
-    case 11: run_modup_fused<6, 5, 32, 64>(c, D, E, T, key, ACC, B, l); break;
-    case 12: run_modup_fused<6, 6, 64, 64>(c, D, E, T, key, ACC, B, l); break;
-    case 13: run_modup_fused<7, 6, 32, 64>(c, D, E, T, key, ACC, B, l); break;
-    case 14: run_modup_fused<7, 7, 32, 32>(c, D, E, T, key, ACC, B, l); break;
-    case 15: run_modup_fused<8, 7, 16, 32>(c, D, E, T, key, ACC, B, l); break;
-    case 16: run_modup_fused<8, 8, 16, 16>(c, D, E, T, key, ACC, B, l); break;
+    case 10: run_modup_fused<5, 5, 32, 32>(c, D, E, T, key, ACC, B, l, part); break;
+    case 11: run_modup_fused<6, 5, 32, 64>(c, D, E, T, key, ACC, B, l, part); break;
+    case 12: run_modup_fused<6, 6, 64, 32>(c, D, E, T, key, ACC, B, l, part); break;
+    case 13: run_modup_fused<7, 6, 32, 32>(c, D, E, T, key, ACC, B, l, part); break;
+    case 14: run_modup_fused<7, 7, 32, 16>(c, D, E, T, key, ACC, B, l, part); break;
+    case 15: run_modup_fused<8, 7, 16, 16>(c, D, E, T, key, ACC, B, l, part); break;
+    case 16: run_modup_fused<8, 8, 16, 8>(c, D, E, T, key, ACC, B, l, part); break;
     default: throw std::invalid_argument("poly_modulus_degree must be 2^10 .. 2^16");
     }
 }

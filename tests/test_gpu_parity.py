@@ -271,3 +271,26 @@ def test_cfg3_matvec_small_n_bitexact(env15):
     got = e.ctx.matmul_diag_col([e.up(a) for a in A], [e.up(x) for x in X], e.rk, e.gk)
     for g, c in zip(got, exp):
         e.same(g, c)
+
+
+@pytest.mark.parametrize("env", [{"HEC_FUSED_MODUP_MAC": "0"}, {"HEC_BMAC_KEYS": "0"}, {"HEC_BMAC_KEYS": "2"}])
+def test_keyswitch_variants_bitexact(orc, hecdna, env):
+    """The engine's alternative key-switch schedules (separate mod-up pass B + MAC kernels; the fused
+    kernel's key-load placements) give the same bits as the oracle."""
+    import os
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        e = Env(orc, hecdna, 1 << 12, [60, 40, 40, 60], seed=77)  # contexts read the switches at creation
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    A = [e.enc(seed=j) for j in range(6)]
+    X = [e.enc(seed=40 + i) for i in range(2)]
+    exp = e.o.matmul_diag_col(A, X, e.rk_h, e.gk_h)
+    got = e.ctx.matmul_diag_col([e.up(a) for a in A], [e.up(x) for x in X], e.rk, e.gk)
+    for g, c in zip(got, exp):
+        e.same(g, c)
