@@ -52,6 +52,19 @@ def algorithmic_bytes_per_matvec(N, l, n, B, ks):
     return (n * s_ct + ks * s_key + s_key) / B + ks * 2 * s_ct + n * s_ct + s_ct3 + s_ct
 
 
+def pmc_traffic(cls, B, logn, level):
+    """HBM bytes per launch of the roofline kernel from the committed rocprofv3 PMC passes
+    (profiles/r01_pmc_k_bmac.json: FETCH_SIZE and WRITE_SIZE in separate passes, gfx950 FETCH x2
+    correction for its 16-B/lane reads), when they were taken at this configuration; else None."""
+    path = os.path.join(ROOT, "profiles", "r01_pmc_k_bmac.json")
+    if cls != "ks_bmac" or not os.path.exists(path):
+        return None
+    p = json.load(open(path))
+    if (p["batch"], p["logN"], p["level"]) != (B, logn, level):
+        return None
+    return p["traffic_bytes_per_dispatch"]
+
+
 def cpu_baseline(N, moduli, n, sample_diags, threads):
     """The oracle (C++ restatement of the reference's SEAL path, `port`) timed on this host on a bounded
     sample: diagonals j in [0, sample_diags) of one matvec, extrapolated by key-switch count."""
@@ -173,28 +186,48 @@ def main():
     value = total / dt
     ks = ks_total(N, args.n)
 
-    # per-phase breakdown: one extra (untimed) profiled step with HIP events on the context stream
+    # per-phase breakdown: one extra (untimed) step with asynchronous HIP event pairs recorded on the
+    # context's stream around every phase (no host synchronisation inside the step)
     breakdown = {}
+    classes = ("ks_intt", "ks_modup", "ks_mac", "ks_modup_a", "ks_bmac", "ks_moddown", "galois", "tensor", "relin",
+               "rescale")
     if not args.no_profile:
-        ctx.profile(True)
+        ctx.profile(2)
         step()
         ctx.synchronize()
-        for cls in ("ks_intt", "ks_modup", "ks_mac", "ks_modup_a", "ks_bmac", "ks_moddown", "galois", "tensor", "relin",
-                    "rescale"):
+        for cls in classes:
             ms, cnt = ctx.profile_read(cls)
-            breakdown[cls] = {"ms": round(ms, 3), "launch_groups": cnt}
-        ctx.profile(False)
+            if cnt:
+                breakdown[cls] = {"ms": round(ms, 3), "launch_groups": cnt}
+        ctx.profile(0)
 
-    # roofline for the dominant kernel group: key-switch mod-up NTT (2 passes); algorithmic bytes per
-    # group = l*l limb-NTTs x 2*N*8 B (SURVEY §8(d) cfg2 unit) x batch
+    # roofline for the dominant phase: algorithmic bytes of one launch group (compulsory reads + writes,
+    # SURVEY §8(d) units: limb = N*8 B, B targets, level l, K = l+1 key moduli) / its average duration
+    K = L + 1
+    limb = N * 8
+    Bt = args.batch
+    algo_limbs = {
+        "ks_intt": 2 * Bt * L,                                   # target limbs in, coefficient limbs out
+        "ks_modup_a": Bt * L + Bt * L * L,                       # D in, l^2 pass-A digit limbs out
+        "ks_bmac": Bt * L * L + Bt * L + 2 * L * K + 2 * Bt * K,  # pass-A digits + T + key in, ACC out
+        "ks_modup": Bt * L + Bt * L * L,                         # D in, l^2 NTT-form digits out
+        "ks_mac": Bt * L * L + Bt * L + 2 * L * K + 2 * Bt * K,   # digits + T + key in, ACC out
+        "ks_moddown": 2 * Bt * K + Bt * L + 2 * Bt * L,           # ACC + c0 in, rotated ct out
+        "galois": 4 * Bt * L,
+    }
     roof = None
-    if breakdown.get("ks_modup", {}).get("launch_groups"):
-        bm = breakdown["ks_modup"]
+    cand = [c for c in algo_limbs if c in breakdown]
+    if cand:
+        dom = max(cand, key=lambda c: breakdown[c]["ms"])
+        bm = breakdown[dom]
         per = bm["ms"] / bm["launch_groups"]
-        algo = L * L * 2 * N * 8 * args.batch
+        algo = algo_limbs[dom] * limb
         ach = algo / (per * 1e-3) / 1e9
+        kern = {"ks_bmac": "k_bmac (mod-up pass B + key MAC, fused)", "ks_modup": "k_ntt mod-up pass A+B",
+                "ks_modup_a": "k_ntt mod-up pass A", "ks_mac": "k_ks_mac"}.get(dom, dom)
         roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "kernel": "ks_modup (k_ntt pass A+B)",
+                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(dom, args.batch, args.logn, L),
+                "kernel": kern,
                 "avg_ms": round(per, 4), "algorithmic_bytes_per_launch": algo}
 
     cpu = None

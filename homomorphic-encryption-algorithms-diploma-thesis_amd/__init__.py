@@ -315,8 +315,9 @@ class Context:
         _check(fn(self.h, buf.p, limb0, nl, npolys))
         return buf.download(a.shape)
 
-    def profile(self, on=True):
-        _check(lib().hec_profile_enable(self.h, int(on)))
+    def profile(self, mode=1):
+        """0 off, 1 synchronous per phase, 2 asynchronous event pairs (resolved by profile_read)."""
+        _check(lib().hec_profile_enable(self.h, int(mode)))
 
     def profile_read(self, cls):
         ms = C.c_double()

@@ -229,21 +229,42 @@ struct Scratch {
 };
 
 // ------------------------------------------------------------------ profiling -------------
+// Per-class GPU time of the engine's phases.  prof_mode 1: event pair + synchronize per scope;
+// prof_mode 2: event pairs from a reusable pool recorded asynchronously (no host sync inside the
+// call), resolved when the profile is read.
 struct ProfScope {
     Ctx &c;
-    std::string name;
+    const char *name;
     hipEvent_t e0 = nullptr, e1 = nullptr;
+    hipEvent_t pool_event()
+    {
+        if (c.ev_used == c.ev_pool.size()) {
+            hipEvent_t e;
+            HEC_HIP(hipEventCreate(&e));
+            c.ev_pool.push_back(e);
+        }
+        return c.ev_pool[c.ev_used++];
+    }
     ProfScope(Ctx &cc, const char *n) : c(cc), name(n)
     {
-        if (!c.prof) return;
-        HEC_HIP(hipEventCreate(&e0));
-        HEC_HIP(hipEventCreate(&e1));
+        if (!c.prof_mode) return;
+        if (c.prof_mode == 2) {
+            e0 = pool_event();
+            e1 = pool_event();
+        } else {
+            HEC_HIP(hipEventCreate(&e0));
+            HEC_HIP(hipEventCreate(&e1));
+        }
         HEC_HIP(hipEventRecord(e0, c.stream));
     }
     ~ProfScope()
     {
-        if (!c.prof || !e0) return;
+        if (!c.prof_mode || !e0) return;
         (void)hipEventRecord(e1, c.stream);
+        if (c.prof_mode == 2) {
+            c.prof_pend.push_back({name, e0, e1});
+            return;
+        }
         (void)hipEventSynchronize(e1);
         float ms = 0;
         (void)hipEventElapsedTime(&ms, e0, e1);
@@ -254,6 +275,20 @@ struct ProfScope {
         (void)hipEventDestroy(e1);
     }
 };
+void prof_resolve(Ctx &c)
+{
+    if (c.prof_pend.empty()) return;
+    HEC_HIP(hipStreamSynchronize(c.stream));
+    for (const auto &p : c.prof_pend) {
+        float ms = 0;
+        HEC_HIP(hipEventElapsedTime(&ms, p.e0, p.e1));
+        auto &r = c.prof_tab[p.name];
+        r.ms += ms;
+        r.n += 1;
+    }
+    c.prof_pend.clear();
+    c.ev_used = 0;
+}
 
 // ------------------------------------------------------------------ batched building blocks
 std::size_t ks_words(const Ctx &c, std::size_t B, std::size_t l)
@@ -624,7 +659,23 @@ int hec_context_create(uint64_t N, const uint64_t *mod, uint64_t K, int device, 
         HEC_HIP(hipMalloc(&c.itwb, K * N * sizeof(ulonglong2)));
         HEC_HIP(hipMemcpy(c.twb, twb.data(), K * N * sizeof(ulonglong2), hipMemcpyHostToDevice));
         HEC_HIP(hipMemcpy(c.itwb, itwb.data(), K * N * sizeof(ulonglong2), hipMemcpyHostToDevice));
-        HEC_HIP(hipMalloc(&c.imap, 64 * (HEC_MAXL + 2) * sizeof(int)));
+        {   // target-prime order tables per level (integer primes first)
+            std::vector<int> tab((c.L + 1) * (HEC_MAXL + 2), 0);
+            c.imap_nint.assign(c.L + 1, 0);
+            for (std::size_t l = 1; l <= c.L; ++l) {
+                int *t = tab.data() + l * (HEC_MAXL + 2), n = 0;
+                for (int pass = 0; pass < 2; ++pass)
+                    for (int I = 0; I <= (int)l; ++I) {
+                        const int kI = I == (int)l ? (int)K - 1 : I;
+                        const bool fp = c.hprimes[kI].fp != 0;
+                        if ((pass == 0) != fp) t[n++] = I;
+                    }
+                for (int I = 0; I <= (int)l; ++I)
+                    if (!c.hprimes[I == (int)l ? K - 1 : I].fp) ++c.imap_nint[l];
+            }
+            HEC_HIP(hipMalloc(&c.imap, tab.size() * sizeof(int)));
+            HEC_HIP(hipMemcpy(c.imap, tab.data(), tab.size() * sizeof(int), hipMemcpyHostToDevice));
+        }
         HEC_HIP(hipMalloc(&c.primes, K * sizeof(DevPrime)));
         HEC_HIP(hipMemcpy(c.primes, c.hprimes.data(), K * sizeof(DevPrime), hipMemcpyHostToDevice));
         HEC_HIP(hipMalloc(&c.tw, K * N * sizeof(ulonglong2)));
@@ -671,6 +722,7 @@ int hec_context_destroy(hec_context *ctx)
         (void)hipStreamDestroy(c.side);
         (void)hipEventDestroy(c.ev_fork);
         (void)hipEventDestroy(c.ev_join);
+        for (hipEvent_t e : c.ev_pool) (void)hipEventDestroy(e);
         delete ctx;
     });
 }
@@ -1438,18 +1490,23 @@ int hec_time_ntt_forward(hec_context *ctx, uint64_t *d, uint64_t nl, uint64_t np
     });
 }
 
-int hec_profile_enable(hec_context *ctx, int on)
+int hec_profile_enable(hec_context *ctx, int mode)
 {
     return guard([&] {
-        need(ctx != nullptr, "null");
-        ctx->c.prof = on != 0;
-        if (on) ctx->c.prof_tab.clear();
+        need(ctx != nullptr && mode >= 0 && mode <= 2, "invalid argument");
+        Ctx &c = ctx->c;
+        set_device(ctx);
+        prof_resolve(c);
+        c.prof_mode = mode;
+        if (mode) c.prof_tab.clear();
     });
 }
 int hec_profile_read(hec_context *ctx, const char *cls, double *total_ms, uint64_t *launches)
 {
     return guard([&] {
         need(ctx && cls, "null");
+        set_device(ctx);
+        prof_resolve(ctx->c);
         auto it = ctx->c.prof_tab.find(cls);
         if (total_ms) *total_ms = it == ctx->c.prof_tab.end() ? 0 : it->second.ms;
         if (launches) *launches = it == ctx->c.prof_tab.end() ? 0 : it->second.n;

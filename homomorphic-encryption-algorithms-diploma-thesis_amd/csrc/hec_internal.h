@@ -56,9 +56,11 @@ struct Ctx {
     ulonglong2 *twb = nullptr;      // device [K][N] pass-B layout of tw: [s][i][chunk] (see hec_kernels.hip)
     ulonglong2 *itwb = nullptr;     // same for itw
     double *twf = nullptr, *itwf = nullptr, *twbf = nullptr, *itwbf = nullptr;  // FP64 twins (q < 2^42)
-    int *imap = nullptr;                    // device ring of 64 target-prime order tables (kernel args)
-    unsigned imap_slot = 0;
-    std::vector<int> imap_host = std::vector<int>(HEC_MAXL + 2);
+    // key-switch target primes I in [0, l] (I == l is P) per level l, integer-arithmetic primes first:
+    // device table imap + l * (HEC_MAXL + 2), built once at context creation; imap_nint[l] of them integer
+    int *imap = nullptr;
+    std::vector<int> imap_nint;
+    const int *imap_at(int l) const { return imap + (std::size_t)l * (HEC_MAXL + 2); }
     int logR = 0;                   // pass split N = R x C, R = 2^ceil(logN/2)
     Workspace ws;
     // host-side constants
@@ -66,10 +68,14 @@ struct Ctx {
     std::vector<std::vector<u64>> ql_inv, ql_inv_q, ql_half_mod;  // rescale at level l (drop prime l-1)
     int bmac_keys = 1;             // HEC_BMAC_KEYS: k_bmac key loads 0 late / 1 before the rounds / 2 one digit ahead
     bool fused_modup_mac = true;  // HEC_FUSED_MODUP_MAC=0: separate mod-up pass B and key MAC kernels
-    // profiling
-    bool prof = false;
+    // profiling (ProfScope in hec_engine.hip)
+    int prof_mode = 0;  // 0 off, 1 synchronous per scope, 2 asynchronous event pairs
     struct ProfRec { double ms = 0; uint64_t n = 0; };
     std::map<std::string, ProfRec> prof_tab;
+    struct ProfPend { const char *name; hipEvent_t e0, e1; };
+    std::vector<ProfPend> prof_pend;
+    std::vector<hipEvent_t> ev_pool;
+    std::size_t ev_used = 0;
     int total_bits(std::size_t level) const
     {
         int b = 0;

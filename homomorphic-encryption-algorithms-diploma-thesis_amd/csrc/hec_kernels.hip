@@ -468,11 +468,11 @@ void divide_round(Ctx &c, const u64 *Y, u64 ysb, u64 ysk, PolyArr X, PolyArr IN,
 template <int LOGP, int NSEG, int EPT, bool FP, int KEYM>
 __device__ __forceinline__ void bmac_body(u64 *lds, u64 *ltw, PolyArr T, const u64 *__restrict__ E, const u64 *__restrict__ key,
                                           u64 *__restrict__ ACC, const TwTables &tt, const DevPrime &pr, int I, int kI,
-                                          int b, int logN, int l, int K)
+                                          int b, int xb, int logN, int l, int K)
 {
     constexpr int P = 1 << LOGP, THREADS = NSEG * P / EPT, LD = P + 1, TWS = 2 * P + 2;
     const u64 N = 1ull << logN;
-    const int seg0 = blockIdx.x * NSEG;
+    const int seg0 = xb * NSEG;
     const u64 base = (u64)seg0 << LOGP;
     const ulonglong2 *tw = tt.b + ((u64)kI << logN);
     const double *twf = tt.fb + ((u64)kI << logN);
@@ -517,28 +517,30 @@ __device__ __forceinline__ void bmac_body(u64 *lds, u64 *ltw, PolyArr T, const u
     };
     u64 kc0[KEYM == 2 ? EPT : 1], kc1[KEYM == 2 ? EPT : 1];
     if constexpr (KEYM == 2) load_keys(0, kc0, kc1);
+    // digit tiles move as 16-B pairs: pair w = threadIdx.x + e THREADS holds block elements 2w, 2w + 1
     u64 nx[EPT];
-    {
-        const u64 *s0 = src(0) + base;
+    auto load_tile = [&](int J) {
+        const ulonglong2 *sp = (const ulonglong2 *)(src(J) + base);
 #pragma unroll
-        for (int e = 0; e < EPT; ++e) nx[e] = s0[threadIdx.x + e * THREADS];
-    }
+        for (int e = 0; e < EPT / 2; ++e) {
+            const ulonglong2 w = sp[threadIdx.x + e * THREADS];
+            nx[2 * e] = w.x;
+            nx[2 * e + 1] = w.y;
+        }
+    };
+    load_tile(0);
     for (int J = 0; J < l; ++J) {
         const bool ntt = J != I;
 #pragma unroll
         for (int e = 0; e < EPT; ++e) {
-            const int li = threadIdx.x + e * THREADS;
+            const int li = 2 * (threadIdx.x + (e / 2) * THREADS) + (e & 1);
             u64 v = nx[e];
             if constexpr (FP) {
                 if (!ntt) v = (u64)__double_as_longlong(u2d(v));  // canonical integer target
             }
             lds[(li / P) * LD + (li % P)] = v;
         }
-        if (J + 1 < l) {
-            const u64 *s1 = src(J + 1) + base;
-#pragma unroll
-            for (int e = 0; e < EPT; ++e) nx[e] = s1[threadIdx.x + e * THREADS];
-        }
+        if (J + 1 < l) load_tile(J + 1);
         u64 k0[EPT], k1[EPT];
         if constexpr (KEYM == 2) {  // keys of digit J were loaded one iteration ago; issue J + 1's now
 #pragma unroll
@@ -599,17 +601,26 @@ __device__ __forceinline__ void bmac_body(u64 *lds, u64 *ltw, PolyArr T, const u
 template <int LOGP, int NSEG, int EPT, int KEYM>
 __global__ void __launch_bounds__(NSEG *(1 << LOGP) / EPT)
     k_bmac(PolyArr T, const u64 *__restrict__ E, const u64 *__restrict__ key, u64 *__restrict__ ACC, TwTables tt,
-           const DevPrime *__restrict__ primes, const int *__restrict__ Imap, int logN, int l, int K, int nint)
+           const DevPrime *__restrict__ primes, const int *__restrict__ Imap, int logN, int l, int K, int nint,
+           int gpad)
 {
     __shared__ u64 lds[NSEG * ((1 << LOGP) + 1)];
     __shared__ u64 ltw[NSEG * (2 * (1 << LOGP) + 2)];
-    const int I = Imap[blockIdx.y], b = blockIdx.z;
+    // 1-D grid, XCD-aware: workgroup w runs on XCD w % 8.  The B blocks of one (chunk block, I) group
+    // read the same key chunk, so they get ids G8*8*B + b*8 + (G % 8): one XCD, dispatched together,
+    // and the key chunk is fetched into that XCD's L2 once instead of once per b.
+    const int w = blockIdx.x, B = gridDim.x / gpad;
+    const int g8 = w & 7, rest = w >> 3, b = rest % B, G = (rest / B) * 8 + g8;
+    const int X = (1 << (logN - LOGP)) / NSEG;
+    if (G >= X * (l + 1)) return;
+    const int yi = G / X, xb = G % X;
+    const int I = Imap[yi];
     const int kI = I == l ? K - 1 : I;
     const DevPrime pr = primes[kI];
-    if ((int)blockIdx.y < nint)
-        bmac_body<LOGP, NSEG, EPT, false, KEYM>(lds, ltw, T, E, key, ACC, tt, pr, I, kI, b, logN, l, K);
+    if (yi < nint)
+        bmac_body<LOGP, NSEG, EPT, false, KEYM>(lds, ltw, T, E, key, ACC, tt, pr, I, kI, b, xb, logN, l, K);
     else
-        bmac_body<LOGP, NSEG, EPT, true, KEYM>(lds, ltw, T, E, key, ACC, tt, pr, I, kI, b, logN, l, K);
+        bmac_body<LOGP, NSEG, EPT, true, KEYM>(lds, ltw, T, E, key, ACC, tt, pr, I, kI, b, xb, logN, l, K);
 }
 
 template <int LOGR, int LOGC, int NA, int NB2>
@@ -629,24 +640,16 @@ static void run_modup_fused(Ctx &c, const u64 *D, u64 *E, PolyArr T, const u64 *
         return;
     }
     // (2b)+(3) fused; integer target primes first (slowest blocks start first)
-    int nfp = 0, nint = 0;
-    int *hm = c.imap_host.data();
-    for (int I = 0; I <= l; ++I) {
-        const int kI = I == l ? (int)c.K - 1 : I;
-        if (!c.hprimes[kI].fp) hm[nint++] = I;
-    }
-    for (int I = 0; I <= l; ++I) {
-        const int kI = I == l ? (int)c.K - 1 : I;
-        if (c.hprimes[kI].fp) hm[nint + nfp++] = I;
-    }
-    int *dm = c.imap + (HEC_MAXL + 2) * (c.imap_slot++ % 64);
-    HEC_HIP(hipMemcpyAsync(dm, hm, (l + 1) * sizeof(int), hipMemcpyHostToDevice, c.stream));
+    const int nint = c.imap_nint[l], nfp = l + 1 - nint;
+    const int *dm = c.imap_at(l);
     constexpr int TB = NB2 * C / EPT;
-    const dim3 grid(R / NB2, nint + nfp, B);
+    constexpr int X = R / NB2;
+    const int groups = X * (l + 1), gpad = (groups + 7) / 8 * 8;
+    const dim3 grid(gpad * B);
     switch (c.bmac_keys) {  // key loads: 0 after the rounds, 1 before them, 2 one digit ahead
-    case 0: k_bmac<LOGC, NB2, EPT, 0><<<grid, TB, 0, c.stream>>>(T, E, key, ACC, fwd, c.primes, dm, c.logN, l, (int)c.K, nint); break;
-    case 1: k_bmac<LOGC, NB2, EPT, 1><<<grid, TB, 0, c.stream>>>(T, E, key, ACC, fwd, c.primes, dm, c.logN, l, (int)c.K, nint); break;
-    default: k_bmac<LOGC, NB2, EPT, 2><<<grid, TB, 0, c.stream>>>(T, E, key, ACC, fwd, c.primes, dm, c.logN, l, (int)c.K, nint); break;
+    case 0: k_bmac<LOGC, NB2, EPT, 0><<<grid, TB, 0, c.stream>>>(T, E, key, ACC, fwd, c.primes, dm, c.logN, l, (int)c.K, nint, gpad); break;
+    case 1: k_bmac<LOGC, NB2, EPT, 1><<<grid, TB, 0, c.stream>>>(T, E, key, ACC, fwd, c.primes, dm, c.logN, l, (int)c.K, nint, gpad); break;
+    default: k_bmac<LOGC, NB2, EPT, 2><<<grid, TB, 0, c.stream>>>(T, E, key, ACC, fwd, c.primes, dm, c.logN, l, (int)c.K, nint, gpad); break;
     }
     HEC_HIP(hipGetLastError());
 }
@@ -753,34 +756,24 @@ __device__ __forceinline__ void ks_mac_fp(PolyArr T, const u64 *__restrict__ E, 
     }
 }
 
-// one launch: blockIdx.y < nfp -> FP64 target primes, the rest integer primes (run concurrently)
+// one launch: blockIdx.y < nint -> integer target primes, the rest FP64 primes (run concurrently)
 template <int BT>
 __global__ void __launch_bounds__(256)
     k_ks_mac(PolyArr T, const u64 *__restrict__ E, const u64 *__restrict__ key, u64 *__restrict__ ACC, int B, int l,
-             int K, int logN, const DevPrime *__restrict__ primes, const int *__restrict__ Imap, int nfp)
+             int K, int logN, const DevPrime *__restrict__ primes, const int *__restrict__ Imap, int nint)
 {
     const int I = Imap[blockIdx.y];
-    if ((int)blockIdx.y < nfp) ks_mac_fp<BT>(T, E, key, ACC, B, l, K, logN, primes, I);
-    else ks_mac_int<BT>(T, E, key, ACC, B, l, K, logN, primes, I);
+    if ((int)blockIdx.y < nint) ks_mac_int<BT>(T, E, key, ACC, B, l, K, logN, primes, I);
+    else ks_mac_fp<BT>(T, E, key, ACC, B, l, K, logN, primes, I);
 }
 
 void ks_mac(Ctx &c, PolyArr T, const u64 *E, const u64 *key, u64 *ACC, int B, int l)
 {
     constexpr int BT = 8;
-    int nfp = 0, nint = 0;
-    int *hm = c.imap_host.data();
-    for (int pass = 0; pass < 2; ++pass)
-        for (int I = 0; I <= l; ++I) {
-            const int kI = I == l ? (int)c.K - 1 : I;
-            const bool fp = c.hprimes[kI].fp != 0;
-            if (pass == 0 && fp) hm[nfp++] = I;
-            if (pass == 1 && !fp) hm[nfp + nint++] = I;
-        }
-    int *dm = c.imap + (HEC_MAXL + 2) * (c.imap_slot++ % 64);  // per-call slot: no host/device race
-    HEC_HIP(hipMemcpyAsync(dm, hm, (l + 1) * sizeof(int), hipMemcpyHostToDevice, c.stream));
+    const int nint = c.imap_nint[l];
     const unsigned bz = (B + BT - 1) / BT;
-    k_ks_mac<BT><<<dim3((unsigned)(c.N / 256), nfp + nint, bz), 256, 0, c.stream>>>(T, E, key, ACC, B, l, (int)c.K,
-                                                                                   c.logN, c.primes, dm, nfp);
+    k_ks_mac<BT><<<dim3((unsigned)(c.N / 256), l + 1, bz), 256, 0, c.stream>>>(T, E, key, ACC, B, l, (int)c.K,
+                                                                              c.logN, c.primes, c.imap_at(l), nint);
     HEC_HIP(hipGetLastError());
 }
 

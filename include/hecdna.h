@@ -167,8 +167,11 @@ int hec_memcpy_d2h(hec_context *ctx, void *dst, const void *src, uint64_t bytes)
  * (average ms per launch written to *ms). */
 int hec_time_ntt_forward(hec_context *ctx, uint64_t *dev_data, uint64_t nlimbs, uint64_t npolys, int reps,
                          double *ms);
-/* Per-kernel-class event timing of the matvec (enable, then read cumulative ms and launch counts). */
-int hec_profile_enable(hec_context *ctx, int on);
+/* Per-kernel-class GPU timing of the engine's phases (ks_intt, ks_modup_a, ks_bmac, ks_moddown, galois,
+ * tensor, relin, rescale, ...).  mode 0 off, 1 event pair + synchronize per phase, 2 asynchronous event
+ * pairs (no host synchronisation inside calls; resolved by hec_profile_read).  Read cumulative ms and
+ * phase counts per class. */
+int hec_profile_enable(hec_context *ctx, int mode);
 int hec_profile_read(hec_context *ctx, const char *kernel_class, double *total_ms, uint64_t *launches);
 
 #ifdef __cplusplus
