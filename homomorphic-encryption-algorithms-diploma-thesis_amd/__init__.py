@@ -18,7 +18,7 @@ import subprocess
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libhecdna.so")
+LIB_PATH = os.environ.get("HECDNA_LIB") or os.path.join(_HERE, "libhecdna.so")  # override: experiments
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "hecdna.h")
 
 _lib = None

@@ -402,7 +402,7 @@ static void ntt_dispatch(Ctx &c, int njobs, const IO1 &first, const IO2 &second)
     case 12: run_ntt2<6, 6, 64, 64, INV>(c, njobs, first, second); break;
     case 13: run_ntt2<7, 6, 32, 64, INV>(c, njobs, first, second); break;
     case 14: run_ntt2<7, 7, 32, 32, INV>(c, njobs, first, second); break;
-    case 15: run_ntt2<8, 7, 16, 32, INV>(c, njobs, first, second); break;
+    case 15: run_ntt2<8, 7, 16, 16, INV>(c, njobs, first, second); break;
     case 16: run_ntt2<8, 8, 16, 16, INV>(c, njobs, first, second); break;
     default: throw std::invalid_argument("poly_modulus_degree must be 2^10 .. 2^16");
     }
@@ -656,15 +656,17 @@ static void run_modup_fused(Ctx &c, const u64 *D, u64 *E, PolyArr T, const u64 *
 
 void ks_modup_mac(Ctx &c, const u64 *D, u64 *E, PolyArr T, const u64 *key, u64 *ACC, int B, int l, int part)
 {
-    // <LOGR, LOGC, pass-A columns per block, fused pass-B chunks per block (256 threads, 8 elements each)>
+    // <LOGR, LOGC, pass-A columns per block, fused pass-B chunks per block>: k_bmac blocks of 64-128
+    // threads (4 chunks at N = 2^15: 110 us per B = 8 call vs 128 / 166 us at 16 / 32 chunks) keep the
+    // serial digit loop of the slow integer-prime blocks short
     switch (c.logN) {
-    case 10: run_modup_fused<5, 5, 32, 32>(c, D, E, T, key, ACC, B, l, part); break;
-    case 11: run_modup_fused<6, 5, 32, 64>(c, D, E, T, key, ACC, B, l, part); break;
-    case 12: run_modup_fused<6, 6, 64, 32>(c, D, E, T, key, ACC, B, l, part); break;
-    case 13: run_modup_fused<7, 6, 32, 32>(c, D, E, T, key, ACC, B, l, part); break;
-    case 14: run_modup_fused<7, 7, 32, 16>(c, D, E, T, key, ACC, B, l, part); break;
-    case 15: run_modup_fused<8, 7, 16, 16>(c, D, E, T, key, ACC, B, l, part); break;
-    case 16: run_modup_fused<8, 8, 16, 8>(c, D, E, T, key, ACC, B, l, part); break;
+    case 10: run_modup_fused<5, 5, 32, 16>(c, D, E, T, key, ACC, B, l, part); break;
+    case 11: run_modup_fused<6, 5, 32, 16>(c, D, E, T, key, ACC, B, l, part); break;
+    case 12: run_modup_fused<6, 6, 64, 8>(c, D, E, T, key, ACC, B, l, part); break;
+    case 13: run_modup_fused<7, 6, 32, 8>(c, D, E, T, key, ACC, B, l, part); break;
+    case 14: run_modup_fused<7, 7, 32, 4>(c, D, E, T, key, ACC, B, l, part); break;
+    case 15: run_modup_fused<8, 7, 16, 4>(c, D, E, T, key, ACC, B, l, part); break;
+    case 16: run_modup_fused<8, 8, 16, 4>(c, D, E, T, key, ACC, B, l, part); break;
     default: throw std::invalid_argument("poly_modulus_degree must be 2^10 .. 2^16");
     }
 }
