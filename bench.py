@@ -110,6 +110,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-diags", type=int, default=48)
     ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--variant", choices=["ctct", "ctpt"], default="ctct",
+                    help="ctct: ciphertext diagonals, the reference's BatchedMatrix::matmul (default); ctpt: "
+                         "plaintext diagonals (multiply_plain, no relinearization; SURVEY 8(f) rank 1)")
     ap.add_argument("--mode", choices=["throughput", "sharded"], default="throughput",
                     help="throughput: replicas, own vectors per rank (the metric, weak scaling); sharded: one "
                          "batch split over ranks by trie subtrees of the diagonals + one RCCL reduce-scatter "
@@ -146,7 +149,14 @@ def main():
         held = set(plan[rank])  # a rank only stores the diagonals of its trie subtrees
     else:
         held = range(args.n)
-    diags = [ctx.ciphertext().fill_uniform(2, L, scale, 10_000 + j) if j in held else None for j in range(args.n)]
+    ctpt = args.variant == "ctpt"
+    if ctpt and sharded:
+        raise SystemExit("--variant ctpt runs in throughput mode")
+    if ctpt:
+        diags = [hec.Plaintext(ctx, None, scale).fill_uniform(L, scale, 10_000 + j) for j in range(args.n)]
+    else:
+        diags = [ctx.ciphertext().fill_uniform(2, L, scale, 10_000 + j) if j in held else None
+                 for j in range(args.n)]
     # sharded: every rank sees the same input batch (same seeds); throughput: own vectors per rank
     cseed = 90_000 + (0 if sharded else 100 * rank)
     cols = [ctx.ciphertext().fill_uniform(2, L, scale, cseed + i) for i in range(args.batch)]
@@ -162,6 +172,8 @@ def main():
     def step():
         if sharded:
             shard.sharded_matvec(ctx, diags, cols, rk, gk, rank, world, plan=plan)
+        elif ctpt:
+            ctx.matmul_diagpt_col(diags, cols, gk, out=outs)
         else:
             ctx.matmul_diag_col(diags, cols, rk, gk, out=outs)
 
@@ -231,7 +243,7 @@ def main():
                 "avg_ms": round(per, 4), "algorithmic_bytes_per_launch": algo}
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not ctpt:
         threads = min(16, os.cpu_count() or 1)
         res, ks_s = cpu_baseline(N, moduli, args.n, args.cpu_sample_diags, threads)
         cpu = {"value": round(1.0 / res[1], 6), "unit": "matvec/s", "cores": 1, "kind": "port",
@@ -247,8 +259,9 @@ def main():
             "value": round(value, 6), "unit": "matvec/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
             "scaling": "strong" if sharded else "weak", "vs_baseline": None, "dtype": "u64", "data": "synthetic",
-            "config": {"workload": f"he_linalg BatchedMatrix::matmul diag x col, {args.n}x{args.n} ct x ct "
-                                   f"matvec, N=2^{args.logn}, L={L}, default Galois keys",
+            "config": {"workload": f"he_linalg BatchedMatrix::matmul diag x col, {args.n}x{args.n} "
+                                   f"{'ct x pt' if ctpt else 'ct x ct'} matvec, N=2^{args.logn}, L={L}, "
+                                   f"default Galois keys",
                        "batch_per_gpu": args.batch, "n": args.n, "key_switches_per_matvec": ks,
                        "parallelism": (f"sharded{world}: diagonals split by rotation-trie subtrees, one RCCL "
                                        f"reduce-scatter of size-3 partials" if sharded else

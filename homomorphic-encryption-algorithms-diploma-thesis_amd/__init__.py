@@ -92,6 +92,8 @@ def lib():
             "hec_rotate_vector_inplace": [vp, vp, C.c_int, vp],
             "hec_apply_galois_inplace": [vp, vp, C.c_uint32, vp],
             "hec_matmul_diag_col": [vp, vp, C.c_uint64, vp, C.c_uint64, vp, vp, vp],
+            "hec_matmul_diagpt_col": [vp, vp, C.c_uint64, vp, C.c_uint64, vp, vp],
+            "hec_plaintext_fill_uniform": [vp, C.c_uint64, C.c_double, C.c_uint64],
             "hec_matmul_diag_col_partial": [vp, vp, C.c_uint64, C.c_uint64, C.c_uint64, vp, C.c_uint64, vp, vp],
             "hec_matmul_diag_col_partial_set": [vp, vp, C.c_uint64, vp, C.c_uint64, vp, C.c_uint64, vp, vp],
             "hec_matmul_finish": [vp, vp, C.c_uint64, vp, vp],
@@ -268,6 +270,13 @@ class Context:
                                          gk.h, self._arr(out)))
         return out
 
+    def matmul_diagpt_col(self, pdiags, cols, gk, out=None):
+        """ct x pt matvec: plaintext diagonals (multiply_plain), one rescale per output, no relin."""
+        out = out or [Ciphertext(self) for _ in cols]
+        _check(lib().hec_matmul_diagpt_col(self.h, self._arr(pdiags), len(pdiags), self._arr(cols), len(cols), gk.h,
+                                           self._arr(out)))
+        return out
+
     def matmul_diag_col_partial(self, diags, j_begin, j_end, cols, gk, out=None):
         out = out or [Ciphertext(self) for _ in cols]
         _check(lib().hec_matmul_diag_col_partial(self.h, self._arr(diags), len(diags), j_begin, j_end,
@@ -411,8 +420,13 @@ class Plaintext:
         h = C.c_void_p()
         _check(lib().hec_plaintext_create(ctx.h, C.byref(h)))
         self.h = h
-        a = np.ascontiguousarray(data, dtype=np.uint64)
-        _check(lib().hec_plaintext_upload(self.h, _p(a), a.shape[0], float(scale)))
+        if data is not None:
+            a = np.ascontiguousarray(data, dtype=np.uint64)
+            _check(lib().hec_plaintext_upload(self.h, _p(a), a.shape[0], float(scale)))
+
+    def fill_uniform(self, level, scale, seed):
+        _check(lib().hec_plaintext_fill_uniform(self.h, level, float(scale), seed))
+        return self
 
     def __del__(self):
         try:

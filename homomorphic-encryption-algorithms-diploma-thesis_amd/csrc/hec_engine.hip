@@ -449,27 +449,38 @@ void walk_trie(Ctx &c, Scratch &s, const RotTrie &t, int node, PolyArr src, int 
 // rotation launch sequence and one key read serve all p columns, and the rotations run over the
 // prefix trie; every out[i] still sums the same terms (modular addition is exact and order free),
 // so the bits equal the reference loop's.
-void matvec_core(hec_context *ctx, const hec_ciphertext *const *diags, std::size_t n,
-                 const std::vector<std::size_t> &js, const hec_ciphertext *const *cols, std::size_t p,
+// diags (ciphertexts) or pdiags (plaintexts, the ct x pt form: multiply_plain, products stay size 2,
+// no relinearization) — exactly one is non-null.
+void matvec_core(hec_context *ctx, const hec_ciphertext *const *diags, const hec_plaintext *const *pdiags,
+                 std::size_t n, const std::vector<std::size_t> &js, const hec_ciphertext *const *cols, std::size_t p,
                  const hec_kswitch_key *rk, const hec_galois_keys *gk, bool finish, hec_ciphertext *const *out)
 {
     Ctx &c = ctx->c;
+    const bool pt = pdiags != nullptr;
     need(n >= 1 && p >= 1 && !js.empty(), "empty matrix operand");
     for (std::size_t j : js) need(j < n, "diagonal index out of range");
     need(gk && gk->ctx == ctx, "galois_keys is not valid for encryption parameters");
-    if (finish) need(rk && rk->ctx == ctx, "relin_keys is not valid for encryption parameters");
+    if (finish && !pt) need(rk && rk->ctx == ctx, "relin_keys is not valid for encryption parameters");
     const std::size_t l = cols[0]->level, N = c.N;
-    for (std::size_t j : js) check_ct(ctx, diags[j]);
     for (std::size_t i = 0; i < p; ++i) check_ct(ctx, cols[i]);
     for (std::size_t i = 0; i < p; ++i) need(cols[i]->size == 2, "encrypted size must be 2");
-    for (std::size_t j : js) need(diags[j]->size == 2, "encrypted size must be 2");
-    for (std::size_t j : js) need(diags[j]->level == l, "encrypted1 and encrypted2 parameter mismatch");
     for (std::size_t i = 0; i < p; ++i) need(cols[i]->level == l, "encrypted1 and encrypted2 parameter mismatch");
-    // scale bookkeeping exactly as multiply_inplace (bound) + add_inplace (are_close) would see it
+    if (pt) {
+        for (std::size_t j : js)
+            need(pdiags[j] && pdiags[j]->ctx == ctx && pdiags[j]->d, "plain is not valid for encryption parameters");
+        for (std::size_t j : js) need(pdiags[j]->level == l, "encrypted_ntt and plain_ntt parameter mismatch");
+    } else {
+        for (std::size_t j : js) check_ct(ctx, diags[j]);
+        for (std::size_t j : js) need(diags[j]->size == 2, "encrypted size must be 2");
+        for (std::size_t j : js) need(diags[j]->level == l, "encrypted1 and encrypted2 parameter mismatch");
+    }
+    auto dscale = [&](std::size_t j) { return pt ? pdiags[j]->scale : diags[j]->scale; };
+    auto ddata = [&](std::size_t j) -> const u64 * { return pt ? pdiags[j]->d : diags[j]->d; };
+    // scale bookkeeping exactly as multiply[_plain]_inplace (bound) + add_inplace (are_close) would see it
     std::vector<double> ps(p);
     for (std::size_t i = 0; i < p; ++i) {
         for (std::size_t k = 0; k < js.size(); ++k) {
-            const double sc = cols[i]->scale * diags[js[k]]->scale;
+            const double sc = cols[i]->scale * dscale(js[k]);
             need(scale_ok(c, sc, l), "scale out of bounds");
             if (k == 0) ps[i] = sc;
             else need(are_close(ps[i], sc), "scale mismatch");
@@ -498,19 +509,21 @@ void matvec_core(hec_context *ctx, const hec_ciphertext *const *diags, std::size
     bool first = true;
     auto visit = [&](std::size_t j, PolyArr src) {
         ProfScope pr(c, "tensor");
-        tensor_acc(c, src, diags[j]->d, l * N, Aa, (int)p, (int)l, first);
+        if (pt) plain_acc(c, src, ddata(j), Aa, (int)p, (int)l, first);
+        else tensor_acc(c, src, ddata(j), l * N, Aa, (int)p, (int)l, first);
         first = false;
     };
     walk_trie(c, s, trie, 0, Xa, 0, (int)p, (int)l, *gk, bufs.data(), S2, visit);
+    const u64 accw = pt ? S2 : S3;  // accumulator words per output
     if (!finish) {
         for (std::size_t i = 0; i < p; ++i) {
-            ensure(out[i], S3);
-            d2d(c, out[i]->d, ACC3 + i * S3, S3);
-            out[i]->size = 3; out[i]->level = l; out[i]->scale = ps[i];
+            ensure(out[i], accw);
+            d2d(c, out[i]->d, ACC3 + i * S3, accw);
+            out[i]->size = pt ? 2 : 3; out[i]->level = l; out[i]->scale = ps[i];
         }
         return;
     }
-    {   // relinearize (SMART_RELIN == 1: once per output) — he_linalg.cpp:1000
+    if (!pt) {  // relinearize (SMART_RELIN == 1: once per output) — he_linalg.cpp:1000
         ProfScope pr(c, "relin");
         keyswitch(c, s, PolyArr{ACC3 + 2 * l * N, S3, 0}, rk->d, Aa, 2, Aa, (int)p, (int)l);
     }
@@ -904,6 +917,24 @@ int hec_plaintext_destroy(hec_plaintext *pt)
         delete pt;
     });
 }
+int hec_plaintext_fill_uniform(hec_plaintext *pt, uint64_t level, double scale, uint64_t seed)
+{
+    return guard([&] {
+        need(pt != nullptr, "null argument");
+        Ctx &c = pt->ctx->c;
+        set_device(pt->ctx);
+        need(level >= 1 && level <= c.L, "plain is not valid for encryption parameters");
+        const std::size_t w = level * c.N;
+        if (pt->cap < w) {
+            if (pt->d) HEC_HIP(hipFree(pt->d));
+            pt->d = dalloc(w);
+            pt->cap = w;
+        }
+        fill_uniform(c, pt->d, 1, (int)level, 0, 0, seed);
+        pt->level = level; pt->scale = scale;
+    });
+}
+
 int hec_plaintext_upload(hec_plaintext *pt, const uint64_t *host, uint64_t level, double scale)
 {
     return guard([&] {
@@ -1223,7 +1254,7 @@ int hec_matmul_diag_col(hec_context *ctx, const hec_ciphertext *const *diags, ui
         need(diags && cols && out, "null argument");
         std::vector<std::size_t> js(n);
         for (std::size_t j = 0; j < n; ++j) js[j] = j;
-        matvec_core(ctx, diags, n, js, cols, p, rk, gk, true, out);
+        matvec_core(ctx, diags, nullptr, n, js, cols, p, rk, gk, true, out);
     });
 }
 
@@ -1237,7 +1268,7 @@ int hec_matmul_diag_col_partial(hec_context *ctx, const hec_ciphertext *const *d
         need(j_begin < j_end && j_end <= n, "empty matrix operand");
         std::vector<std::size_t> js;
         for (uint64_t j = j_begin; j < j_end; ++j) js.push_back(j);
-        matvec_core(ctx, diags, n, js, cols, p, nullptr, gk, false, acc_out);
+        matvec_core(ctx, diags, nullptr, n, js, cols, p, nullptr, gk, false, acc_out);
     });
 }
 
@@ -1251,7 +1282,20 @@ int hec_matmul_diag_col_partial_set(hec_context *ctx, const hec_ciphertext *cons
         std::vector<std::size_t> js(j_idx, j_idx + nj);
         std::sort(js.begin(), js.end());
         need(std::adjacent_find(js.begin(), js.end()) == js.end(), "duplicate diagonal index");
-        matvec_core(ctx, diags, n, js, cols, p, nullptr, gk, false, acc_out);
+        matvec_core(ctx, diags, nullptr, n, js, cols, p, nullptr, gk, false, acc_out);
+    });
+}
+
+int hec_matmul_diagpt_col(hec_context *ctx, const hec_plaintext *const *diags, uint64_t n,
+                          const hec_ciphertext *const *cols, uint64_t p, const hec_galois_keys *gk,
+                          hec_ciphertext *const *out)
+{
+    return guard([&] {
+        set_device(ctx);
+        need(diags && cols && out, "null argument");
+        std::vector<std::size_t> js(n);
+        for (std::size_t j = 0; j < n; ++j) js[j] = j;
+        matvec_core(ctx, nullptr, diags, n, js, cols, p, nullptr, gk, true, out);
     });
 }
 

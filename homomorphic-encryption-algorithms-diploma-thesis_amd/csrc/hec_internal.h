@@ -102,6 +102,8 @@ void divide_round(Ctx &c, const u64 *Y, u64 ysb, u64 ysk, PolyArr X, PolyArr IN,
                   int nk, int nl, int last_idx, const u64 *inv, const u64 *inv_q, u64 *Z);
 void galois_permute(Ctx &c, PolyArr in, PolyArr out, int B, int nk, int nl, u32 elt);
 void tensor_acc(Ctx &c, PolyArr R, const u64 *A, u64 a_sk, PolyArr ACC, int B, int l, bool assign);
+// ct x pt: ACC polys 0, 1 (+)= R[b] (x) P for the B entries (multiply_plain + add_inplace)
+void plain_acc(Ctx &c, PolyArr R, const u64 *P, PolyArr ACC, int B, int l, bool assign);
 void tensor_sum(Ctx &c, PolyArr R, PolyArr A, u64 *ACC, u64 acc_sk, int B, int l);
 void ew_add(Ctx &c, PolyArr a, PolyArr b, PolyArr out, int B, int nk, int nl, int mode);  // 0 add, 1 sub
 void ew_negate(Ctx &c, PolyArr a, int B, int nk, int nl);

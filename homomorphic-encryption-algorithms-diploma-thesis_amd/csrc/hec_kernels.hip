@@ -845,6 +845,37 @@ void tensor_acc(Ctx &c, PolyArr R, const u64 *A, u64 a_sk, PolyArr ACC, int B, i
     HEC_HIP(hipGetLastError());
 }
 
+// ct x pt: ACC[b] polys 0, 1 (+)= R[b] (x) P, SEAL multiply_plain (one Barrett
+// reduction per product) then add_inplace
+__global__ void __launch_bounds__(256)
+    k_plain_acc(PolyArr R, const u64 *__restrict__ P, PolyArr ACC, int B, int logN, u64 total, int assign,
+                const DevPrime *__restrict__ primes)
+{
+    const u64 idx = (u64)blockIdx.x * 256 + threadIdx.x;
+    if (idx >= total) return;
+    const DevPrime pr = primes[idx >> logN];
+    const u64 pv = P[idx];
+    for (int b = 0; b < B; ++b) {
+        const u64 *r = R.p + b * R.sb;
+        const u64 d0 = mulmod(r[idx], pv, pr), d1 = mulmod(r[R.sk + idx], pv, pr);
+        u64 *o = ACC.p + b * ACC.sb;
+        if (assign) {
+            o[idx] = d0; o[ACC.sk + idx] = d1;
+        } else {
+            o[idx] = addmod(o[idx], d0, pr.q);
+            o[ACC.sk + idx] = addmod(o[ACC.sk + idx], d1, pr.q);
+        }
+    }
+}
+
+void plain_acc(Ctx &c, PolyArr R, const u64 *P, PolyArr ACC, int B, int l, bool assign)
+{
+    const u64 total = (u64)l * c.N;
+    k_plain_acc<<<(unsigned)((total + 255) / 256), 256, 0, c.stream>>>(R, P, ACC, B, c.logN, total, assign ? 1 : 0,
+                                                                        c.primes);
+    HEC_HIP(hipGetLastError());
+}
+
 // ACC (size 3) = sum_b R[b] (x) A[b]  (col x col^T form: one output, the batch is the j-sum)
 __global__ void __launch_bounds__(256)
     k_tensor_sum(PolyArr R, PolyArr A, u64 *__restrict__ ACC, u64 acc_sk, int B, int logN, u64 total,

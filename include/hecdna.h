@@ -84,6 +84,8 @@ int hec_ciphertext_fill_uniform(hec_ciphertext *ct, uint64_t size, uint64_t leve
 int hec_plaintext_create(hec_context *ctx, hec_plaintext **out);
 int hec_plaintext_destroy(hec_plaintext *pt);
 int hec_plaintext_upload(hec_plaintext *pt, const uint64_t *host, uint64_t level, double scale);
+/* synthetic NTT-form plaintext: uniform residues mod q_i from a seeded device generator (benchmarks) */
+int hec_plaintext_fill_uniform(hec_plaintext *pt, uint64_t level, double scale, uint64_t seed);
 
 /* ---------------------------------------------------------------- keys -------------------- */
 /* RelinKeys (KeyGenerator::create_relin_keys, matrix_operations.cpp:1061-1062): data u64[L][2][K][N] */
@@ -134,6 +136,14 @@ int hec_matmul_diag_col_partial(hec_context *ctx, const hec_ciphertext *const *d
 int hec_matmul_diag_col_partial_set(hec_context *ctx, const hec_ciphertext *const *diags, uint64_t n,
                                     const uint64_t *j_idx, uint64_t nj, const hec_ciphertext *const *cols, uint64_t p,
                                     const hec_galois_keys *gk, hec_ciphertext *const *acc_out);
+/* ct x pt matvec (the plaintext-diagonal form of BatchedMatrix::matmul diag x col,
+ * he_linalg.cpp:943-1006, with `*= eval % plain` = multiply_plain_inplace, he_operators.cpp:128-142):
+ *   out[i] = rescale_to_next( sum_j diags[j] (x) rot(cols[i], j) )
+ * diags: n NTT-form plaintexts at the columns' level (SEAL CKKSEncoder output layout u64[level][N]).
+ * The products stay size 2, so there is no relinearization; rotations as in hec_matmul_diag_col. */
+int hec_matmul_diagpt_col(hec_context *ctx, const hec_plaintext *const *diags, uint64_t n,
+                          const hec_ciphertext *const *cols, uint64_t p, const hec_galois_keys *gk,
+                          hec_ciphertext *const *out);
 /* relinearize + rescale a batch of size-3 accumulators (he_linalg.cpp:999-1002) */
 int hec_matmul_finish(hec_context *ctx, hec_ciphertext *const *acc, uint64_t p, const hec_kswitch_key *rk,
                       hec_ciphertext *const *out);

@@ -294,3 +294,38 @@ def test_keyswitch_variants_bitexact(orc, hecdna, env):
     got = e.ctx.matmul_diag_col([e.up(a) for a in A], [e.up(x) for x in X], e.rk, e.gk)
     for g, c in zip(got, exp):
         e.same(g, c)
+
+
+def _ctpt_oracle(e, P, pscale, X):
+    """ct x pt matvec composed from pinned oracle ops: out[i] = rescale(sum_j multiply_plain(rot(X[i], j), P[j]))."""
+    outs = []
+    for x in X:
+        acc = None
+        for j, pj in enumerate(P):
+            r = x if j == 0 else e.o.rotate(x, j, e.gk_h)
+            t = e.o.multiply_plain(r, pj, pscale)
+            acc = t if acc is None else e.o.add(acc, t)
+        outs.append(e.o.rescale(acc))
+    return outs
+
+
+@pytest.mark.parametrize("which,n", [("env11", 12), ("env15", 5)])
+def test_matvec_ct_x_pt_bitexact(request, which, n):
+    e = request.getfixturevalue(which)
+    L = len(e.m) - 1
+    pscale = 2.0**40
+    P = [e.o.encode(e.rng.uniform(-1, 1, e.N // 2), pscale, L) for _ in range(n)]
+    X = [e.enc(seed=700 + i) for i in range(2)]
+    exp = _ctpt_oracle(e, P, pscale, X)
+    got = e.ctx.matmul_diagpt_col([e.ctx.plaintext(p, pscale) for p in P], [e.up(x) for x in X], e.gk)
+    for g, c in zip(got, exp):
+        e.same(g, c)
+
+
+def test_matvec_ct_x_pt_errors(env11, hecdna):
+    e = env11
+    L = len(e.m) - 1
+    pts = [e.ctx.plaintext(e.o.encode(e.rng.uniform(-1, 1, e.N // 2), 2.0**40, L - 1), 2.0**40) for _ in range(3)]
+    X = [e.up(e.enc(seed=800))]
+    with pytest.raises(hecdna.InvalidArgument, match="parameter mismatch"):
+        e.ctx.matmul_diagpt_col(pts, X, e.gk)
