@@ -83,6 +83,15 @@ __device__ __forceinline__ void gs_bfly(u64 &X, u64 &Y, u64 w, u64 wq, u64 q, u6
 
 __device__ __forceinline__ u32 bitrev(u32 x, int bits) { return __brev(x) >> (32 - bits); }
 
+// SEAL GaloisTool::apply_galois_ntt source index: out[t] = in[galois_src(t)],
+//   galois_src(t) = bitrev(((elt (2 bitrev(t) + 1)) >> 1) & (N - 1)); elt = 1 is the identity.
+// Adjacent pairs map to adjacent pairs: galois_src(2w + 1) = galois_src(2w) ^ 1.
+__device__ __forceinline__ u32 galois_src(u32 t, u32 elt, int logN)
+{
+    const u32 r = 2u * bitrev(t, logN) + 1u;
+    return bitrev(((elt * r) & ((2u << logN) - 1u)) >> 1, logN);
+}
+
 // ------------------------------------------------------------------ exact FP64 modular arithmetic
 // For q < 2^42 (fp = 1) residues are carried as integer-valued doubles.  gfx950 issues an FP64
 // FMA in 4 cycles per wave vs 8 for a 32-bit integer multiply, and a 64x64->128 product needs

@@ -296,7 +296,10 @@ std::size_t ks_words(const Ctx &c, std::size_t B, std::size_t l)
     return c.N * B * (l + (l + 1) * l + 2 * (l + 1) + 2 * l) + 4 * 64;
 }
 
-void keyswitch(Ctx &c, Scratch &s, PolyArr T, const u64 *key, PolyArr IN, int in_nk, PolyArr OUT, int B, int l)
+// T (the target polys) and IN (added to the output) are read through the Galois permutation of elt
+// (elt = 1: as they are).  OUT must not overlap T or IN when elt != 1 (the reads gather).
+void keyswitch(Ctx &c, Scratch &s, PolyArr T, const u64 *key, PolyArr IN, int in_nk, PolyArr OUT, int B, int l,
+               u32 elt = 1)
 {
     const u64 N = c.N;
     const std::size_t top = s.top;
@@ -306,16 +309,16 @@ void keyswitch(Ctx &c, Scratch &s, PolyArr T, const u64 *key, PolyArr IN, int in
     for (int i = 0; i <= HEC_MAXL; ++i) pmap[i] = i;
     {
         ProfScope ps(c, "ks_intt");
-        ntt_strided(c, true, T.p, T.sb, D, l * N, l, pmap, B * l);
+        ntt_strided(c, true, T.p, T.sb, D, l * N, l, pmap, B * l, elt);
     }
     if (c.fused_modup_mac) {  // mod-up pass A, then pass B fused with the key MAC (no E round trip)
         {
             ProfScope ps(c, "ks_modup_a");
-            ks_modup_mac(c, D, E, T, key, ACC, B, l, 1);
+            ks_modup_mac(c, D, E, T, key, ACC, B, l, 1, elt);
         }
         {
             ProfScope ps(c, "ks_bmac");
-            ks_modup_mac(c, D, E, T, key, ACC, B, l, 2);
+            ks_modup_mac(c, D, E, T, key, ACC, B, l, 2, elt);
         }
     } else {
         {
@@ -324,7 +327,7 @@ void keyswitch(Ctx &c, Scratch &s, PolyArr T, const u64 *key, PolyArr IN, int in
         }
         {
             ProfScope ps(c, "ks_mac");
-            ks_mac(c, T, E, key, ACC, B, l);
+            ks_mac(c, T, E, key, ACC, B, l, elt);
         }
     }
     {
@@ -332,15 +335,23 @@ void keyswitch(Ctx &c, Scratch &s, PolyArr T, const u64 *key, PolyArr IN, int in
         const int pP[1] = {(int)c.K - 1};
         ntt_strided(c, true, ACC + l * N, (l + 1) * N, ACC + l * N, (l + 1) * N, 1, pP, 2 * B);
         divide_round(c, ACC + l * N, 2 * (l + 1) * N, (l + 1) * N, PolyArr{ACC, 2 * (l + 1) * N, (l + 1) * N}, IN,
-                     in_nk, OUT, B, 2, l, (int)c.K - 1, c.p_inv.data(), c.p_inv_q.data(), Z);
+                     in_nk, OUT, B, 2, l, (int)c.K - 1, c.p_inv.data(), c.p_inv_q.data(), Z, elt);
     }
     s.top = top;
 }
 
-// X (size 2) -> OUT = apply_galois(X, elt) followed by key switching; OUT may alias X
+// X (size 2) -> OUT = apply_galois(X, elt) followed by key switching (SEAL apply_galois_inplace).
+// When OUT does not alias X the permutation is applied inside the key switch's loads (the INTT of c1,
+// the target reuse in the MAC, the c0 add in the mod-down) and never materialised; otherwise X is
+// first permuted into scratch.
 void galois_ks(Ctx &c, Scratch &s, PolyArr X, PolyArr OUT, int B, int l, u32 elt, const u64 *key)
 {
     const u64 N = c.N;
+    const bool alias = OUT.p == X.p || !c.fuse_galois;
+    if (!alias) {
+        keyswitch(c, s, PolyArr{X.p + X.sk, X.sb, 0}, key, PolyArr{X.p, X.sb, X.sk}, 1, OUT, B, l, elt);
+        return;
+    }
     const std::size_t top = s.top;
     u64 *S = s.take((u64)2 * B * l * N);
     {
@@ -607,6 +618,7 @@ int hec_context_create(uint64_t N, const uint64_t *mod, uint64_t K, int device, 
         c.device = device;
         if (const char *f = std::getenv("HEC_FUSED_MODUP_MAC")) c.fused_modup_mac = f[0] != '0';
         if (const char *f = std::getenv("HEC_BMAC_KEYS")) c.bmac_keys = f[0] - '0';
+        if (const char *f = std::getenv("HEC_FUSE_GALOIS")) c.fuse_galois = f[0] != '0';
         c.N = N;
         c.logN = __builtin_ctzll(N);
         c.K = K;

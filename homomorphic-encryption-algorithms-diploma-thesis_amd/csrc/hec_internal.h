@@ -67,6 +67,7 @@ struct Ctx {
     std::vector<u64> p_inv, p_inv_q, p_half_mod;            // key switch mod-down (per data prime)
     std::vector<std::vector<u64>> ql_inv, ql_inv_q, ql_half_mod;  // rescale at level l (drop prime l-1)
     int bmac_keys = 1;             // HEC_BMAC_KEYS: k_bmac key loads 0 late / 1 before the rounds / 2 one digit ahead
+    bool fuse_galois = true;       // HEC_FUSE_GALOIS=0: materialise apply_galois before the key switch
     bool fused_modup_mac = true;  // HEC_FUSED_MODUP_MAC=0: separate mod-up pass B and key MAC kernels
     // profiling (ProfScope in hec_engine.hip)
     int prof_mode = 0;  // 0 off, 1 synchronous per scope, 2 asynchronous event pairs
@@ -87,19 +88,22 @@ struct Ctx {
 // ---------------------------------------------------------------- launchers (hec_kernels.hip)
 // Batched NTT: job -> poly = job / nl, limb = job % nl; reads src + poly*ps_src + limb*N, writes
 // dst + poly*ps_dst + limb*N (src may equal dst), prime = pmap[limb].
+// elt != 1: the first pass loads src through the Galois permutation of elt (apply_galois_ntt fused).
 void ntt_strided(Ctx &c, bool inverse, const u64 *src, u64 ps_src, u64 *dst, u64 ps_dst, int nl, const int *pmap,
-                 int njobs);
+                 int njobs, u32 elt = 1);
 // Key-switch phases (B targets at level l; see hec_engine.hip for the dataflow)
 void ks_modup(Ctx &c, const u64 *D, u64 *E, int B, int l);
-void ks_mac(Ctx &c, PolyArr T, const u64 *E, const u64 *key, u64 *ACC, int B, int l);
+void ks_mac(Ctx &c, PolyArr T, const u64 *E, const u64 *key, u64 *ACC, int B, int l, u32 elt);
 // fused: pass A of the mod-up NTTs (part & 1), then (pass B + key MAC) per target prime -> ACC[b][k][I]
 // (part & 2)
-void ks_modup_mac(Ctx &c, const u64 *D, u64 *E, PolyArr T, const u64 *key, u64 *ACC, int B, int l, int part);
+void ks_modup_mac(Ctx &c, const u64 *D, u64 *E, PolyArr T, const u64 *key, u64 *ACC, int B, int l, int part,
+                  u32 elt);
 // divide-and-round by `last_idx` prime: Y = coefficient-form last limb per (b,k) (address Y + b*ysb + k*ysk),
 // X / IN / OUT addressed (b,k,i), nk polys per batch entry, nl output limbs.
 //   OUT = IN + (X - NTT(corr)) * inv   (IN optional; inv = last^-1 mod q_i)
+// in_elt != 1: IN is read through the Galois permutation of in_elt
 void divide_round(Ctx &c, const u64 *Y, u64 ysb, u64 ysk, PolyArr X, PolyArr IN, int in_nk, PolyArr OUT, int B,
-                  int nk, int nl, int last_idx, const u64 *inv, const u64 *inv_q, u64 *Z);
+                  int nk, int nl, int last_idx, const u64 *inv, const u64 *inv_q, u64 *Z, u32 in_elt = 1);
 void galois_permute(Ctx &c, PolyArr in, PolyArr out, int B, int nk, int nl, u32 elt);
 void tensor_acc(Ctx &c, PolyArr R, const u64 *A, u64 a_sk, PolyArr ACC, int B, int l, bool assign);
 // ct x pt: ACC polys 0, 1 (+)= R[b] (x) P for the B entries (multiply_plain + add_inplace)

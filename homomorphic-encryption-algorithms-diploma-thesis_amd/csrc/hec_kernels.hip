@@ -18,26 +18,31 @@
 namespace hec {
 
 // =============================================================================== NTT IO ====
-struct StridedIO {  // job -> (poly = job / nl, limb = job % nl); src/dst may alias (in place)
+// job -> (poly = job / nl, limb = job % nl); src/dst may alias (in place).  elt != 1 loads through the
+// Galois permutation (apply_galois_ntt fused into the load: src[galois_src(g)]).
+struct StridedIO {
     const u64 *src;
     u64 *dst;
     u64 ps_src, ps_dst;
     int nl, logN;
+    u32 elt;
     int pmap[HEC_MAXL + 1];
     struct Bound {
         const u64 *s;
         u64 *d;
         int prime;
+        u32 elt;
+        int logN;
         struct Pre {};
         __device__ Pre pre(u64) const { return {}; }
-        __device__ u64 load(u64 g) const { return s[g]; }
+        __device__ u64 load(u64 g) const { return s[elt == 1 ? g : galois_src((u32)g, elt, logN)]; }
         __device__ void store(u64 g, u64 v, Pre) const { d[g] = v; }
     };
     __device__ Bound bind(int job) const
     {
         const int poly = job / nl, limb = job % nl;
         return Bound{src + (u64)poly * ps_src + ((u64)limb << logN), dst + (u64)poly * ps_dst + ((u64)limb << logN),
-                     pmap[limb]};
+                     pmap[limb], elt, logN};
     }
 };
 
@@ -140,6 +145,7 @@ struct DivRoundIO_B {
     u64 *Z;
     PolyArr X, IN, OUT;
     int nk, nl, logN, in_nk;  // IN is added for polys k < in_nk only
+    u32 elt;                  // IN is read through the Galois permutation (elt != 1)
     const DevPrime *primes;
     u64 inv[HEC_MAXL], inv_q[HEC_MAXL];
     struct Bound {
@@ -147,10 +153,15 @@ struct DivRoundIO_B {
         u64 *out;
         u64 q, w, wq;
         int prime;
+        u32 elt;
+        int logN;
         struct Pre {  // operands of the post-op, loaded before the butterfly rounds
             u64 x, in;
         };
-        __device__ Pre pre(u64 g) const { return Pre{x[g], in ? in[g] : 0}; }
+        __device__ Pre pre(u64 g) const
+        {
+            return Pre{x[g], in ? in[elt == 1 ? g : galois_src((u32)g, elt, logN)] : 0};
+        }
         __device__ u64 load(u64 g) const { return z[g]; }
         __device__ void store(u64 g, u64 v, Pre p) const
         {
@@ -165,7 +176,7 @@ struct DivRoundIO_B {
         const u64 li = (u64)i << logN;
         return Bound{Z + ((u64)job << logN), X.p + b * X.sb + k * X.sk + li,
                      (IN.p && k < in_nk) ? IN.p + b * IN.sb + k * IN.sk + li : nullptr, OUT.p + b * OUT.sb + k * OUT.sk + li,
-                     primes[i].q, inv[i], inv_q[i], i};
+                     primes[i].q, inv[i], inv_q[i], i, elt, logN};
     }
 };
 
@@ -408,19 +419,20 @@ static void ntt_dispatch(Ctx &c, int njobs, const IO1 &first, const IO2 &second)
     }
 }
 
-static StridedIO strided(const u64 *src, u64 *dst, u64 ps_src, u64 ps_dst, int nl, int logN, const int *pmap)
+static StridedIO strided(const u64 *src, u64 *dst, u64 ps_src, u64 ps_dst, int nl, int logN, const int *pmap,
+                         u32 elt = 1)
 {
     StridedIO io{};
-    io.src = src; io.dst = dst; io.ps_src = ps_src; io.ps_dst = ps_dst; io.nl = nl; io.logN = logN;
+    io.src = src; io.dst = dst; io.ps_src = ps_src; io.ps_dst = ps_dst; io.nl = nl; io.logN = logN; io.elt = elt;
     for (int i = 0; i < nl && i <= HEC_MAXL; ++i) io.pmap[i] = pmap[i];
     return io;
 }
 
 void ntt_strided(Ctx &c, bool inverse, const u64 *src, u64 ps_src, u64 *dst, u64 ps_dst, int nl, const int *pmap,
-                 int njobs)
+                 int njobs, u32 elt)
 {
     if (nl > HEC_MAXL + 1) throw std::invalid_argument("too many limbs");
-    const StridedIO first = strided(src, dst, ps_src, ps_dst, nl, c.logN, pmap);
+    const StridedIO first = strided(src, dst, ps_src, ps_dst, nl, c.logN, pmap, elt);
     const StridedIO second = strided(dst, dst, ps_dst, ps_dst, nl, c.logN, pmap);
     if (inverse) ntt_dispatch<true>(c, njobs, first, second);
     else ntt_dispatch<false>(c, njobs, first, second);
@@ -435,7 +447,7 @@ void ks_modup(Ctx &c, const u64 *D, u64 *E, int B, int l)
 }
 
 void divide_round(Ctx &c, const u64 *Y, u64 ysb, u64 ysk, PolyArr X, PolyArr IN, int in_nk, PolyArr OUT, int B,
-                  int nk, int nl, int last_idx, const u64 *inv, const u64 *inv_q, u64 *Z)
+                  int nk, int nl, int last_idx, const u64 *inv, const u64 *inv_q, u64 *Z, u32 in_elt)
 {
     if (nl > HEC_MAXL) throw std::invalid_argument("too many limbs");
     DivRoundIO_A a{};
@@ -443,7 +455,7 @@ void divide_round(Ctx &c, const u64 *Y, u64 ysb, u64 ysk, PolyArr X, PolyArr IN,
     a.last = c.q[last_idx]; a.half = a.last >> 1; a.primes = c.primes;
     for (int i = 0; i < nl; ++i) a.fix[i] = c.q[i] - (a.half % c.q[i]);
     DivRoundIO_B b{};
-    b.Z = Z; b.X = X; b.IN = IN; b.OUT = OUT; b.nk = nk; b.nl = nl; b.logN = c.logN; b.in_nk = in_nk;
+    b.Z = Z; b.X = X; b.IN = IN; b.OUT = OUT; b.nk = nk; b.nl = nl; b.logN = c.logN; b.in_nk = in_nk; b.elt = in_elt;
     b.primes = c.primes;
     for (int i = 0; i < nl; ++i) { b.inv[i] = inv[i]; b.inv_q[i] = inv_q[i]; }
     ntt_dispatch<false>(c, B * nk * nl, a, b);
@@ -468,7 +480,7 @@ void divide_round(Ctx &c, const u64 *Y, u64 ysb, u64 ysk, PolyArr X, PolyArr IN,
 template <int LOGP, int NSEG, int EPT, bool FP, int KEYM>
 __device__ __forceinline__ void bmac_body(u64 *lds, u64 *ltw, PolyArr T, const u64 *__restrict__ E, const u64 *__restrict__ key,
                                           u64 *__restrict__ ACC, const TwTables &tt, const DevPrime &pr, int I, int kI,
-                                          int b, int xb, int logN, int l, int K)
+                                          int b, int xb, int logN, int l, int K, u32 elt)
 {
     constexpr int P = 1 << LOGP, THREADS = NSEG * P / EPT, LD = P + 1, TWS = 2 * P + 2;
     const u64 N = 1ull << logN;
@@ -520,6 +532,17 @@ __device__ __forceinline__ void bmac_body(u64 *lds, u64 *ltw, PolyArr T, const u
     // digit tiles move as 16-B pairs: pair w = threadIdx.x + e THREADS holds block elements 2w, 2w + 1
     u64 nx[EPT];
     auto load_tile = [&](int J) {
+        if (J == I && elt != 1) {  // the NTT-form target through the Galois permutation (pairs stay pairs)
+            const u64 *sp = src(J);
+#pragma unroll
+            for (int e = 0; e < EPT / 2; ++e) {
+                const u32 t = galois_src((u32)(base + 2 * (threadIdx.x + e * THREADS)), elt, logN);
+                const ulonglong2 w = *(const ulonglong2 *)(sp + (t & ~1u));
+                nx[2 * e] = (t & 1) ? w.y : w.x;
+                nx[2 * e + 1] = (t & 1) ? w.x : w.y;
+            }
+            return;
+        }
         const ulonglong2 *sp = (const ulonglong2 *)(src(J) + base);
 #pragma unroll
         for (int e = 0; e < EPT / 2; ++e) {
@@ -602,7 +625,7 @@ template <int LOGP, int NSEG, int EPT, int KEYM>
 __global__ void __launch_bounds__(NSEG *(1 << LOGP) / EPT)
     k_bmac(PolyArr T, const u64 *__restrict__ E, const u64 *__restrict__ key, u64 *__restrict__ ACC, TwTables tt,
            const DevPrime *__restrict__ primes, const int *__restrict__ Imap, int logN, int l, int K, int nint,
-           int gpad)
+           int gpad, u32 elt)
 {
     __shared__ u64 lds[NSEG * ((1 << LOGP) + 1)];
     __shared__ u64 ltw[NSEG * (2 * (1 << LOGP) + 2)];
@@ -618,14 +641,14 @@ __global__ void __launch_bounds__(NSEG *(1 << LOGP) / EPT)
     const int kI = I == l ? K - 1 : I;
     const DevPrime pr = primes[kI];
     if (yi < nint)
-        bmac_body<LOGP, NSEG, EPT, false, KEYM>(lds, ltw, T, E, key, ACC, tt, pr, I, kI, b, xb, logN, l, K);
+        bmac_body<LOGP, NSEG, EPT, false, KEYM>(lds, ltw, T, E, key, ACC, tt, pr, I, kI, b, xb, logN, l, K, elt);
     else
-        bmac_body<LOGP, NSEG, EPT, true, KEYM>(lds, ltw, T, E, key, ACC, tt, pr, I, kI, b, xb, logN, l, K);
+        bmac_body<LOGP, NSEG, EPT, true, KEYM>(lds, ltw, T, E, key, ACC, tt, pr, I, kI, b, xb, logN, l, K, elt);
 }
 
 template <int LOGR, int LOGC, int NA, int NB2>
 static void run_modup_fused(Ctx &c, const u64 *D, u64 *E, PolyArr T, const u64 *key, u64 *ACC, int B, int l,
-                            int part)
+                            int part, u32 elt)
 {
     constexpr int R = 1 << LOGR, C = 1 << LOGC, EPT = 8;
     const TwTables fwd{c.tw, c.twb, c.twf, c.twbf};
@@ -647,26 +670,27 @@ static void run_modup_fused(Ctx &c, const u64 *D, u64 *E, PolyArr T, const u64 *
     const int groups = X * (l + 1), gpad = (groups + 7) / 8 * 8;
     const dim3 grid(gpad * B);
     switch (c.bmac_keys) {  // key loads: 0 after the rounds, 1 before them, 2 one digit ahead
-    case 0: k_bmac<LOGC, NB2, EPT, 0><<<grid, TB, 0, c.stream>>>(T, E, key, ACC, fwd, c.primes, dm, c.logN, l, (int)c.K, nint, gpad); break;
-    case 1: k_bmac<LOGC, NB2, EPT, 1><<<grid, TB, 0, c.stream>>>(T, E, key, ACC, fwd, c.primes, dm, c.logN, l, (int)c.K, nint, gpad); break;
-    default: k_bmac<LOGC, NB2, EPT, 2><<<grid, TB, 0, c.stream>>>(T, E, key, ACC, fwd, c.primes, dm, c.logN, l, (int)c.K, nint, gpad); break;
+    case 0: k_bmac<LOGC, NB2, EPT, 0><<<grid, TB, 0, c.stream>>>(T, E, key, ACC, fwd, c.primes, dm, c.logN, l, (int)c.K, nint, gpad, elt); break;
+    case 1: k_bmac<LOGC, NB2, EPT, 1><<<grid, TB, 0, c.stream>>>(T, E, key, ACC, fwd, c.primes, dm, c.logN, l, (int)c.K, nint, gpad, elt); break;
+    default: k_bmac<LOGC, NB2, EPT, 2><<<grid, TB, 0, c.stream>>>(T, E, key, ACC, fwd, c.primes, dm, c.logN, l, (int)c.K, nint, gpad, elt); break;
     }
     HEC_HIP(hipGetLastError());
 }
 
-void ks_modup_mac(Ctx &c, const u64 *D, u64 *E, PolyArr T, const u64 *key, u64 *ACC, int B, int l, int part)
+void ks_modup_mac(Ctx &c, const u64 *D, u64 *E, PolyArr T, const u64 *key, u64 *ACC, int B, int l, int part,
+                  u32 elt)
 {
     // <LOGR, LOGC, pass-A columns per block, fused pass-B chunks per block>: k_bmac blocks of 64-128
     // threads (4 chunks at N = 2^15: 110 us per B = 8 call vs 128 / 166 us at 16 / 32 chunks) keep the
     // serial digit loop of the slow integer-prime blocks short
     switch (c.logN) {
-    case 10: run_modup_fused<5, 5, 32, 16>(c, D, E, T, key, ACC, B, l, part); break;
-    case 11: run_modup_fused<6, 5, 32, 16>(c, D, E, T, key, ACC, B, l, part); break;
-    case 12: run_modup_fused<6, 6, 64, 8>(c, D, E, T, key, ACC, B, l, part); break;
-    case 13: run_modup_fused<7, 6, 32, 8>(c, D, E, T, key, ACC, B, l, part); break;
-    case 14: run_modup_fused<7, 7, 32, 4>(c, D, E, T, key, ACC, B, l, part); break;
-    case 15: run_modup_fused<8, 7, 16, 4>(c, D, E, T, key, ACC, B, l, part); break;
-    case 16: run_modup_fused<8, 8, 16, 4>(c, D, E, T, key, ACC, B, l, part); break;
+    case 10: run_modup_fused<5, 5, 32, 16>(c, D, E, T, key, ACC, B, l, part, elt); break;
+    case 11: run_modup_fused<6, 5, 32, 16>(c, D, E, T, key, ACC, B, l, part, elt); break;
+    case 12: run_modup_fused<6, 6, 64, 8>(c, D, E, T, key, ACC, B, l, part, elt); break;
+    case 13: run_modup_fused<7, 6, 32, 8>(c, D, E, T, key, ACC, B, l, part, elt); break;
+    case 14: run_modup_fused<7, 7, 32, 4>(c, D, E, T, key, ACC, B, l, part, elt); break;
+    case 15: run_modup_fused<8, 7, 16, 4>(c, D, E, T, key, ACC, B, l, part, elt); break;
+    case 16: run_modup_fused<8, 8, 16, 4>(c, D, E, T, key, ACC, B, l, part, elt); break;
     default: throw std::invalid_argument("poly_modulus_degree must be 2^10 .. 2^16");
     }
 }
@@ -678,10 +702,11 @@ void ks_modup_mac(Ctx &c, const u64 *D, u64 *E, PolyArr T, const u64 *key, u64 *
 template <int BT>
 __device__ __forceinline__ void ks_mac_int(PolyArr T, const u64 *__restrict__ E, const u64 *__restrict__ key,
                                            u64 *__restrict__ ACC, int B, int l, int K, int logN,
-                                           const DevPrime *__restrict__ primes, int I)
+                                           const DevPrime *__restrict__ primes, int I, u32 elt)
 {
     const u64 N = 1ull << logN;
     const u64 g = (u64)blockIdx.x * 256 + threadIdx.x;
+    const u64 tg = elt == 1 ? g : galois_src((u32)g, elt, logN);
     const int b0 = blockIdx.z * BT;
     const int kI = I == l ? K - 1 : I;
     const DevPrime pr = primes[kI];
@@ -695,7 +720,7 @@ __device__ __forceinline__ void ks_mac_int(PolyArr T, const u64 *__restrict__ E,
         for (int t = 0; t < BT; ++t) {
             const int b = b0 + t;
             if (b < B) {
-                const u64 e = (I == J) ? T.p[b * T.sb + (u64)J * N + g]
+                const u64 e = (I == J) ? T.p[b * T.sb + (u64)J * N + tg]
                                        : E[((u64)((b * (l + 1) + I) * l + J) << logN) + g];
                 mac128(a0[t], e, k0);
                 mac128(a1[t], e, k1);
@@ -717,7 +742,7 @@ __device__ __forceinline__ void ks_mac_int(PolyArr T, const u64 *__restrict__ E,
 template <int BT>
 __device__ __forceinline__ void ks_mac_fp(PolyArr T, const u64 *__restrict__ E, const u64 *__restrict__ key,
                                           u64 *__restrict__ ACC, int B, int l, int K, int logN,
-                                          const DevPrime *__restrict__ primes, int I)
+                                          const DevPrime *__restrict__ primes, int I, u32 elt)
 {
     const u64 N = 1ull << logN;
     if ((u64)blockIdx.x * 512 >= N) return;  // FP blocks own two coefficients per thread
@@ -736,8 +761,14 @@ __device__ __forceinline__ void ks_mac_fp(PolyArr T, const u64 *__restrict__ E, 
         for (int t = 0; t < BT; ++t) {
             const int b = b0 + t;
             if (b < B) {
-                const ulonglong2 e = (I == J) ? *(const ulonglong2 *)(T.p + b * T.sb + (u64)J * N + g)
-                                              : *(const ulonglong2 *)(E + (((u64)((b * (l + 1) + I) * l + J)) << logN) + g);
+                ulonglong2 e;
+                if (I == J) {
+                    const u64 *tp = T.p + b * T.sb + (u64)J * N;
+                    e = elt == 1 ? *(const ulonglong2 *)(tp + g)
+                                 : ulonglong2{tp[galois_src((u32)g, elt, logN)], tp[galois_src((u32)g + 1, elt, logN)]};
+                } else {
+                    e = *(const ulonglong2 *)(E + (((u64)((b * (l + 1) + I) * l + J)) << logN) + g);
+                }
                 const double e0 = u2d(e.x), e1 = u2d(e.y);
                 a0[t][0] += fp_mulmod(e0, k00, pr.qd, pr.qinv);
                 a0[t][1] += fp_mulmod(e1, k01, pr.qd, pr.qinv);
@@ -762,20 +793,20 @@ __device__ __forceinline__ void ks_mac_fp(PolyArr T, const u64 *__restrict__ E, 
 template <int BT>
 __global__ void __launch_bounds__(256)
     k_ks_mac(PolyArr T, const u64 *__restrict__ E, const u64 *__restrict__ key, u64 *__restrict__ ACC, int B, int l,
-             int K, int logN, const DevPrime *__restrict__ primes, const int *__restrict__ Imap, int nint)
+             int K, int logN, const DevPrime *__restrict__ primes, const int *__restrict__ Imap, int nint, u32 elt)
 {
     const int I = Imap[blockIdx.y];
-    if ((int)blockIdx.y < nint) ks_mac_int<BT>(T, E, key, ACC, B, l, K, logN, primes, I);
-    else ks_mac_fp<BT>(T, E, key, ACC, B, l, K, logN, primes, I);
+    if ((int)blockIdx.y < nint) ks_mac_int<BT>(T, E, key, ACC, B, l, K, logN, primes, I, elt);
+    else ks_mac_fp<BT>(T, E, key, ACC, B, l, K, logN, primes, I, elt);
 }
 
-void ks_mac(Ctx &c, PolyArr T, const u64 *E, const u64 *key, u64 *ACC, int B, int l)
+void ks_mac(Ctx &c, PolyArr T, const u64 *E, const u64 *key, u64 *ACC, int B, int l, u32 elt)
 {
     constexpr int BT = 8;
     const int nint = c.imap_nint[l];
     const unsigned bz = (B + BT - 1) / BT;
     k_ks_mac<BT><<<dim3((unsigned)(c.N / 256), l + 1, bz), 256, 0, c.stream>>>(T, E, key, ACC, B, l, (int)c.K,
-                                                                              c.logN, c.primes, c.imap_at(l), nint);
+                                                                              c.logN, c.primes, c.imap_at(l), nint, elt);
     HEC_HIP(hipGetLastError());
 }
 
