@@ -56,7 +56,7 @@ def pmc_traffic(cls, B, logn, level):
     """HBM bytes per launch of the roofline kernel from the committed rocprofv3 PMC passes
     (profiles/r01_pmc_k_bmac.json: FETCH_SIZE and WRITE_SIZE in separate passes, gfx950 FETCH x2
     correction for its 16-B/lane reads), when they were taken at this configuration; else None."""
-    path = os.path.join(ROOT, "profiles", "r01_pmc_k_bmac.json")
+    path = os.path.join(ROOT, "profiles", f"r01_pmc_k_bmac_B{B}.json")
     if cls != "ks_bmac" or not os.path.exists(path):
         return None
     p = json.load(open(path))
@@ -104,7 +104,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--batch", type=int, default=8, help="input vectors per GPU per step (p)")
+    ap.add_argument("--batch", type=int, default=32, help="input vectors per GPU per step (p)")
     ap.add_argument("--n", type=int, default=4096, help="matrix dimension (diagonals)")
     ap.add_argument("--logn", type=int, default=15)
     ap.add_argument("--no-cpu-baseline", action="store_true")
