@@ -619,6 +619,7 @@ int hec_context_create(uint64_t N, const uint64_t *mod, uint64_t K, int device, 
         if (const char *f = std::getenv("HEC_FUSED_MODUP_MAC")) c.fused_modup_mac = f[0] != '0';
         if (const char *f = std::getenv("HEC_BMAC_KEYS")) c.bmac_keys = f[0] - '0';
         if (const char *f = std::getenv("HEC_FUSE_GALOIS")) c.fuse_galois = f[0] != '0';
+        if (const char *f = std::getenv("HEC_SPLIT_CLASSES")) c.split_classes = f[0] - '0';
         c.N = N;
         c.logN = __builtin_ctzll(N);
         c.K = K;

@@ -67,6 +67,8 @@ struct Ctx {
     std::vector<u64> p_inv, p_inv_q, p_half_mod;            // key switch mod-down (per data prime)
     std::vector<std::vector<u64>> ql_inv, ql_inv_q, ql_half_mod;  // rescale at level l (drop prime l-1)
     int bmac_keys = 1;             // HEC_BMAC_KEYS: k_bmac key loads 0 late / 1 before the rounds / 2 one digit ahead
+    int split_classes = 0;         // HEC_SPLIT_CLASSES: mod-up A / k_bmac as one mixed launch (0), FP64 and
+                                   // integer launches on one stream (1) or on two streams (2)
     bool fuse_galois = true;       // HEC_FUSE_GALOIS=0: materialise apply_galois before the key switch
     bool fused_modup_mac = true;  // HEC_FUSED_MODUP_MAC=0: separate mod-up pass B and key MAC kernels
     // profiling (ProfScope in hec_engine.hip)

@@ -15,6 +15,8 @@
 // small IO functors, so the key switch never materialises them separately.
 #include "hec_internal.h"
 
+#include <type_traits>
+
 namespace hec {
 
 // =============================================================================== NTT IO ====
@@ -33,6 +35,7 @@ struct StridedIO {
         int prime;
         u32 elt;
         int logN;
+        bool valid = true;
         struct Pre {};
         __device__ Pre pre(u64) const { return {}; }
         __device__ u64 load(u64 g) const { return s[elt == 1 ? g : galois_src((u32)g, elt, logN)]; }
@@ -48,10 +51,21 @@ struct StridedIO {
 
 // Key-switch mod-up: job t -> (b, I, J), I in [0, l] (I == l is the special prime P), J in [0, l),
 // I != J.  E layout [b][I][J][N].
+// With Il set (a class-filtered launch) job -> (b, I = Il[.], J in [0, l)), the J == I jobs being empty.
 struct ModUpMap {
     int l, logN, kP;
+    const int *Il = nullptr;
+    int nI = 0;
     __device__ void map(int job, int &b, int &I, int &J) const
     {
+        if (Il) {
+            const int per = nI * l;
+            b = job / per;
+            const int t = job % per;
+            I = Il[t / l];
+            J = t % l;
+            return;
+        }
         const int per = l * l;
         b = job / per;
         const int t = job % per;
@@ -76,6 +90,7 @@ struct ModUpIO_A {  // load digit J (coefficient form, canonical mod q_J) reduce
         u64 *d;
         u64 q, r1;
         int prime;
+        bool valid = true;
         struct Pre {};
         __device__ Pre pre(u64) const { return {}; }
         __device__ u64 load(u64 g) const { return barrett64(s[g], q, r1); }
@@ -86,7 +101,7 @@ struct ModUpIO_A {  // load digit J (coefficient form, canonical mod q_J) reduce
         int b, I, J;
         m.map(job, b, I, J);
         const int p = I == m.l ? m.kP : I;
-        return Bound{D + ((u64)(b * m.l + J) << m.logN), E + m.eoff(b, I, J), primes[p].q, primes[p].r1, p};
+        return Bound{D + ((u64)(b * m.l + J) << m.logN), E + m.eoff(b, I, J), primes[p].q, primes[p].r1, p, I != J};
     }
 };
 struct ModUpIO_B {
@@ -95,6 +110,7 @@ struct ModUpIO_B {
     struct Bound {
         u64 *p;
         int prime;
+        bool valid = true;
         struct Pre {};
         __device__ Pre pre(u64) const { return {}; }
         __device__ u64 load(u64 g) const { return p[g]; }
@@ -104,7 +120,7 @@ struct ModUpIO_B {
     {
         int b, I, J;
         m.map(job, b, I, J);
-        return Bound{E + m.eoff(b, I, J), I == m.l ? m.kP : I};
+        return Bound{E + m.eoff(b, I, J), I == m.l ? m.kP : I, I != J};
     }
 };
 
@@ -125,6 +141,7 @@ struct DivRoundIO_A {
         u64 *z;
         u64 last, half, q, r1, fix;
         int prime;
+        bool valid = true;
         struct Pre {};
         __device__ Pre pre(u64) const { return {}; }
         __device__ u64 load(u64 g) const
@@ -155,6 +172,7 @@ struct DivRoundIO_B {
         int prime;
         u32 elt;
         int logN;
+        bool valid = true;
         struct Pre {  // operands of the post-op, loaded before the butterfly rounds
             u64 x, in;
         };
@@ -372,15 +390,20 @@ __device__ __forceinline__ void ntt_pass_body(u64 *lds, const Bound &bio, const 
     }
 }
 
-template <int LOGP, int NSEG, bool INV, bool PASS_A, bool FINAL, class IO>
+// CLS 0: per-block branch on the prime's arithmetic class; 1 / 2: an FP64-only / integer-only launch
+// (a smaller register budget for the FP64 kernel when a launch's jobs are all of one class)
+template <int LOGP, int NSEG, bool INV, bool PASS_A, bool FINAL, class IO, int CLS = 0>
 __global__ void __launch_bounds__(NSEG *(1 << LOGP) / 16)
     k_ntt(const IO io, TwTables tt, const DevPrime *__restrict__ primes, int logN)
 {
     static_assert(LOGP >= 5 && LOGP <= 8, "two rounds of 4 stages");
     __shared__ u64 lds[PASS_A ? (1 << LOGP) * (NSEG + 1) : NSEG * ((1 << LOGP) + 1)];
     const auto bio = io.bind(blockIdx.y);
+    if (!bio.valid) return;  // uniform per block
     const DevPrime pr = primes[bio.prime];
-    if (pr.fp) ntt_pass_body<LOGP, NSEG, INV, PASS_A, FINAL, true>(lds, bio, pr, tt, logN);
+    if constexpr (CLS == 1) ntt_pass_body<LOGP, NSEG, INV, PASS_A, FINAL, true>(lds, bio, pr, tt, logN);
+    else if constexpr (CLS == 2) ntt_pass_body<LOGP, NSEG, INV, PASS_A, FINAL, false>(lds, bio, pr, tt, logN);
+    else if (pr.fp) ntt_pass_body<LOGP, NSEG, INV, PASS_A, FINAL, true>(lds, bio, pr, tt, logN);
     else ntt_pass_body<LOGP, NSEG, INV, PASS_A, FINAL, false>(lds, bio, pr, tt, logN);
 }
 
@@ -621,11 +644,13 @@ __device__ __forceinline__ void bmac_body(u64 *lds, u64 *ltw, PolyArr T, const u
 }
 
 // one launch: blockIdx.y < nint -> integer target primes, the rest FP64 (blocks of both kinds overlap)
-template <int LOGP, int NSEG, int EPT, int KEYM>
+// CLS 0: Imap lists every target prime, the first nint integer ones (per-block branch); CLS 1 / 2: an
+// FP64-only / integer-only launch over the nI primes of Imap (FP64-only: 162 VGPRs, 3 waves/SIMD).
+template <int LOGP, int NSEG, int EPT, int KEYM, int CLS>
 __global__ void __launch_bounds__(NSEG *(1 << LOGP) / EPT)
     k_bmac(PolyArr T, const u64 *__restrict__ E, const u64 *__restrict__ key, u64 *__restrict__ ACC, TwTables tt,
-           const DevPrime *__restrict__ primes, const int *__restrict__ Imap, int logN, int l, int K, int nint,
-           int gpad, u32 elt)
+           const DevPrime *__restrict__ primes, const int *__restrict__ Imap, int nI, int logN, int l, int K,
+           int nint, int gpad, u32 elt)
 {
     __shared__ u64 lds[NSEG * ((1 << LOGP) + 1)];
     __shared__ u64 ltw[NSEG * (2 * (1 << LOGP) + 2)];
@@ -635,15 +660,38 @@ __global__ void __launch_bounds__(NSEG *(1 << LOGP) / EPT)
     const int w = blockIdx.x, B = gridDim.x / gpad;
     const int g8 = w & 7, rest = w >> 3, b = rest % B, G = (rest / B) * 8 + g8;
     const int X = (1 << (logN - LOGP)) / NSEG;
-    if (G >= X * (l + 1)) return;
+    if (G >= X * nI) return;
     const int yi = G / X, xb = G % X;
     const int I = Imap[yi];
     const int kI = I == l ? K - 1 : I;
     const DevPrime pr = primes[kI];
-    if (yi < nint)
+    if constexpr (CLS == 1)
+        bmac_body<LOGP, NSEG, EPT, true, KEYM>(lds, ltw, T, E, key, ACC, tt, pr, I, kI, b, xb, logN, l, K, elt);
+    else if constexpr (CLS == 2)
+        bmac_body<LOGP, NSEG, EPT, false, KEYM>(lds, ltw, T, E, key, ACC, tt, pr, I, kI, b, xb, logN, l, K, elt);
+    else if (yi < nint)
         bmac_body<LOGP, NSEG, EPT, false, KEYM>(lds, ltw, T, E, key, ACC, tt, pr, I, kI, b, xb, logN, l, K, elt);
     else
         bmac_body<LOGP, NSEG, EPT, true, KEYM>(lds, ltw, T, E, key, ACC, tt, pr, I, kI, b, xb, logN, l, K, elt);
+}
+
+// fork -> (integer-class launch on the side stream) || (FP64-class launch on the main stream) -> join,
+// or both in order on the main stream
+template <class FI, class FF>
+static void dual(Ctx &c, bool two_streams, const FI &launch_int, const FF &launch_fp)
+{
+    if (two_streams) {
+        HEC_HIP(hipEventRecord(c.ev_fork, c.stream));
+        HEC_HIP(hipStreamWaitEvent(c.side, c.ev_fork, 0));
+        launch_int(c.side);
+        HEC_HIP(hipEventRecord(c.ev_join, c.side));
+        launch_fp(c.stream);
+        HEC_HIP(hipStreamWaitEvent(c.stream, c.ev_join, 0));
+    } else {
+        launch_int(c.stream);
+        launch_fp(c.stream);
+    }
+    HEC_HIP(hipGetLastError());
 }
 
 template <int LOGR, int LOGC, int NA, int NB2>
@@ -653,27 +701,52 @@ static void run_modup_fused(Ctx &c, const u64 *D, u64 *E, PolyArr T, const u64 *
     constexpr int R = 1 << LOGR, C = 1 << LOGC, EPT = 8;
     const TwTables fwd{c.tw, c.twb, c.twf, c.twbf};
     // (2a) pass A of every mod-up NTT (B * l * l jobs), output E[b][I][J] (lazy, pass-A domain)
+    const int nint = c.imap_nint[l], nfp = l + 1 - nint;
+    const int *dm = c.imap_at(l);
+    const bool split = c.split_classes != 0 && nint > 0 && nfp > 0;
     if (part & 1) {
-        ModUpMap m{l, c.logN, (int)c.K - 1};
-        k_ntt<LOGR, NA, false, true, false><<<dim3(C / NA, B * l * l), NA * R / 16, 0, c.stream>>>(
-            ModUpIO_A{m, D, E, c.primes}, fwd, c.primes, c.logN);
+        if (!split) {
+            ModUpMap m{l, c.logN, (int)c.K - 1};
+            k_ntt<LOGR, NA, false, true, false><<<dim3(C / NA, B * l * l), NA * R / 16, 0, c.stream>>>(
+                ModUpIO_A{m, D, E, c.primes}, fwd, c.primes, c.logN);
+        } else {
+            const ModUpMap mi{l, c.logN, (int)c.K - 1, dm, nint}, mf{l, c.logN, (int)c.K - 1, dm + nint, nfp};
+            dual(
+                c, c.split_classes == 2,
+                [&](hipStream_t st) {
+                    k_ntt<LOGR, NA, false, true, false, ModUpIO_A, 2><<<dim3(C / NA, B * nint * l), NA * R / 16, 0,
+                                                                         st>>>(ModUpIO_A{mi, D, E, c.primes}, fwd,
+                                                                               c.primes, c.logN);
+                },
+                [&](hipStream_t st) {
+                    k_ntt<LOGR, NA, false, true, false, ModUpIO_A, 1><<<dim3(C / NA, B * nfp * l), NA * R / 16, 0,
+                                                                         st>>>(ModUpIO_A{mf, D, E, c.primes}, fwd,
+                                                                               c.primes, c.logN);
+                });
+        }
     }
     if (!(part & 2)) {
         HEC_HIP(hipGetLastError());
         return;
     }
     // (2b)+(3) fused; integer target primes first (slowest blocks start first)
-    const int nint = c.imap_nint[l], nfp = l + 1 - nint;
-    const int *dm = c.imap_at(l);
     constexpr int TB = NB2 * C / EPT;
     constexpr int X = R / NB2;
-    const int groups = X * (l + 1), gpad = (groups + 7) / 8 * 8;
-    const dim3 grid(gpad * B);
-    switch (c.bmac_keys) {  // key loads: 0 after the rounds, 1 before them, 2 one digit ahead
-    case 0: k_bmac<LOGC, NB2, EPT, 0><<<grid, TB, 0, c.stream>>>(T, E, key, ACC, fwd, c.primes, dm, c.logN, l, (int)c.K, nint, gpad, elt); break;
-    case 1: k_bmac<LOGC, NB2, EPT, 1><<<grid, TB, 0, c.stream>>>(T, E, key, ACC, fwd, c.primes, dm, c.logN, l, (int)c.K, nint, gpad, elt); break;
-    default: k_bmac<LOGC, NB2, EPT, 2><<<grid, TB, 0, c.stream>>>(T, E, key, ACC, fwd, c.primes, dm, c.logN, l, (int)c.K, nint, gpad, elt); break;
-    }
+    auto launch = [&](auto cls, hipStream_t st, const int *Il, int nI) {
+        constexpr int CL = decltype(cls)::value;
+        const int gpad = (X * nI + 7) / 8 * 8;
+        const dim3 grid(gpad * B);
+        switch (c.bmac_keys) {  // key loads: 0 after the rounds, 1 before them, 2 one digit ahead
+        case 0: k_bmac<LOGC, NB2, EPT, 0, CL><<<grid, TB, 0, st>>>(T, E, key, ACC, fwd, c.primes, Il, nI, c.logN, l, (int)c.K, nint, gpad, elt); break;
+        case 1: k_bmac<LOGC, NB2, EPT, 1, CL><<<grid, TB, 0, st>>>(T, E, key, ACC, fwd, c.primes, Il, nI, c.logN, l, (int)c.K, nint, gpad, elt); break;
+        default: k_bmac<LOGC, NB2, EPT, 2, CL><<<grid, TB, 0, st>>>(T, E, key, ACC, fwd, c.primes, Il, nI, c.logN, l, (int)c.K, nint, gpad, elt); break;
+        }
+    };
+    if (!split) launch(std::integral_constant<int, 0>{}, c.stream, dm, l + 1);
+    else
+        dual(
+            c, c.split_classes == 2, [&](hipStream_t st) { launch(std::integral_constant<int, 2>{}, st, dm, nint); },
+            [&](hipStream_t st) { launch(std::integral_constant<int, 1>{}, st, dm + nint, nfp); });
     HEC_HIP(hipGetLastError());
 }
 
