@@ -439,19 +439,34 @@ struct RotTrie {
     std::size_t key_switches() const { return nodes.size() - 1; }
 };
 
+// Rotation buffers of the trie walk: nb per depth, taken round robin by consecutive children at a
+// depth, so the buffer of a visited terminal stays intact for nb - 1 more siblings (deferred tensors).
+struct TrieBufs {
+    std::vector<std::vector<u64 *>> b;  // [depth][slot]
+    std::vector<unsigned> next;
+    TrieBufs(Scratch &s, int depth, int nb, u64 words) : b(depth + 1), next(depth + 1, 0)
+    {
+        for (int d = 0; d <= depth; ++d)
+            for (int k = 0; k < (d == 0 ? 1 : nb); ++k) b[d].push_back(s.take(words));
+    }
+    u64 *take(int d) { return b[d][next[d]++ % b[d].size()]; }
+};
+
 // Depth-first walk: visit(tag, src) for every terminal of `node`, then for each child compute the
-// child's rotation into bufs[depth + 1] and recurse.  A buffer at depth d is only overwritten after
-// the subtree that read it has been enqueued (stream order makes that safe).
-template <class F>
+// child's rotation into a depth + 1 buffer and recurse.  before_write(buf) runs before a buffer is
+// overwritten (the caller flushes deferred work that still reads it).  A buffer is only rewritten
+// after the subtree that read it has been enqueued (stream order makes that safe).
+template <class F, class W>
 void walk_trie(Ctx &c, Scratch &s, const RotTrie &t, int node, PolyArr src, int depth, int B, int l,
-               const hec_galois_keys &gk, u64 *const *bufs, u64 stride, F &visit)
+               const hec_galois_keys &gk, TrieBufs &bufs, u64 stride, F &visit, W &before_write)
 {
     for (std::size_t tag : t.nodes[node].terminals) visit(tag, src);
     for (int ch : t.nodes[node].children) {
         const u32 e = t.nodes[ch].elt;
-        const PolyArr dst{bufs[depth + 1], stride, (u64)l * c.N};
+        const PolyArr dst{bufs.take(depth + 1), stride, (u64)l * c.N};
+        before_write(dst.p);
         galois_ks(c, s, src, dst, B, l, e, gk.keys.at(e));
-        walk_trie(c, s, t, ch, dst, depth + 1, B, l, gk, bufs, stride, visit);
+        walk_trie(c, s, t, ch, dst, depth + 1, B, l, gk, bufs, stride, visit, before_write);
     }
 }
 
@@ -509,22 +524,44 @@ void matvec_core(hec_context *ctx, const hec_ciphertext *const *diags, const hec
     }
     const u64 S2 = 2 * l * N, S3 = 3 * l * N;
     const int D = trie.depth;
-    std::size_t words = p * (S2 * (D + 1) + S3) + 2 * p * l * N + ks_words(c, p, l) + (D + 80) * 64;
+    const int nb = pt ? 1 : c.tensor_defer_bufs;  // rotation buffers per depth
+    std::size_t words = p * (S2 * (1 + (std::size_t)D * nb) + S3) + 2 * p * l * N + ks_words(c, p, l) +
+                        (D * nb + 80) * 64;
     if (finish) words += rescale_words(c, p, 2, l) + p * 2 * (l - 1) * N;
     Scratch s(c, words);
-    std::vector<u64 *> bufs(D + 1);
-    for (int d = 0; d <= D; ++d) bufs[d] = s.take(p * S2);
+    TrieBufs bufs(s, D, nb, p * S2);
     u64 *ACC3 = s.take(p * S3);
-    for (std::size_t i = 0; i < p; ++i) d2d(c, bufs[0] + i * S2, cols[i]->d, S2);
-    const PolyArr Xa{bufs[0], S2, l * N}, Aa{ACC3, S3, l * N};
+    for (std::size_t i = 0; i < p; ++i) d2d(c, bufs.b[0][0] + i * S2, cols[i]->d, S2);
+    const PolyArr Xa{bufs.b[0][0], S2, l * N}, Aa{ACC3, S3, l * N};
     bool first = true;
-    auto visit = [&](std::size_t j, PolyArr src) {
+    // ct x ct: the tensor products of up to TB_MAX visited terminals are deferred and applied in one
+    // k_tensor_multi pass (ACC3 read/written once per batch); a batch is flushed when full or before
+    // one of its rotation buffers is overwritten
+    TensorBatch tb{};
+    auto flush = [&] {
+        if (tb.T == 0) return;
         ProfScope pr(c, "tensor");
-        if (pt) plain_acc(c, src, ddata(j), Aa, (int)p, (int)l, first);
-        else tensor_acc(c, src, ddata(j), l * N, Aa, (int)p, (int)l, first);
+        tensor_multi(c, tb, S2, l * N, l * N, Aa, (int)p, (int)l, first);
         first = false;
+        tb.T = 0;
     };
-    walk_trie(c, s, trie, 0, Xa, 0, (int)p, (int)l, *gk, bufs.data(), S2, visit);
+    auto visit = [&](std::size_t j, PolyArr src) {
+        if (pt) {
+            ProfScope pr(c, "tensor");
+            plain_acc(c, src, ddata(j), Aa, (int)p, (int)l, first);
+            first = false;
+            return;
+        }
+        tb.r[tb.T] = src.p;
+        tb.a[tb.T] = ddata(j);
+        if (++tb.T == std::min(TB_MAX, c.tensor_defer_max)) flush();
+    };
+    auto before_write = [&](const u64 *buf) {
+        for (int t = 0; t < tb.T; ++t)
+            if (tb.r[t] == buf) return flush();
+    };
+    walk_trie(c, s, trie, 0, Xa, 0, (int)p, (int)l, *gk, bufs, S2, visit, before_write);
+    flush();
     const u64 accw = pt ? S2 : S3;  // accumulator words per output
     if (!finish) {
         for (std::size_t i = 0; i < p; ++i) {
@@ -620,6 +657,8 @@ int hec_context_create(uint64_t N, const uint64_t *mod, uint64_t K, int device, 
         if (const char *f = std::getenv("HEC_BMAC_KEYS")) c.bmac_keys = f[0] - '0';
         if (const char *f = std::getenv("HEC_FUSE_GALOIS")) c.fuse_galois = f[0] != '0';
         if (const char *f = std::getenv("HEC_SPLIT_CLASSES")) c.split_classes = f[0] - '0';
+        if (const char *f = std::getenv("HEC_TENSOR_DEFER")) c.tensor_defer_max = std::max(1, std::atoi(f));
+        if (const char *f = std::getenv("HEC_TENSOR_BUFS")) c.tensor_defer_bufs = std::max(1, std::atoi(f));
         c.N = N;
         c.logN = __builtin_ctzll(N);
         c.K = K;
@@ -1378,18 +1417,18 @@ int hec_matmul_col_colT(hec_context *ctx, const hec_ciphertext *const *A, uint64
         const int D = trie.depth;
         Scratch s(c, n * S2 * (D + 2) + p * (S3 + So) + ks_words(c, std::max<uint64_t>(n, p), l) + 2 * n * l * N +
                          rescale_words(c, p, 2, l) + (D + 80) * 64);
-        std::vector<u64 *> bufs(D + 1);
-        for (int d = 0; d <= D; ++d) bufs[d] = s.take(n * S2);
+        TrieBufs bufs(s, D, 1, n * S2);
         u64 *Aw = s.take(n * S2), *AC = s.take(p * S3), *O = s.take(p * So);
         for (uint64_t j = 0; j < n; ++j) {
             d2d(c, Aw + j * S2, A[j]->d, S2);
-            d2d(c, bufs[0] + j * S2, B[j]->d, S2);
+            d2d(c, bufs.b[0][0] + j * S2, B[j]->d, S2);
         }
-        const PolyArr Ba{bufs[0], S2, l * N}, Aa{Aw, S2, l * N};
+        const PolyArr Ba{bufs.b[0][0], S2, l * N}, Aa{Aw, S2, l * N};
         auto visit = [&](std::size_t i, PolyArr src) {  // out[i] = sum_j rot(B[j], i) (x) A[j]
             tensor_sum(c, src, Aa, AC + i * S3, l * N, (int)n, (int)l);
         };
-        walk_trie(c, s, trie, 0, Ba, 0, (int)n, (int)l, *gk, bufs.data(), S2, visit);
+        auto no_flush = [](const u64 *) {};
+        walk_trie(c, s, trie, 0, Ba, 0, (int)n, (int)l, *gk, bufs, S2, visit, no_flush);
         const PolyArr Ca{AC, S3, l * N};
         keyswitch(c, s, PolyArr{AC + 2 * l * N, S3, 0}, rk->d, Ca, 2, Ca, (int)p, (int)l);
         rescale_batch(c, s, Ca, (int)p, 2, (int)l, PolyArr{O, So, (l - 1) * N});

@@ -69,6 +69,8 @@ struct Ctx {
     int bmac_keys = 1;             // HEC_BMAC_KEYS: k_bmac key loads 0 late / 1 before the rounds / 2 one digit ahead
     int split_classes = 0;         // HEC_SPLIT_CLASSES: mod-up A / k_bmac as one mixed launch (0), FP64 and
                                    // integer launches on one stream (1) or on two streams (2)
+    int tensor_defer_max = 12;     // HEC_TENSOR_DEFER: terminals per deferred tensor batch (1 = immediate)
+    int tensor_defer_bufs = 4;     // HEC_TENSOR_BUFS: rotation buffers per trie depth
     bool fuse_galois = true;       // HEC_FUSE_GALOIS=0: materialise apply_galois before the key switch
     bool fused_modup_mac = true;  // HEC_FUSED_MODUP_MAC=0: separate mod-up pass B and key MAC kernels
     // profiling (ProfScope in hec_engine.hip)
@@ -108,6 +110,16 @@ void divide_round(Ctx &c, const u64 *Y, u64 ysb, u64 ysk, PolyArr X, PolyArr IN,
                   int nk, int nl, int last_idx, const u64 *inv, const u64 *inv_q, u64 *Z, u32 in_elt = 1);
 void galois_permute(Ctx &c, PolyArr in, PolyArr out, int B, int nk, int nl, u32 elt);
 void tensor_acc(Ctx &c, PolyArr R, const u64 *A, u64 a_sk, PolyArr ACC, int B, int l, bool assign);
+// deferred tensor products: ACC[b] (=|+=) sum_t R_t[b] (x) A_t, T <= TB_MAX rotated inputs
+// (R_t[b] at r[t] + b r_sb, polys r_sk apart; A_t polys a_sk apart)
+constexpr int TB_MAX = 12;
+struct TensorBatch {
+    const u64 *r[TB_MAX];
+    const u64 *a[TB_MAX];
+    int T;
+};
+void tensor_multi(Ctx &c, const TensorBatch &tb, u64 r_sb, u64 r_sk, u64 a_sk, PolyArr ACC, int B, int l,
+                  bool assign);
 // ct x pt: ACC polys 0, 1 (+)= R[b] (x) P for the B entries (multiply_plain + add_inplace)
 void plain_acc(Ctx &c, PolyArr R, const u64 *P, PolyArr ACC, int B, int l, bool assign);
 void tensor_sum(Ctx &c, PolyArr R, PolyArr A, u64 *ACC, u64 acc_sk, int B, int l);
