@@ -70,7 +70,7 @@ struct Ctx {
     int split_classes = 0;         // HEC_SPLIT_CLASSES: mod-up A / k_bmac as one mixed launch (0), FP64 and
                                    // integer launches on one stream (1) or on two streams (2)
     int tensor_defer_max = 12;     // HEC_TENSOR_DEFER: terminals per deferred tensor batch (1 = immediate)
-    int tensor_defer_bufs = 4;     // HEC_TENSOR_BUFS: rotation buffers per trie depth
+    int tensor_defer_bufs = 8;     // HEC_TENSOR_BUFS: rotation buffers per trie depth
     bool fuse_galois = true;       // HEC_FUSE_GALOIS=0: materialise apply_galois before the key switch
     bool fused_modup_mac = true;  // HEC_FUSED_MODUP_MAC=0: separate mod-up pass B and key MAC kernels
     // profiling (ProfScope in hec_engine.hip)
