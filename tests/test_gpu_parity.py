@@ -332,3 +332,66 @@ def test_matvec_ct_x_pt_errors(env11, hecdna):
     X = [e.up(e.enc(seed=800))]
     with pytest.raises(hecdna.InvalidArgument, match="parameter mismatch"):
         e.ctx.matmul_diagpt_col(pts, X, e.gk)
+
+
+# ----------------------------------------------------------------- matvec edge cases --
+def test_matvec_single_diagonal_no_rotation(env11):
+    """n = 1: only the j = 0 term (he_linalg.cpp:979, no rotation), then relin + rescale."""
+    e = env11
+    A, X = [e.enc(seed=900)], [e.enc(seed=901), e.enc(seed=902)]
+    exp = e.o.matmul_diag_col(A, X, e.rk_h, e.gk_h)
+    got = e.ctx.matmul_diag_col([e.up(a) for a in A], [e.up(x) for x in X], e.rk, e.gk)
+    for g, c in zip(got, exp):
+        e.same(g, c)
+
+
+def test_matvec_key_subset_uses_naf(orc, hecdna):
+    """With only the keys for steps +-1, 2, 4, 8 (no conjugation, no larger powers), rotations by
+    3, 5, 6, 7 decompose by NAF into those keys exactly as SEAL's rotate_internal does."""
+    N = 1 << 11
+    m = orc.Oracle.create_coeff_modulus(N, [50, 36, 36, 50])
+    o = orc.Oracle(N, m)
+    elts = [o.elt_from_step(s) for s in (1, -1, 2, -2, 4, -4, 8, -8)]
+    e = Env(orc, hecdna, N, [50, 36, 36, 50], seed=55, elts=elts)
+    A = [e.enc(seed=910 + j) for j in range(8)]
+    X = [e.enc(seed=920)]
+    exp = e.o.matmul_diag_col(A, X, e.rk_h, e.gk_h)
+    got = e.ctx.matmul_diag_col([e.up(a) for a in A], [e.up(x) for x in X], e.rk, e.gk)
+    e.same(got[0], exp[0])
+
+
+def test_matvec_errors_follow_seal(env11, hecdna):
+    e = env11
+    X = [e.up(e.enc(seed=930))]
+    A = [e.up(e.enc(seed=931 + j)) for j in range(4)]
+    partial_keys = e.ctx.galois_keys({k: v for k, v in e.gk_h.items() if k == e.o.elt_from_step(1)})
+    with pytest.raises(hecdna.InvalidArgument, match="Galois key not present"):
+        e.ctx.matmul_diag_col(A, X, e.rk, partial_keys)        # rot by 2 needs the step-2 key
+    with pytest.raises(hecdna.InvalidArgument, match="scale mismatch"):
+        e.ctx.matmul_diag_col(A[:3] + [e.up(e.enc(seed=935, scale=2.0**39))], X, e.rk, e.gk)
+    with pytest.raises(hecdna.InvalidArgument, match="parameter mismatch"):
+        e.ctx.matmul_diag_col(A[:3] + [e.up(e.enc(seed=936, level=2))], X, e.rk, e.gk)
+    low = [e.up(e.enc(seed=940 + j, level=1, scale=2.0**20)) for j in range(2)]
+    with pytest.raises(hecdna.InvalidArgument, match="end of modulus switching chain reached"):
+        e.ctx.matmul_diag_col(low, [e.up(e.enc(seed=945, level=1, scale=2.0**20))], e.rk, e.gk)
+    with pytest.raises(hecdna.InvalidArgument, match="scale out of bounds"):   # SEAL's multiply check first
+        e.ctx.matmul_diag_col([e.up(e.enc(seed=946, level=1))], [e.up(e.enc(seed=947, level=1))], e.rk, e.gk)
+    big = [A[0]] * (e.N // 2 + 1)                                 # j = N/2 is outside the slot range
+    with pytest.raises(hecdna.InvalidArgument, match="step count too large"):
+        e.ctx.matmul_diag_col(big, X, e.rk, e.gk)
+    with pytest.raises(hecdna.InvalidArgument):
+        e.ctx.matmul_diag_col([], X, e.rk, e.gk)
+
+
+def test_matvec_partial_sum_of_all_singletons(env11):
+    """Sum of the n single-diagonal partials mod q = the full accumulator (any j order)."""
+    e = env11
+    n = 6
+    gA = [e.up(e.enc(seed=950 + j)) for j in range(n)]
+    gX = [e.up(e.enc(seed=960))]
+    full = e.ctx.matmul_diag_col_partial(gA, 0, n, gX, e.gk)[0].download()
+    q = np.array(e.m[:3], dtype=np.uint64).reshape(1, 3, 1)
+    acc = np.zeros_like(full)
+    for j in reversed(range(n)):
+        acc = (acc + e.ctx.matmul_diag_col_partial_set(gA, [j], gX, e.gk)[0].download()) % q
+    assert np.array_equal(acc, full)
