@@ -307,14 +307,16 @@ void keyswitch(Ctx &c, Scratch &s, PolyArr T, const u64 *key, PolyArr IN, int in
         *Z = s.take((u64)B * 2 * l * N);
     int pmap[HEC_MAXL + 1];
     for (int i = 0; i <= HEC_MAXL; ++i) pmap[i] = i;
+    const bool fan = c.fan_out && c.fused_modup_mac;
     {
-        ProfScope ps(c, "ks_intt");
-        ntt_strided(c, true, T.p, T.sb, D, l * N, l, pmap, B * l, elt);
+        ProfScope ps(c, "ks_intt");  // with fan-out only its first pass; the fan kernel finishes it
+        ntt_strided(c, true, T.p, T.sb, D, l * N, l, pmap, B * l, elt, fan ? 1 : 3);
     }
     if (c.fused_modup_mac) {  // mod-up pass A, then pass B fused with the key MAC (no E round trip)
         {
             ProfScope ps(c, "ks_modup_a");
-            ks_modup_mac(c, D, E, T, key, ACC, B, l, 1, elt);
+            if (fan) fan_modup(c, D, E, B, l);
+            else ks_modup_mac(c, D, E, T, key, ACC, B, l, 1, elt);
         }
         {
             ProfScope ps(c, "ks_bmac");
@@ -333,9 +335,10 @@ void keyswitch(Ctx &c, Scratch &s, PolyArr T, const u64 *key, PolyArr IN, int in
     {
         ProfScope ps(c, "ks_moddown");
         const int pP[1] = {(int)c.K - 1};
-        ntt_strided(c, true, ACC + l * N, (l + 1) * N, ACC + l * N, (l + 1) * N, 1, pP, 2 * B);
+        ntt_strided(c, true, ACC + l * N, (l + 1) * N, ACC + l * N, (l + 1) * N, 1, pP, 2 * B, 1, fan ? 1 : 3);
+        if (fan) fan_divide_round(c, ACC + l * N, 2 * (l + 1) * N, (l + 1) * N, Z, B, 2, l, (int)c.K - 1);
         divide_round(c, ACC + l * N, 2 * (l + 1) * N, (l + 1) * N, PolyArr{ACC, 2 * (l + 1) * N, (l + 1) * N}, IN,
-                     in_nk, OUT, B, 2, l, (int)c.K - 1, c.p_inv.data(), c.p_inv_q.data(), Z, elt);
+                     in_nk, OUT, B, 2, l, (int)c.K - 1, c.p_inv.data(), c.p_inv_q.data(), Z, elt, fan ? 2 : 3);
     }
     s.top = top;
 }
@@ -656,6 +659,7 @@ int hec_context_create(uint64_t N, const uint64_t *mod, uint64_t K, int device, 
         if (const char *f = std::getenv("HEC_FUSED_MODUP_MAC")) c.fused_modup_mac = f[0] != '0';
         if (const char *f = std::getenv("HEC_BMAC_KEYS")) c.bmac_keys = f[0] - '0';
         if (const char *f = std::getenv("HEC_FUSE_GALOIS")) c.fuse_galois = f[0] != '0';
+        if (const char *f = std::getenv("HEC_FAN")) c.fan_out = f[0] != '0';
         if (const char *f = std::getenv("HEC_SPLIT_CLASSES")) c.split_classes = f[0] - '0';
         if (const char *f = std::getenv("HEC_TENSOR_DEFER")) c.tensor_defer_max = std::max(1, std::atoi(f));
         if (const char *f = std::getenv("HEC_TENSOR_BUFS")) c.tensor_defer_bufs = std::max(1, std::atoi(f));

@@ -71,6 +71,7 @@ struct Ctx {
                                    // integer launches on one stream (1) or on two streams (2)
     int tensor_defer_max = 12;     // HEC_TENSOR_DEFER: terminals per deferred tensor batch (1 = immediate)
     int tensor_defer_bufs = 8;     // HEC_TENSOR_BUFS: rotation buffers per trie depth
+    bool fan_out = true;           // HEC_FAN=0: separate INTT pass A (fan-out fuses it into the forward passes A)
     bool fuse_galois = true;       // HEC_FUSE_GALOIS=0: materialise apply_galois before the key switch
     bool fused_modup_mac = true;  // HEC_FUSED_MODUP_MAC=0: separate mod-up pass B and key MAC kernels
     // profiling (ProfScope in hec_engine.hip)
@@ -93,8 +94,9 @@ struct Ctx {
 // Batched NTT: job -> poly = job / nl, limb = job % nl; reads src + poly*ps_src + limb*N, writes
 // dst + poly*ps_dst + limb*N (src may equal dst), prime = pmap[limb].
 // elt != 1: the first pass loads src through the Galois permutation of elt (apply_galois_ntt fused).
+// stages: 1 first pass only, 2 second pass only, 3 both.
 void ntt_strided(Ctx &c, bool inverse, const u64 *src, u64 ps_src, u64 *dst, u64 ps_dst, int nl, const int *pmap,
-                 int njobs, u32 elt = 1);
+                 int njobs, u32 elt = 1, int stages = 3);
 // Key-switch phases (B targets at level l; see hec_engine.hip for the dataflow)
 void ks_modup(Ctx &c, const u64 *D, u64 *E, int B, int l);
 void ks_mac(Ctx &c, PolyArr T, const u64 *E, const u64 *key, u64 *ACC, int B, int l, u32 elt);
@@ -107,7 +109,14 @@ void ks_modup_mac(Ctx &c, const u64 *D, u64 *E, PolyArr T, const u64 *key, u64 *
 //   OUT = IN + (X - NTT(corr)) * inv   (IN optional; inv = last^-1 mod q_i)
 // in_elt != 1: IN is read through the Galois permutation of in_elt
 void divide_round(Ctx &c, const u64 *Y, u64 ysb, u64 ysk, PolyArr X, PolyArr IN, int in_nk, PolyArr OUT, int B,
-                  int nk, int nl, int last_idx, const u64 *inv, const u64 *inv_q, u64 *Z, u32 in_elt = 1);
+                  int nk, int nl, int last_idx, const u64 *inv, const u64 *inv_q, u64 *Z, u32 in_elt = 1,
+                  int stages = 3);
+// fan-out kernels (see hec_kernels.hip): finish an INTT whose first pass ran (inverse pass A) and run
+// the forward pass A of every target prime from registers.
+//   mod-up:  D[b][J] -> E[b][I][J] (I != J), the input of k_bmac / ks_modup's pass B
+//   mod-down: last limb (b, k) at Y + b ysb + k ysk -> Z[b][k][i], the input of divide_round pass B
+void fan_modup(Ctx &c, const u64 *D, u64 *E, int B, int l);
+void fan_divide_round(Ctx &c, const u64 *Y, u64 ysb, u64 ysk, u64 *Z, int B, int nk, int nl, int last_idx);
 void galois_permute(Ctx &c, PolyArr in, PolyArr out, int B, int nk, int nl, u32 elt);
 void tensor_acc(Ctx &c, PolyArr R, const u64 *A, u64 a_sk, PolyArr ACC, int B, int l, bool assign);
 // deferred tensor products: ACC[b] (=|+=) sum_t R_t[b] (x) A_t, T <= TB_MAX rotated inputs

@@ -409,18 +409,18 @@ __global__ void __launch_bounds__(NSEG *(1 << LOGP) / 16)
 }
 
 template <int LOGR, int LOGC, int NA, int NB, bool INV, class IO1, class IO2>
-static void run_ntt2(Ctx &c, int njobs, const IO1 &first, const IO2 &second)
+static void run_ntt2(Ctx &c, int njobs, const IO1 &first, const IO2 &second, int stages)
 {
     constexpr int R = 1 << LOGR, C = 1 << LOGC;
     const dim3 gA(C / NA, njobs), gB(R / NB, njobs);
     constexpr int TA = NA * R / 16, TB = NB * C / 16;
     const TwTables fwd{c.tw, c.twb, c.twf, c.twbf}, inv{c.itw, c.itwb, c.itwf, c.itwbf};
     if constexpr (!INV) {
-        k_ntt<LOGR, NA, false, true, false><<<gA, TA, 0, c.stream>>>(first, fwd, c.primes, c.logN);
-        k_ntt<LOGC, NB, false, false, true><<<gB, TB, 0, c.stream>>>(second, fwd, c.primes, c.logN);
+        if (stages & 1) k_ntt<LOGR, NA, false, true, false><<<gA, TA, 0, c.stream>>>(first, fwd, c.primes, c.logN);
+        if (stages & 2) k_ntt<LOGC, NB, false, false, true><<<gB, TB, 0, c.stream>>>(second, fwd, c.primes, c.logN);
     } else {
-        k_ntt<LOGC, NB, true, false, false><<<gB, TB, 0, c.stream>>>(first, inv, c.primes, c.logN);
-        k_ntt<LOGR, NA, true, true, true><<<gA, TA, 0, c.stream>>>(second, inv, c.primes, c.logN);
+        if (stages & 1) k_ntt<LOGC, NB, true, false, false><<<gB, TB, 0, c.stream>>>(first, inv, c.primes, c.logN);
+        if (stages & 2) k_ntt<LOGR, NA, true, true, true><<<gA, TA, 0, c.stream>>>(second, inv, c.primes, c.logN);
     }
     HEC_HIP(hipGetLastError());
 }
@@ -428,17 +428,17 @@ static void run_ntt2(Ctx &c, int njobs, const IO1 &first, const IO2 &second)
 // forward: first = pass A IO (pre-op load), second = pass B IO (post-op store);
 // inverse: first = pass B IO, second = pass A IO.
 template <bool INV, class IO1, class IO2>
-static void ntt_dispatch(Ctx &c, int njobs, const IO1 &first, const IO2 &second)
+static void ntt_dispatch(Ctx &c, int njobs, const IO1 &first, const IO2 &second, int stages = 3)
 {
     if (njobs <= 0) return;
     switch (c.logN) {
-    case 10: run_ntt2<5, 5, 32, 32, INV>(c, njobs, first, second); break;
-    case 11: run_ntt2<6, 5, 32, 64, INV>(c, njobs, first, second); break;
-    case 12: run_ntt2<6, 6, 64, 64, INV>(c, njobs, first, second); break;
-    case 13: run_ntt2<7, 6, 32, 64, INV>(c, njobs, first, second); break;
-    case 14: run_ntt2<7, 7, 32, 32, INV>(c, njobs, first, second); break;
-    case 15: run_ntt2<8, 7, 16, 16, INV>(c, njobs, first, second); break;
-    case 16: run_ntt2<8, 8, 16, 16, INV>(c, njobs, first, second); break;
+    case 10: run_ntt2<5, 5, 32, 32, INV>(c, njobs, first, second, stages); break;
+    case 11: run_ntt2<6, 5, 32, 64, INV>(c, njobs, first, second, stages); break;
+    case 12: run_ntt2<6, 6, 64, 64, INV>(c, njobs, first, second, stages); break;
+    case 13: run_ntt2<7, 6, 32, 64, INV>(c, njobs, first, second, stages); break;
+    case 14: run_ntt2<7, 7, 32, 32, INV>(c, njobs, first, second, stages); break;
+    case 15: run_ntt2<8, 7, 16, 16, INV>(c, njobs, first, second, stages); break;
+    case 16: run_ntt2<8, 8, 16, 16, INV>(c, njobs, first, second, stages); break;
     default: throw std::invalid_argument("poly_modulus_degree must be 2^10 .. 2^16");
     }
 }
@@ -453,13 +453,13 @@ static StridedIO strided(const u64 *src, u64 *dst, u64 ps_src, u64 ps_dst, int n
 }
 
 void ntt_strided(Ctx &c, bool inverse, const u64 *src, u64 ps_src, u64 *dst, u64 ps_dst, int nl, const int *pmap,
-                 int njobs, u32 elt)
+                 int njobs, u32 elt, int stages)
 {
     if (nl > HEC_MAXL + 1) throw std::invalid_argument("too many limbs");
     const StridedIO first = strided(src, dst, ps_src, ps_dst, nl, c.logN, pmap, elt);
     const StridedIO second = strided(dst, dst, ps_dst, ps_dst, nl, c.logN, pmap);
-    if (inverse) ntt_dispatch<true>(c, njobs, first, second);
-    else ntt_dispatch<false>(c, njobs, first, second);
+    if (inverse) ntt_dispatch<true>(c, njobs, first, second, stages);
+    else ntt_dispatch<false>(c, njobs, first, second, stages);
 }
 
 void ks_modup(Ctx &c, const u64 *D, u64 *E, int B, int l)
@@ -471,7 +471,7 @@ void ks_modup(Ctx &c, const u64 *D, u64 *E, int B, int l)
 }
 
 void divide_round(Ctx &c, const u64 *Y, u64 ysb, u64 ysk, PolyArr X, PolyArr IN, int in_nk, PolyArr OUT, int B,
-                  int nk, int nl, int last_idx, const u64 *inv, const u64 *inv_q, u64 *Z, u32 in_elt)
+                  int nk, int nl, int last_idx, const u64 *inv, const u64 *inv_q, u64 *Z, u32 in_elt, int stages)
 {
     if (nl > HEC_MAXL) throw std::invalid_argument("too many limbs");
     DivRoundIO_A a{};
@@ -482,7 +482,157 @@ void divide_round(Ctx &c, const u64 *Y, u64 ysb, u64 ysk, PolyArr X, PolyArr IN,
     b.Z = Z; b.X = X; b.IN = IN; b.OUT = OUT; b.nk = nk; b.nl = nl; b.logN = c.logN; b.in_nk = in_nk; b.elt = in_elt;
     b.primes = c.primes;
     for (int i = 0; i < nl; ++i) { b.inv[i] = inv[i]; b.inv_q[i] = inv_q[i]; }
-    ntt_dispatch<false>(c, B * nk * nl, a, b);
+    ntt_dispatch<false>(c, B * nk * nl, a, b, stages);
+}
+
+// =============================================================== fan-out: INTT pass A -> fwd passes A ==
+// A block owns NSEG columns (R rows) of one source limb whose inverse pass B already ran.  It finishes
+// the INTT (inverse pass A, N^-1 scaling, canonical residues), keeps the coefficient-form column values
+// in registers and, for every target prime t of the source, transforms them (FAN::xf: the mod-up
+// reduction mod q_t, or the mod-down rounding) and runs the forward pass A for q_t, storing the
+// pass-A-domain tile for the following pass-B kernel (k_bmac / the divide-and-round pass B).  The
+// coefficient-form limb is never stored, and it is read once instead of once per target.
+struct FanModUp {  // source (b, J) = D[b][J] (inverse pass-B domain) -> E[b][I][J], I != J, mod q_I
+    const u64 *D;
+    u64 *E;
+    int l, logN, kP;
+    const DevPrime *primes;
+    struct Src { const u64 *in; int prime; };
+    struct Tgt { bool valid; int prime; u64 *out; u64 q, r1; };
+    __device__ int ntargets() const { return l + 1; }
+    __device__ Src src(int job) const { return Src{D + ((u64)job << logN), job % l}; }
+    __device__ Tgt tgt(int job, int I) const
+    {
+        const int b = job / l, J = job % l, p = I == l ? kP : I;
+        return Tgt{I != J, p, E + (((u64)((b * (l + 1) + I) * l + J)) << logN), primes[p].q, primes[p].r1};
+    }
+    __device__ u64 xf(const Tgt &t, u64 d) const { return barrett64(d, t.q, t.r1); }
+};
+struct FanDivRound {  // source (b, k) = last limb (inverse pass-B domain) -> Z[b][k][i] for i < nl
+    const u64 *Y;
+    u64 ysb, ysk;
+    u64 *Z;
+    int nk, nl, logN, last_idx;
+    u64 last, half;
+    const DevPrime *primes;
+    u64 fix[HEC_MAXL];
+    struct Src { const u64 *in; int prime; };
+    struct Tgt { bool valid; int prime; u64 *out; u64 q, r1, fix; };
+    __device__ int ntargets() const { return nl; }
+    __device__ Src src(int job) const { return Src{Y + (u64)(job / nk) * ysb + (u64)(job % nk) * ysk, last_idx}; }
+    __device__ Tgt tgt(int job, int i) const
+    {
+        return Tgt{true, i, Z + ((u64)(job * nl + i) << logN), primes[i].q, primes[i].r1, fix[i]};
+    }
+    __device__ u64 xf(const Tgt &t, u64 d) const
+    {
+        u64 v = d + half;
+        v = v >= last ? v - last : v;
+        return barrett64(v, t.q, t.r1) + t.fix;
+    }
+};
+
+template <int LOGP, int NSEG, bool FP, class Lds>
+__device__ __forceinline__ void fan_rounds(u64 *lds, const Lds &addr, int ts, const TwTables &tt, const DevPrime &pr,
+                                           int prime, int logN, bool inverse)
+{
+    auto twidx = [](int s, int i) -> u64 { return (1ull << s) + (u64)i; };
+    const ulonglong2 *tw = tt.a + ((u64)prime << logN);
+    const double *twf = tt.fa + ((u64)prime << logN);
+    if (!inverse) {
+        ntt_round<LOGP, 0, false, FP>(lds, addr, ts, twidx, tw, twf, pr);
+        __syncthreads();
+        ntt_round<LOGP, 1, false, FP>(lds, addr, ts, twidx, tw, twf, pr);
+    } else {
+        ntt_round<LOGP, 1, true, FP>(lds, addr, ts, twidx, tw, twf, pr);
+        __syncthreads();
+        ntt_round<LOGP, 0, true, FP>(lds, addr, ts, twidx, tw, twf, pr);
+    }
+}
+
+template <int LOGP, int NSEG, class FAN>
+__global__ void __launch_bounds__(NSEG *(1 << LOGP) / 16)
+    k_fan(const FAN fan, TwTables inv, TwTables fwd, const DevPrime *__restrict__ primes, int logN)
+{
+    constexpr int P = 1 << LOGP, THREADS = NSEG * P / 16, LD = NSEG + 1, ITS = 16;
+    __shared__ u64 lds[P * LD];
+    const int seg0 = blockIdx.x * NSEG, lc = logN - LOGP;
+    const int ts = threadIdx.x / NSEG, sg = threadIdx.x % NSEG;
+    auto addr = [sg](int x) { return x * LD + sg; };
+    auto gidx = [&](int it) { const int li = threadIdx.x + it * THREADS; return ((u64)(li / NSEG) << lc) + seg0 + li % NSEG; };
+    auto lidx = [&](int it) { const int li = threadIdx.x + it * THREADS; return (li / NSEG) * LD + li % NSEG; };
+    const auto src = fan.src(blockIdx.y);
+    const DevPrime ps = primes[src.prime];
+#pragma unroll
+    for (int it = 0; it < ITS; ++it) lds[lidx(it)] = src.in[gidx(it)];
+    __syncthreads();
+    if (ps.fp) fan_rounds<LOGP, NSEG, true>(lds, addr, ts, inv, ps, src.prime, logN, true);
+    else fan_rounds<LOGP, NSEG, false>(lds, addr, ts, inv, ps, src.prime, logN, true);
+    __syncthreads();
+    u64 d[ITS];  // canonical coefficient-form values of the source limb
+#pragma unroll
+    for (int it = 0; it < ITS; ++it) {
+        const u64 v = lds[lidx(it)];
+        if (ps.fp) d[it] = fp_canon(fp_mulmod(__longlong_as_double((long long)v), ps.ninv_d, ps.qd, ps.qinv), ps.qd, ps.qinv);
+        else d[it] = shoup(v, ps.ninv, ps.ninv_q, ps.q);
+    }
+    const int nt = fan.ntargets();
+    for (int t = 0; t < nt; ++t) {
+        const auto tg = fan.tgt(blockIdx.y, t);
+        if (!tg.valid) continue;
+        const DevPrime pt = primes[tg.prime];
+        __syncthreads();  // the previous target's tile has been read out
+#pragma unroll
+        for (int it = 0; it < ITS; ++it) {
+            u64 v = fan.xf(tg, d[it]);
+            if (pt.fp) v = (u64)__double_as_longlong(u2d(v));
+            lds[lidx(it)] = v;
+        }
+        __syncthreads();
+        if (pt.fp) fan_rounds<LOGP, NSEG, true>(lds, addr, ts, fwd, pt, tg.prime, logN, false);
+        else fan_rounds<LOGP, NSEG, false>(lds, addr, ts, fwd, pt, tg.prime, logN, false);
+        __syncthreads();
+#pragma unroll
+        for (int it = 0; it < ITS; ++it) tg.out[gidx(it)] = lds[lidx(it)];
+    }
+}
+
+template <int LOGR, int LOGC, int NA, class FAN>
+static void run_fan(Ctx &c, int njobs, const FAN &fan)
+{
+    constexpr int R = 1 << LOGR, C = 1 << LOGC;
+    const TwTables fwd{c.tw, c.twb, c.twf, c.twbf}, inv{c.itw, c.itwb, c.itwf, c.itwbf};
+    k_fan<LOGR, NA><<<dim3(C / NA, njobs), NA * R / 16, 0, c.stream>>>(fan, inv, fwd, c.primes, c.logN);
+    HEC_HIP(hipGetLastError());
+}
+template <class FAN>
+static void fan_dispatch(Ctx &c, int njobs, const FAN &fan)
+{
+    switch (c.logN) {
+    case 10: run_fan<5, 5, 32>(c, njobs, fan); break;
+    case 11: run_fan<6, 5, 32>(c, njobs, fan); break;
+    case 12: run_fan<6, 6, 64>(c, njobs, fan); break;
+    case 13: run_fan<7, 6, 32>(c, njobs, fan); break;
+    case 14: run_fan<7, 7, 32>(c, njobs, fan); break;
+    case 15: run_fan<8, 7, 16>(c, njobs, fan); break;
+    case 16: run_fan<8, 8, 16>(c, njobs, fan); break;
+    default: throw std::invalid_argument("poly_modulus_degree must be 2^10 .. 2^16");
+    }
+}
+
+void fan_modup(Ctx &c, const u64 *D, u64 *E, int B, int l)
+{
+    fan_dispatch(c, B * l, FanModUp{D, E, l, c.logN, (int)c.K - 1, c.primes});
+}
+
+void fan_divide_round(Ctx &c, const u64 *Y, u64 ysb, u64 ysk, u64 *Z, int B, int nk, int nl, int last_idx)
+{
+    if (nl > HEC_MAXL) throw std::invalid_argument("too many limbs");
+    FanDivRound f{};
+    f.Y = Y; f.ysb = ysb; f.ysk = ysk; f.Z = Z; f.nk = nk; f.nl = nl; f.logN = c.logN; f.last_idx = last_idx;
+    f.last = c.q[last_idx]; f.half = f.last >> 1; f.primes = c.primes;
+    for (int i = 0; i < nl; ++i) f.fix[i] = c.q[i] - (f.half % c.q[i]);
+    fan_dispatch(c, B * nk, f);
 }
 
 // ====================================================================== fused mod-up B + MAC ==
