@@ -527,7 +527,7 @@ void matvec_core(hec_context *ctx, const hec_ciphertext *const *diags, const hec
     }
     const u64 S2 = 2 * l * N, S3 = 3 * l * N;
     const int D = trie.depth;
-    const int nb = pt ? 1 : c.tensor_defer_bufs;  // rotation buffers per depth
+    const int nb = c.tensor_defer_bufs;  // rotation buffers per depth
     std::size_t words = p * (S2 * (1 + (std::size_t)D * nb) + S3) + 2 * p * l * N + ks_words(c, p, l) +
                         (D * nb + 80) * 64;
     if (finish) words += rescale_words(c, p, 2, l) + p * 2 * (l - 1) * N;
@@ -537,24 +537,18 @@ void matvec_core(hec_context *ctx, const hec_ciphertext *const *diags, const hec
     for (std::size_t i = 0; i < p; ++i) d2d(c, bufs.b[0][0] + i * S2, cols[i]->d, S2);
     const PolyArr Xa{bufs.b[0][0], S2, l * N}, Aa{ACC3, S3, l * N};
     bool first = true;
-    // ct x ct: the tensor products of up to TB_MAX visited terminals are deferred and applied in one
-    // k_tensor_multi pass (ACC3 read/written once per batch); a batch is flushed when full or before
-    // one of its rotation buffers is overwritten
+    // the products of up to TB_MAX visited terminals (ct x ct tensors, or ct x pt plain products) are
+    // deferred and applied in one k_tensor_multi pass (the accumulator read/written once per batch); a
+    // batch is flushed when full or before one of its rotation buffers is overwritten
     TensorBatch tb{};
     auto flush = [&] {
         if (tb.T == 0) return;
         ProfScope pr(c, "tensor");
-        tensor_multi(c, tb, S2, l * N, l * N, Aa, (int)p, (int)l, first);
+        tensor_multi(c, tb, S2, l * N, l * N, Aa, (int)p, (int)l, first, pt);
         first = false;
         tb.T = 0;
     };
     auto visit = [&](std::size_t j, PolyArr src) {
-        if (pt) {
-            ProfScope pr(c, "tensor");
-            plain_acc(c, src, ddata(j), Aa, (int)p, (int)l, first);
-            first = false;
-            return;
-        }
         tb.r[tb.T] = src.p;
         tb.a[tb.T] = ddata(j);
         if (++tb.T == std::min(TB_MAX, c.tensor_defer_max)) flush();

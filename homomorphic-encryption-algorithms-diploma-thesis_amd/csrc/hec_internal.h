@@ -128,9 +128,7 @@ struct TensorBatch {
     int T;
 };
 void tensor_multi(Ctx &c, const TensorBatch &tb, u64 r_sb, u64 r_sk, u64 a_sk, PolyArr ACC, int B, int l,
-                  bool assign);
-// ct x pt: ACC polys 0, 1 (+)= R[b] (x) P for the B entries (multiply_plain + add_inplace)
-void plain_acc(Ctx &c, PolyArr R, const u64 *P, PolyArr ACC, int B, int l, bool assign);
+                  bool assign, bool plain = false);  // plain: the A_t are plaintexts (ct x pt, 2-poly ACC)
 void tensor_sum(Ctx &c, PolyArr R, PolyArr A, u64 *ACC, u64 acc_sk, int B, int l);
 void ew_add(Ctx &c, PolyArr a, PolyArr b, PolyArr out, int B, int nk, int nl, int mode);  // 0 add, 1 sub
 void ew_negate(Ctx &c, PolyArr a, int B, int nk, int nl);

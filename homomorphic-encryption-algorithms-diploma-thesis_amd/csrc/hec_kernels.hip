@@ -1105,6 +1105,8 @@ void tensor_acc(Ctx &c, PolyArr R, const u64 *A, u64 a_sk, PolyArr ACC, int B, i
 // product is reduced (SEAL ckks_multiply) and the sums are taken mod q, so the bits equal T
 // successive k_tensor_acc calls.  FP64 primes: exact fp_mulmod products (|.| <= 0.53 q) summed as
 // integer-valued doubles (|sum| <= 1.6 q T < 2^53), canonicalised once.
+// PT: the A_t are plaintexts (ct x pt: d0 = r0 p, d1 = r1 p, multiply_plain), ACC has 2 polys.
+template <bool PT>
 __global__ void __launch_bounds__(256)
     k_tensor_multi(TensorBatch tb, u64 r_sb, u64 r_sk, u64 a_sk, PolyArr ACC, int B, int logN, u64 total, int assign,
                    const DevPrime *__restrict__ primes)
@@ -1113,79 +1115,64 @@ __global__ void __launch_bounds__(256)
     if (idx >= total) return;
     const DevPrime pr = primes[idx >> logN];
     for (int b = 0; b < B; ++b) {
-        u64 d0, d1, d2;
+        u64 d0, d1, d2 = 0;
         if (pr.fp) {
             double s0 = 0, s1 = 0, s2 = 0;
             for (int t = 0; t < tb.T; ++t) {
                 const u64 *r = tb.r[t] + b * r_sb;
-                const double r0 = u2d(r[idx]), r1 = u2d(r[r_sk + idx]);
-                const double a0 = u2d(tb.a[t][idx]), a1 = u2d(tb.a[t][a_sk + idx]);
+                const double r0 = u2d(r[idx]), r1 = u2d(r[r_sk + idx]), a0 = u2d(tb.a[t][idx]);
                 s0 += fp_mulmod(r0, a0, pr.qd, pr.qinv);
-                s1 += fp_mulmod(r0, a1, pr.qd, pr.qinv) + fp_mulmod(r1, a0, pr.qd, pr.qinv);
-                s2 += fp_mulmod(r1, a1, pr.qd, pr.qinv);
+                if constexpr (PT) {
+                    s1 += fp_mulmod(r1, a0, pr.qd, pr.qinv);
+                } else {
+                    const double a1 = u2d(tb.a[t][a_sk + idx]);
+                    s1 += fp_mulmod(r0, a1, pr.qd, pr.qinv) + fp_mulmod(r1, a0, pr.qd, pr.qinv);
+                    s2 += fp_mulmod(r1, a1, pr.qd, pr.qinv);
+                }
             }
             d0 = fp_canon(s0, pr.qd, pr.qinv);
             d1 = fp_canon(s1, pr.qd, pr.qinv);
-            d2 = fp_canon(s2, pr.qd, pr.qinv);
+            if constexpr (!PT) d2 = fp_canon(s2, pr.qd, pr.qinv);
         } else {
-            d0 = d1 = d2 = 0;
+            d0 = d1 = 0;
             for (int t = 0; t < tb.T; ++t) {
                 const u64 *r = tb.r[t] + b * r_sb;
-                const u64 r0 = r[idx], r1 = r[r_sk + idx], a0 = tb.a[t][idx], a1 = tb.a[t][a_sk + idx];
+                const u64 r0 = r[idx], r1 = r[r_sk + idx], a0 = tb.a[t][idx];
                 d0 = addmod(d0, mulmod(r0, a0, pr), pr.q);
-                U128 m{r0 * a1, mulhi64(r0, a1)};
-                mac128(m, r1, a0);
-                d1 = addmod(d1, barrett128(m.lo, m.hi, pr.q, pr.r0, pr.r1), pr.q);
-                d2 = addmod(d2, mulmod(r1, a1, pr), pr.q);
+                if constexpr (PT) {
+                    d1 = addmod(d1, mulmod(r1, a0, pr), pr.q);
+                } else {
+                    const u64 a1 = tb.a[t][a_sk + idx];
+                    U128 m{r0 * a1, mulhi64(r0, a1)};
+                    mac128(m, r1, a0);
+                    d1 = addmod(d1, barrett128(m.lo, m.hi, pr.q, pr.r0, pr.r1), pr.q);
+                    d2 = addmod(d2, mulmod(r1, a1, pr), pr.q);
+                }
             }
         }
         u64 *o = ACC.p + b * ACC.sb;
         if (assign) {
-            o[idx] = d0; o[ACC.sk + idx] = d1; o[2 * ACC.sk + idx] = d2;
-        } else {
-            o[idx] = addmod(o[idx], d0, pr.q);
-            o[ACC.sk + idx] = addmod(o[ACC.sk + idx], d1, pr.q);
-            o[2 * ACC.sk + idx] = addmod(o[2 * ACC.sk + idx], d2, pr.q);
-        }
-    }
-}
-
-void tensor_multi(Ctx &c, const TensorBatch &tb, u64 r_sb, u64 r_sk, u64 a_sk, PolyArr ACC, int B, int l, bool assign)
-{
-    const u64 total = (u64)l * c.N;
-    k_tensor_multi<<<(unsigned)((total + 255) / 256), 256, 0, c.stream>>>(tb, r_sb, r_sk, a_sk, ACC, B, c.logN, total,
-                                                                           assign ? 1 : 0, c.primes);
-    HEC_HIP(hipGetLastError());
-}
-
-// ct x pt: ACC[b] polys 0, 1 (+)= R[b] (x) P, SEAL multiply_plain (one Barrett
-// reduction per product) then add_inplace
-__global__ void __launch_bounds__(256)
-    k_plain_acc(PolyArr R, const u64 *__restrict__ P, PolyArr ACC, int B, int logN, u64 total, int assign,
-                const DevPrime *__restrict__ primes)
-{
-    const u64 idx = (u64)blockIdx.x * 256 + threadIdx.x;
-    if (idx >= total) return;
-    const DevPrime pr = primes[idx >> logN];
-    const u64 pv = P[idx];
-    for (int b = 0; b < B; ++b) {
-        const u64 *r = R.p + b * R.sb;
-        const u64 d0 = mulmod(r[idx], pv, pr), d1 = mulmod(r[R.sk + idx], pv, pr);
-        u64 *o = ACC.p + b * ACC.sb;
-        if (assign) {
             o[idx] = d0; o[ACC.sk + idx] = d1;
+            if constexpr (!PT) o[2 * ACC.sk + idx] = d2;
         } else {
             o[idx] = addmod(o[idx], d0, pr.q);
             o[ACC.sk + idx] = addmod(o[ACC.sk + idx], d1, pr.q);
+            if constexpr (!PT) o[2 * ACC.sk + idx] = addmod(o[2 * ACC.sk + idx], d2, pr.q);
         }
     }
 }
 
-void plain_acc(Ctx &c, PolyArr R, const u64 *P, PolyArr ACC, int B, int l, bool assign)
+void tensor_multi(Ctx &c, const TensorBatch &tb, u64 r_sb, u64 r_sk, u64 a_sk, PolyArr ACC, int B, int l, bool assign,
+                  bool plain)
 {
     const u64 total = (u64)l * c.N;
-    k_plain_acc<<<(unsigned)((total + 255) / 256), 256, 0, c.stream>>>(R, P, ACC, B, c.logN, total, assign ? 1 : 0,
-                                                                        c.primes);
+    const unsigned grid = (unsigned)((total + 255) / 256);
+    if (plain)
+        k_tensor_multi<true><<<grid, 256, 0, c.stream>>>(tb, r_sb, r_sk, a_sk, ACC, B, c.logN, total, assign ? 1 : 0,
+                                                          c.primes);
+    else
+        k_tensor_multi<false><<<grid, 256, 0, c.stream>>>(tb, r_sb, r_sk, a_sk, ACC, B, c.logN, total, assign ? 1 : 0,
+                                                           c.primes);
     HEC_HIP(hipGetLastError());
 }
 
