@@ -651,19 +651,24 @@ void fan_divide_round(Ctx &c, const u64 *Y, u64 ysb, u64 ysk, u64 *Z, int B, int
 // Grid (R / NSEG, l + 1, B): blocks of one (chunk block, I) for different b are R/NSEG * (l+1) apart,
 // a multiple of 8 for logN >= 14, so they run on one XCD and share its L2 copy of the key chunk.
 // The integer target primes come first in Imap: their blocks are the slowest, so they start first.
+// k_bmac LDS segment stride (words): P data words + P/8 pad words + 8
+constexpr int bmac_ld(int logp) { return (1 << logp) + (1 << logp) / 8 + 8; }
+
 template <int LOGP, int NSEG, int EPT, bool FP, int KEYM>
 __device__ __forceinline__ void bmac_body(u64 *lds, u64 *ltw, PolyArr T, const u64 *__restrict__ E, const u64 *__restrict__ key,
                                           u64 *__restrict__ ACC, const TwTables &tt, const DevPrime &pr, int I, int kI,
                                           int b, int xb, int logN, int l, int K, u32 elt)
 {
-    constexpr int P = 1 << LOGP, THREADS = NSEG * P / EPT, LD = P + 1, TWS = 2 * P + 2;
+    constexpr int P = 1 << LOGP, THREADS = NSEG * P / EPT, LD = bmac_ld(LOGP), TWS = 2 * P + 2;
     const u64 N = 1ull << logN;
     const int seg0 = xb * NSEG;
     const u64 base = (u64)seg0 << LOGP;
     const ulonglong2 *tw = tt.b + ((u64)kI << logN);
     const double *twf = tt.fb + ((u64)kI << logN);
     const int ts = threadIdx.x / NSEG, sg = threadIdx.x % NSEG;
-    auto addr = [sg](int x) { return sg * LD + x; };
+    // one pad word per 8 elements plus a segment stride of P + P/8 + 8: the three round access patterns
+    // and the staging writes go from 4-way to <= 2-way LDS bank conflicts (64 banks, 32-lane halves)
+    auto addr = [sg](int x) { return sg * LD + x + (x >> 3); };
     const u64 R = 1ull << (logN - LOGP);
     // the pass-B twiddles of a chunk do not depend on the digit J: stage the block's (NSEG chunks x
     // (P - 1) entries) once into LDS, rows padded to TWS words (bank spread), lanes = consecutive chunks
@@ -735,7 +740,7 @@ __device__ __forceinline__ void bmac_body(u64 *lds, u64 *ltw, PolyArr T, const u
             if constexpr (FP) {
                 if (!ntt) v = (u64)__double_as_longlong(u2d(v));  // canonical integer target
             }
-            lds[(li / P) * LD + (li % P)] = v;
+            lds[(li / P) * LD + (li % P) + ((li % P) >> 3)] = v;
         }
         if (J + 1 < l) load_tile(J + 1);
         u64 k0[EPT], k1[EPT];
@@ -803,7 +808,7 @@ __global__ void __launch_bounds__(NSEG *(1 << LOGP) / EPT)
            const DevPrime *__restrict__ primes, const int *__restrict__ Imap, int nI, int logN, int l, int K,
            int nint, int gpad, u32 elt)
 {
-    __shared__ u64 lds[NSEG * ((1 << LOGP) + 1)];
+    __shared__ u64 lds[NSEG * bmac_ld(LOGP)];
     __shared__ u64 ltw[NSEG * (2 * (1 << LOGP) + 2)];
     // 1-D grid, XCD-aware: workgroup w runs on XCD w % 8.  The B blocks of one (chunk block, I) group
     // read the same key chunk, so they get ids G8*8*B + b*8 + (G % 8): one XCD, dispatched together,
