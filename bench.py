@@ -201,8 +201,8 @@ def main():
     # per-phase breakdown: one extra (untimed) step with asynchronous HIP event pairs recorded on the
     # context's stream around every phase (no host synchronisation inside the step)
     breakdown = {}
-    classes = ("ks_intt", "ks_modup", "ks_mac", "ks_modup_a", "ks_bmac", "ks_moddown", "galois", "tensor", "relin",
-               "rescale")
+    classes = ("ks_intt", "ks_modup", "ks_mac", "ks_modup_a", "ks_bmac", "ks_modup_h", "ks_hmac", "ks_moddown",
+               "galois", "tensor", "relin", "rescale")
     if not args.no_profile:
         ctx.profile(2)
         step()
@@ -224,6 +224,8 @@ def main():
         "ks_bmac": Bt * L * L + Bt * L + 2 * L * K + 2 * Bt * K,  # pass-A digits + T + key in, ACC out
         "ks_modup": Bt * L + Bt * L * L,                         # D in, l^2 NTT-form digits out
         "ks_mac": Bt * L * L + Bt * L + 2 * L * K + 2 * Bt * K,   # digits + T + key in, ACC out
+        "ks_modup_h": Bt * L + Bt * L * L,                       # hoisted node: D in, l^2 NTT-form digits out
+        "ks_hmac": Bt * L * L + Bt * L + K + 2 * L * K + 2 * Bt * K,  # node digits + T + W + key in, ACC out
         "ks_moddown": 2 * Bt * K + Bt * L + 2 * Bt * L,           # ACC + c0 in, rotated ct out
         "galois": 4 * Bt * L,
     }
@@ -236,6 +238,8 @@ def main():
         algo = algo_limbs[dom] * limb
         ach = algo / (per * 1e-3) / 1e9
         kern = {"ks_bmac": "k_bmac (mod-up pass B + key MAC, fused)", "ks_modup": "k_ntt mod-up pass A+B",
+                "ks_hmac": "k_hmac (hoisted key MAC of one rotation)",
+                "ks_modup_h": "k_fan + k_ntt pass B (hoisted mod-up of a trie node)",
                 "ks_modup_a": "k_ntt mod-up pass A", "ks_mac": "k_ks_mac"}.get(dom, dom)
         roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(dom, args.batch, args.logn, L),

@@ -50,6 +50,7 @@ struct hec_kswitch_key {
 struct hec_galois_keys {
     hec_context *ctx = nullptr;
     std::map<u32, u64 *> keys;
+    std::map<u32, u64 *> negw;  // hoisted mod-up: W_elt[I] = NTT_I(sign mask of elt), built on first use
 };
 
 namespace {
@@ -296,6 +297,20 @@ std::size_t ks_words(const Ctx &c, std::size_t B, std::size_t l)
     return c.N * B * (l + (l + 1) * l + 2 * (l + 1) + 2 * l) + 4 * 64;
 }
 
+// key-switch mod-down (SEAL switch_key_inplace step 4): the P-limb INTT's first pass, the fan-out that
+// finishes it and forms the rounding limbs, and divide_round's pass B (OUT = IN + (ACC_i - r) P^-1)
+void moddown(Ctx &c, u64 *ACC, u64 *Z, PolyArr IN, int in_nk, PolyArr OUT, int B, int l, u32 elt)
+{
+    const u64 N = c.N;
+    const bool fan = c.fan_out;
+    ProfScope ps(c, "ks_moddown");
+    const int pP[1] = {(int)c.K - 1};
+    ntt_strided(c, true, ACC + l * N, (l + 1) * N, ACC + l * N, (l + 1) * N, 1, pP, 2 * B, 1, fan ? 1 : 3);
+    if (fan) fan_divide_round(c, ACC + l * N, 2 * (l + 1) * N, (l + 1) * N, Z, B, 2, l, (int)c.K - 1);
+    divide_round(c, ACC + l * N, 2 * (l + 1) * N, (l + 1) * N, PolyArr{ACC, 2 * (l + 1) * N, (l + 1) * N}, IN, in_nk,
+                 OUT, B, 2, l, (int)c.K - 1, c.p_inv.data(), c.p_inv_q.data(), Z, elt, fan ? 2 : 3);
+}
+
 // T (the target polys) and IN (added to the output) are read through the Galois permutation of elt
 // (elt = 1: as they are).  OUT must not overlap T or IN when elt != 1 (the reads gather).
 void keyswitch(Ctx &c, Scratch &s, PolyArr T, const u64 *key, PolyArr IN, int in_nk, PolyArr OUT, int B, int l,
@@ -332,15 +347,81 @@ void keyswitch(Ctx &c, Scratch &s, PolyArr T, const u64 *key, PolyArr IN, int in
             ks_mac(c, T, E, key, ACC, B, l, elt);
         }
     }
-    {
-        ProfScope ps(c, "ks_moddown");
-        const int pP[1] = {(int)c.K - 1};
-        ntt_strided(c, true, ACC + l * N, (l + 1) * N, ACC + l * N, (l + 1) * N, 1, pP, 2 * B, 1, fan ? 1 : 3);
-        if (fan) fan_divide_round(c, ACC + l * N, 2 * (l + 1) * N, (l + 1) * N, Z, B, 2, l, (int)c.K - 1);
-        divide_round(c, ACC + l * N, 2 * (l + 1) * N, (l + 1) * N, PolyArr{ACC, 2 * (l + 1) * N, (l + 1) * N}, IN,
-                     in_nk, OUT, B, 2, l, (int)c.K - 1, c.p_inv.data(), c.p_inv_q.data(), Z, elt, fan ? 2 : 3);
-    }
+    moddown(c, ACC, Z, IN, in_nk, OUT, B, l, elt);
     s.top = top;
+}
+
+// hoisted mod-up data of one trie node (B targets at level l): D = INTT(c1) (canonical coefficient form),
+// E[b][I][J] = NTT_I(D_J mod q_I) (canonical NTT form, J != I), zero lists of D (see hec_kernels.hip)
+struct Hoist {
+    u64 *D = nullptr, *E = nullptr;
+    int *zl = nullptr;
+};
+std::size_t hoist_words(const Ctx &c, std::size_t B, std::size_t l)
+{
+    return c.N * B * (l + (l + 1) * l) + (B * l * (HEC_ZCAP + 1) * sizeof(int) + 7) / 8 + 3 * 64;
+}
+Hoist hoist_alloc(const Ctx &c, Scratch &s, int B, int l)
+{
+    Hoist h;
+    h.D = s.take((u64)B * l * c.N);
+    h.E = s.take((u64)B * (l + 1) * l * c.N);
+    h.zl = reinterpret_cast<int *>(s.take(((u64)B * l * (HEC_ZCAP + 1) * sizeof(int) + 7) / 8));
+    return h;
+}
+void hoist_node(Ctx &c, PolyArr X, int B, int l, const Hoist &h)
+{
+    const u64 N = c.N;
+    int pmap[HEC_MAXL + 1];
+    for (int i = 0; i <= HEC_MAXL; ++i) pmap[i] = i;
+    {
+        ProfScope ps(c, "ks_intt");
+        ntt_strided(c, true, X.p + X.sk, X.sb, h.D, l * N, l, pmap, B * l);
+        zero_scan(c, h.D, B * l, h.zl);
+    }
+    ProfScope ps(c, "ks_modup_h");
+    fan_modup(c, h.D, h.E, B, l, true);  // pass A of every NTT_I(D_J mod q_I), from the canonical D
+    ks_modup(c, h.D, h.E, B, l, 2);      // pass B, canonical NTT-form digits
+}
+// one child of a hoisted node: OUT = key switch of apply_galois(X, elt) (X: the node's ciphertexts)
+void hoisted_child(Ctx &c, Scratch &s, PolyArr X, const Hoist &h, const u64 *W, const u64 *key, PolyArr OUT, int B,
+                   int l, u32 elt)
+{
+    const u64 N = c.N;
+    const std::size_t top = s.top;
+    u64 *ACC = s.take((u64)B * 2 * (l + 1) * N), *Z = s.take((u64)B * 2 * l * N);
+    {
+        ProfScope ps(c, "ks_hmac");
+        hoisted_mac(c, PolyArr{X.p + X.sk, X.sb, 0}, h.E, W, h.zl, key, ACC, B, l, elt);
+    }
+    moddown(c, ACC, Z, PolyArr{X.p, X.sb, X.sk}, 1, OUT, B, l, elt);
+    s.top = top;
+}
+std::size_t hoisted_child_words(const Ctx &c, std::size_t B, std::size_t l)
+{
+    return c.N * B * (2 * (l + 1) + 2 * l) + 2 * 64;
+}
+
+// the sign-mask NTTs of a Galois key (built on first use): W[I] = NTT_I(m), m[t] = 1 iff coefficient t of
+// apply_galois(x, elt) is a negated coefficient of x, i.e. t elt^-1 mod 2N >= N
+const u64 *galois_negw(hec_context *ctx, hec_galois_keys &gk, u32 elt)
+{
+    auto it = gk.negw.find(elt);
+    if (it != gk.negw.end()) return it->second;
+    Ctx &c = ctx->c;
+    const u64 N = c.N, m2 = 2 * N;
+    const u64 einv = invm(elt, m2);
+    std::vector<u64> mask(c.K * N);
+    for (u64 t = 0; t < N; ++t) mask[t] = ((t * einv) % m2) >= N ? 1 : 0;
+    for (std::size_t i = 1; i < c.K; ++i) std::copy(mask.begin(), mask.begin() + N, mask.begin() + i * N);
+    u64 *W = dalloc(c.K * N);
+    HEC_HIP(hipMemcpyAsync(W, mask.data(), c.K * N * sizeof(u64), hipMemcpyHostToDevice, c.stream));
+    int pmap[HEC_MAXL + 1];
+    for (int i = 0; i <= HEC_MAXL; ++i) pmap[i] = i;
+    ntt_strided(c, false, W, c.K * N, W, c.K * N, (int)c.K, pmap, (int)c.K);
+    HEC_HIP(hipStreamSynchronize(c.stream));  // the host mask goes out of scope
+    gk.negw[elt] = W;
+    return W;
 }
 
 // X (size 2) -> OUT = apply_galois(X, elt) followed by key switching (SEAL apply_galois_inplace).
@@ -473,6 +554,30 @@ void walk_trie(Ctx &c, Scratch &s, const RotTrie &t, int node, PolyArr src, int 
     }
 }
 
+// The same walk with the hoisted mod-up (hec_kernels.hip): a node with at least min_children children
+// computes INTT(c1) and the NTT-form digits of every (target prime, digit) once into hs[depth]; each
+// child then only runs the hoisted key MAC and the mod-down.  Nodes with fewer children use the fused
+// per-rotation key switch.
+template <class F, class W>
+void walk_trie_hoisted(Ctx &c, Scratch &s, const RotTrie &t, int node, PolyArr src, int depth, int B, int l,
+                       hec_context *ctx, hec_galois_keys &gk, TrieBufs &bufs, const std::vector<Hoist> &hs,
+                       u64 stride, int min_children, F &visit, W &before_write)
+{
+    for (std::size_t tag : t.nodes[node].terminals) visit(tag, src);
+    const auto &ch = t.nodes[node].children;
+    const bool hoisted = (int)ch.size() >= min_children;
+    if (hoisted) hoist_node(c, src, B, l, hs[depth]);
+    for (int cn : ch) {
+        const u32 e = t.nodes[cn].elt;
+        const PolyArr dst{bufs.take(depth + 1), stride, (u64)l * c.N};
+        before_write(dst.p);
+        if (hoisted) hoisted_child(c, s, src, hs[depth], galois_negw(ctx, gk, e), gk.keys.at(e), dst, B, l, e);
+        else galois_ks(c, s, src, dst, B, l, e, gk.keys.at(e));
+        walk_trie_hoisted(c, s, t, cn, dst, depth + 1, B, l, ctx, gk, bufs, hs, stride, min_children, visit,
+                          before_write);
+    }
+}
+
 // BatchedMatrix::matmul diag x col (he_linalg.cpp:943-1006) for the p columns at once, diagonals
 // [jb, je).  The loop over i (output column) is interchanged with the loop over j so that one
 // rotation launch sequence and one key read serve all p columns, and the rotations run over the
@@ -528,8 +633,10 @@ void matvec_core(hec_context *ctx, const hec_ciphertext *const *diags, const hec
     const u64 S2 = 2 * l * N, S3 = 3 * l * N;
     const int D = trie.depth;
     const int nb = c.tensor_defer_bufs;  // rotation buffers per depth
+    const bool hoist = c.hoist && D > 0;
     std::size_t words = p * (S2 * (1 + (std::size_t)D * nb) + S3) + 2 * p * l * N + ks_words(c, p, l) +
                         (D * nb + 80) * 64;
+    if (hoist) words += D * hoist_words(c, p, l) + hoisted_child_words(c, p, l);
     if (finish) words += rescale_words(c, p, 2, l) + p * 2 * (l - 1) * N;
     Scratch s(c, words);
     TrieBufs bufs(s, D, nb, p * S2);
@@ -557,8 +664,34 @@ void matvec_core(hec_context *ctx, const hec_ciphertext *const *diags, const hec
         for (int t = 0; t < tb.T; ++t)
             if (tb.r[t] == buf) return flush();
     };
-    walk_trie(c, s, trie, 0, Xa, 0, (int)p, (int)l, *gk, bufs, S2, visit, before_write);
+    if (hoist) {
+        hec_galois_keys &gkm = const_cast<hec_galois_keys &>(*gk);  // negw is a per-key cache
+        for (std::size_t nd = 1; nd < trie.nodes.size(); ++nd) galois_negw(ctx, gkm, trie.nodes[nd].elt);
+        std::vector<Hoist> hs(D);
+        for (int d = 0; d < D; ++d) hs[d] = hoist_alloc(c, s, (int)p, (int)l);
+        HEC_HIP(hipMemsetAsync(c.zflag, 0, sizeof(int), c.stream));
+        walk_trie_hoisted(c, s, trie, 0, Xa, 0, (int)p, (int)l, ctx, gkm, bufs, hs, S2, c.hoist_min_children, visit,
+                          before_write);
+    } else {
+        walk_trie(c, s, trie, 0, Xa, 0, (int)p, (int)l, *gk, bufs, S2, visit, before_write);
+    }
     flush();
+    if (hoist) {  // a digit limb with more zero coefficients than the hoisted MAC corrects: recompute
+        int zf = 0;
+        HEC_HIP(hipMemcpyAsync(&zf, c.zflag, sizeof(int), hipMemcpyDeviceToHost, c.stream));
+        HEC_HIP(hipStreamSynchronize(c.stream));
+        if (zf) {
+            c.hoist = false;
+            try {
+                matvec_core(ctx, diags, pdiags, n, js, cols, p, rk, gk, finish, out);
+            } catch (...) {
+                c.hoist = true;
+                throw;
+            }
+            c.hoist = true;
+            return;
+        }
+    }
     const u64 accw = pt ? S2 : S3;  // accumulator words per output
     if (!finish) {
         for (std::size_t i = 0; i < p; ++i) {
@@ -654,6 +787,8 @@ int hec_context_create(uint64_t N, const uint64_t *mod, uint64_t K, int device, 
         if (const char *f = std::getenv("HEC_BMAC_KEYS")) c.bmac_keys = f[0] - '0';
         if (const char *f = std::getenv("HEC_FUSE_GALOIS")) c.fuse_galois = f[0] != '0';
         if (const char *f = std::getenv("HEC_FAN")) c.fan_out = f[0] != '0';
+        if (const char *f = std::getenv("HEC_HOIST")) c.hoist = f[0] != '0';
+        if (const char *f = std::getenv("HEC_HOIST_MIN")) c.hoist_min_children = std::max(1, std::atoi(f));
         if (const char *f = std::getenv("HEC_SPLIT_CLASSES")) c.split_classes = f[0] - '0';
         if (const char *f = std::getenv("HEC_TENSOR_DEFER")) c.tensor_defer_max = std::max(1, std::atoi(f));
         if (const char *f = std::getenv("HEC_TENSOR_BUFS")) c.tensor_defer_bufs = std::max(1, std::atoi(f));
@@ -669,6 +804,7 @@ int hec_context_create(uint64_t N, const uint64_t *mod, uint64_t K, int device, 
         HEC_HIP(hipEventCreateWithFlags(&c.ev_fork, hipEventDisableTiming));
         HEC_HIP(hipEventCreateWithFlags(&c.ev_join, hipEventDisableTiming));
         std::vector<ulonglong2> tw(K * N), itw(K * N);
+        std::vector<u64> psipow(K * 2 * N);  // hoisted mod-up: psi_i^e, e in [0, 2N)
         for (uint64_t i = 0; i < K; ++i) {
             const u64 q = c.q[i];
             DevPrime p{};
@@ -685,6 +821,13 @@ int hec_context_create(uint64_t N, const uint64_t *mod, uint64_t K, int device, 
             p.ninv_d = (double)p.ninv;
             c.hprimes.push_back(p);
             const u64 root = minimal_root(2 * N, q), iroot = invm(root, q);
+            {
+                u64 e = 1;
+                for (uint64_t k = 0; k < 2 * N; ++k) {
+                    psipow[i * 2 * N + k] = e;
+                    e = (u64)((u128)e * root % q);
+                }
+            }
             u64 pw = 1, ipw = 1;
             for (uint64_t k = 0; k < N; ++k) {  // tw[bitrev(k)] = root^k
                 const u32 t = brev((u32)k, c.logN);
@@ -722,6 +865,17 @@ int hec_context_create(uint64_t N, const uint64_t *mod, uint64_t K, int device, 
         HEC_HIP(hipMalloc(&c.itwb, K * N * sizeof(ulonglong2)));
         HEC_HIP(hipMemcpy(c.twb, twb.data(), K * N * sizeof(ulonglong2), hipMemcpyHostToDevice));
         HEC_HIP(hipMemcpy(c.itwb, itwb.data(), K * N * sizeof(ulonglong2), hipMemcpyHostToDevice));
+        {   // hoisted mod-up constants: psi powers per key prime, q_J mod q_I
+            HEC_HIP(hipMalloc(&c.psipow, psipow.size() * sizeof(u64)));
+            HEC_HIP(hipMemcpy(c.psipow, psipow.data(), psipow.size() * sizeof(u64), hipMemcpyHostToDevice));
+            std::vector<u64> cji(c.L * K);
+            for (std::size_t J = 0; J < c.L; ++J)
+                for (std::size_t I = 0; I < K; ++I) cji[J * K + I] = c.q[J] % c.q[I];
+            HEC_HIP(hipMalloc(&c.cji, cji.size() * sizeof(u64)));
+            HEC_HIP(hipMemcpy(c.cji, cji.data(), cji.size() * sizeof(u64), hipMemcpyHostToDevice));
+            HEC_HIP(hipMalloc(&c.zflag, sizeof(int)));
+            HEC_HIP(hipMemset(c.zflag, 0, sizeof(int)));
+        }
         {   // target-prime order tables per level (integer primes first)
             std::vector<int> tab((c.L + 1) * (HEC_MAXL + 2), 0);
             c.imap_nint.assign(c.L + 1, 0);
@@ -776,6 +930,9 @@ int hec_context_destroy(hec_context *ctx)
         c.ws.release();
         (void)hipFree(c.primes);
         (void)hipFree(c.imap);
+        (void)hipFree(c.psipow);
+        (void)hipFree(c.cji);
+        (void)hipFree(c.zflag);
         (void)hipFree(c.tw);
         (void)hipFree(c.itw);
         (void)hipFree(c.twb);
@@ -1087,6 +1244,7 @@ int hec_galois_keys_destroy(hec_galois_keys *gk)
         if (!gk) return;
         (void)hipStreamSynchronize(gk->ctx->c.stream);
         for (auto &kv : gk->keys) (void)hipFree(kv.second);
+        for (auto &kv : gk->negw) (void)hipFree(kv.second);
         delete gk;
     });
 }

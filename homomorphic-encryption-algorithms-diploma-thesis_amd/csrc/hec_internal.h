@@ -61,6 +61,11 @@ struct Ctx {
     int *imap = nullptr;
     std::vector<int> imap_nint;
     const int *imap_at(int l) const { return imap + (std::size_t)l * (HEC_MAXL + 2); }
+    // hoisted mod-up (see hec_kernels.hip): psi_i^e for e in [0, 2N) per key prime, c[J][I] = q_J mod q_I,
+    // and a device flag raised when a digit limb holds more zero coefficients than the kernels correct
+    u64 *psipow = nullptr;
+    u64 *cji = nullptr;
+    int *zflag = nullptr;
     int logR = 0;                   // pass split N = R x C, R = 2^ceil(logN/2)
     Workspace ws;
     // host-side constants
@@ -71,6 +76,8 @@ struct Ctx {
                                    // integer launches on one stream (1) or on two streams (2)
     int tensor_defer_max = 12;     // HEC_TENSOR_DEFER: terminals per deferred tensor batch (1 = immediate)
     int tensor_defer_bufs = 8;     // HEC_TENSOR_BUFS: rotation buffers per trie depth
+    bool hoist = true;             // HEC_HOIST=0: no hoisted mod-up in the rotation trie walk
+    int hoist_min_children = 2;    // HEC_HOIST_MIN: children a trie node needs to be hoisted
     bool fan_out = true;           // HEC_FAN=0: separate INTT pass A (fan-out fuses it into the forward passes A)
     bool fuse_galois = true;       // HEC_FUSE_GALOIS=0: materialise apply_galois before the key switch
     bool fused_modup_mac = true;  // HEC_FUSED_MODUP_MAC=0: separate mod-up pass B and key MAC kernels
@@ -98,7 +105,7 @@ struct Ctx {
 void ntt_strided(Ctx &c, bool inverse, const u64 *src, u64 ps_src, u64 *dst, u64 ps_dst, int nl, const int *pmap,
                  int njobs, u32 elt = 1, int stages = 3);
 // Key-switch phases (B targets at level l; see hec_engine.hip for the dataflow)
-void ks_modup(Ctx &c, const u64 *D, u64 *E, int B, int l);
+void ks_modup(Ctx &c, const u64 *D, u64 *E, int B, int l, int stages = 3);  // stages as ntt_strided
 void ks_mac(Ctx &c, PolyArr T, const u64 *E, const u64 *key, u64 *ACC, int B, int l, u32 elt);
 // fused: pass A of the mod-up NTTs (part & 1), then (pass B + key MAC) per target prime -> ACC[b][k][I]
 // (part & 2)
@@ -115,7 +122,14 @@ void divide_round(Ctx &c, const u64 *Y, u64 ysb, u64 ysk, PolyArr X, PolyArr IN,
 // the forward pass A of every target prime from registers.
 //   mod-up:  D[b][J] -> E[b][I][J] (I != J), the input of k_bmac / ks_modup's pass B
 //   mod-down: last limb (b, k) at Y + b ysb + k ysk -> Z[b][k][i], the input of divide_round pass B
-void fan_modup(Ctx &c, const u64 *D, u64 *E, int B, int l);
+void fan_modup(Ctx &c, const u64 *D, u64 *E, int B, int l, bool direct = false);
+// hoisted mod-up (hec_kernels.hip): zero_scan lists the zero coefficients of nlimbs canonical limbs
+// (zl: per limb count + HEC_ZCAP positions; more raises c.zflag); hoisted_mac is one child's key MAC
+// from the node's NTT-form digits E, the child's sign-mask NTTs W (K limbs) and X1 = the node's c1.
+#define HEC_ZCAP 8
+void zero_scan(Ctx &c, const u64 *D, int nlimbs, int *zl);
+void hoisted_mac(Ctx &c, PolyArr X1, const u64 *E, const u64 *W, const int *zl, const u64 *key, u64 *ACC, int B,
+                 int l, u32 elt);
 void fan_divide_round(Ctx &c, const u64 *Y, u64 ysb, u64 ysk, u64 *Z, int B, int nk, int nl, int last_idx);
 void galois_permute(Ctx &c, PolyArr in, PolyArr out, int B, int nk, int nl, u32 elt);
 void tensor_acc(Ctx &c, PolyArr R, const u64 *A, u64 a_sk, PolyArr ACC, int B, int l, bool assign);

@@ -462,12 +462,12 @@ void ntt_strided(Ctx &c, bool inverse, const u64 *src, u64 ps_src, u64 *dst, u64
     else ntt_dispatch<false>(c, njobs, first, second, stages);
 }
 
-void ks_modup(Ctx &c, const u64 *D, u64 *E, int B, int l)
+void ks_modup(Ctx &c, const u64 *D, u64 *E, int B, int l, int stages)
 {
     ModUpMap m{l, c.logN, (int)c.K - 1};
     ModUpIO_A a{m, D, E, c.primes};
     ModUpIO_B b{m, E};
-    ntt_dispatch<false>(c, B * l * l, a, b);
+    ntt_dispatch<false>(c, B * l * l, a, b, stages);
 }
 
 void divide_round(Ctx &c, const u64 *Y, u64 ysb, u64 ysk, PolyArr X, PolyArr IN, int in_nk, PolyArr OUT, int B,
@@ -492,7 +492,10 @@ void divide_round(Ctx &c, const u64 *Y, u64 ysb, u64 ysk, PolyArr X, PolyArr IN,
 // reduction mod q_t, or the mod-down rounding) and runs the forward pass A for q_t, storing the
 // pass-A-domain tile for the following pass-B kernel (k_bmac / the divide-and-round pass B).  The
 // coefficient-form limb is never stored, and it is read once instead of once per target.
-struct FanModUp {  // source (b, J) = D[b][J] (inverse pass-B domain) -> E[b][I][J], I != J, mod q_I
+// kDirect: D already holds the canonical coefficient form (hoisted mod-up), so there is no inverse pass.
+template <bool DIRECT>
+struct FanModUpT {  // source (b, J) = D[b][J] (inverse pass-B domain) -> E[b][I][J], I != J, mod q_I
+    static constexpr bool kDirect = DIRECT;
     const u64 *D;
     u64 *E;
     int l, logN, kP;
@@ -508,7 +511,9 @@ struct FanModUp {  // source (b, J) = D[b][J] (inverse pass-B domain) -> E[b][I]
     }
     __device__ u64 xf(const Tgt &t, u64 d) const { return barrett64(d, t.q, t.r1); }
 };
+using FanModUp = FanModUpT<false>;
 struct FanDivRound {  // source (b, k) = last limb (inverse pass-B domain) -> Z[b][k][i] for i < nl
+    static constexpr bool kDirect = false;
     const u64 *Y;
     u64 ysb, ysk;
     u64 *Z;
@@ -563,18 +568,23 @@ __global__ void __launch_bounds__(NSEG *(1 << LOGP) / 16)
     auto lidx = [&](int it) { const int li = threadIdx.x + it * THREADS; return (li / NSEG) * LD + li % NSEG; };
     const auto src = fan.src(blockIdx.y);
     const DevPrime ps = primes[src.prime];
-#pragma unroll
-    for (int it = 0; it < ITS; ++it) lds[lidx(it)] = src.in[gidx(it)];
-    __syncthreads();
-    if (ps.fp) fan_rounds<LOGP, NSEG, true>(lds, addr, ts, inv, ps, src.prime, logN, true);
-    else fan_rounds<LOGP, NSEG, false>(lds, addr, ts, inv, ps, src.prime, logN, true);
-    __syncthreads();
     u64 d[ITS];  // canonical coefficient-form values of the source limb
+    if constexpr (FAN::kDirect) {
 #pragma unroll
-    for (int it = 0; it < ITS; ++it) {
-        const u64 v = lds[lidx(it)];
-        if (ps.fp) d[it] = fp_canon(fp_mulmod(__longlong_as_double((long long)v), ps.ninv_d, ps.qd, ps.qinv), ps.qd, ps.qinv);
-        else d[it] = shoup(v, ps.ninv, ps.ninv_q, ps.q);
+        for (int it = 0; it < ITS; ++it) d[it] = src.in[gidx(it)];
+    } else {
+#pragma unroll
+        for (int it = 0; it < ITS; ++it) lds[lidx(it)] = src.in[gidx(it)];
+        __syncthreads();
+        if (ps.fp) fan_rounds<LOGP, NSEG, true>(lds, addr, ts, inv, ps, src.prime, logN, true);
+        else fan_rounds<LOGP, NSEG, false>(lds, addr, ts, inv, ps, src.prime, logN, true);
+        __syncthreads();
+#pragma unroll
+        for (int it = 0; it < ITS; ++it) {
+            const u64 v = lds[lidx(it)];
+            if (ps.fp) d[it] = fp_canon(fp_mulmod(__longlong_as_double((long long)v), ps.ninv_d, ps.qd, ps.qinv), ps.qd, ps.qinv);
+            else d[it] = shoup(v, ps.ninv, ps.ninv_q, ps.q);
+        }
     }
     const int nt = fan.ntargets();
     for (int t = 0; t < nt; ++t) {
@@ -620,9 +630,132 @@ static void fan_dispatch(Ctx &c, int njobs, const FAN &fan)
     }
 }
 
-void fan_modup(Ctx &c, const u64 *D, u64 *E, int B, int l)
+void fan_modup(Ctx &c, const u64 *D, u64 *E, int B, int l, bool direct)
 {
-    fan_dispatch(c, B * l, FanModUp{D, E, l, c.logN, (int)c.K - 1, c.primes});
+    if (direct) fan_dispatch(c, B * l, FanModUpT<true>{D, E, l, c.logN, (int)c.K - 1, c.primes});
+    else fan_dispatch(c, B * l, FanModUp{D, E, l, c.logN, (int)c.K - 1, c.primes});
+}
+
+// ================================================================================ hoisted mod-up ==
+// A trie node's rotations all key-switch digits of the same polynomial, permuted.  With D = INTT(c1)
+// of the node (canonical, coefficient form) the child for Galois element elt has digit J
+//   d'_J[t] = D_J[u]            if u = t elt^-1 mod 2N < N
+//           = q_J - D_J[u - N]  if u >= N and D_J[u - N] != 0,   0 if D_J[u - N] == 0,
+// so for I != J, mod q_I and in the NTT domain (SEAL's apply_galois_ntt permutation, gal()):
+//   NTT_I(d'_J mod q_I)[k] = E_J[I][gal(k)] + (q_J mod q_I) W_elt,I[k]
+//                            - (q_J mod q_I) sum over zeros D_J[u] = 0 that land negated at t of psi_I^((2 bitrev(k) + 1) t)
+// with E_J[I] = NTT_I(D_J mod q_I) computed once per node and W_elt,I = NTT_I(sign mask of elt) once
+// per key.  Every term is exact mod q_I, so each child's key-switch input equals SEAL's bit for bit,
+// while the node's mod-up NTTs are shared by all its children.  Zero positions are listed per (b, J)
+// by k_zscan (at most HEC_ZCAP; more raises zflag and the caller recomputes without hoisting).
+__global__ void __launch_bounds__(256) k_zscan(const u64 *__restrict__ D, int *__restrict__ zl, int *zflag, int logN)
+{
+    const u64 N = 1ull << logN;
+    const u64 g = (u64)blockIdx.x * 256 + threadIdx.x;
+    if (g >= N) return;
+    const int limb = blockIdx.y;
+    if (D[((u64)limb << logN) + g] == 0) {
+        int *z = zl + limb * (HEC_ZCAP + 1);
+        const int k = atomicAdd(z, 1);
+        if (k < HEC_ZCAP) z[1 + k] = (int)g;
+        else atomicOr(zflag, 1);
+    }
+}
+
+void zero_scan(Ctx &c, const u64 *D, int nlimbs, int *zl)
+{
+    HEC_HIP(hipMemsetAsync(zl, 0, (std::size_t)nlimbs * (HEC_ZCAP + 1) * sizeof(int), c.stream));
+    k_zscan<<<dim3((unsigned)(c.N / 256), nlimbs), 256, 0, c.stream>>>(D, zl, c.zflag, c.logN);
+    HEC_HIP(hipGetLastError());
+}
+
+// The hoisted key MAC of one child: ACC[b][k][I] = sum_J e_J[I] key[J][k][I] over the node's canonical
+// NTT-form digits E[b][I][J] (J != I) through the child's permutation plus the sign-mask term above,
+// and the child's own NTT-form target T = gal(c1) for J == I.  A thread owns two adjacent coefficients
+// (their sources are adjacent too) for BT batch entries, so each key and W word is read once per BT.
+// Grid: 1-D, XCD-aware like k_bmac (the batch groups of one (coefficient block, I) share an XCD).
+template <int BT>
+__global__ void __launch_bounds__(256)
+    k_hmac(PolyArr X1, const u64 *__restrict__ E, const u64 *__restrict__ W, const int *__restrict__ zl,
+           const u64 *__restrict__ key, u64 *__restrict__ ACC, int B, int l, int K, int logN,
+           const DevPrime *__restrict__ primes, const int *__restrict__ Imap, int nI, const u64 *__restrict__ cji,
+           const u64 *__restrict__ psipow, u32 elt, int gpad)
+{
+    const u64 N = 1ull << logN;
+    const int nbg = (B + BT - 1) / BT;
+    const int w = blockIdx.x;
+    const int g8 = w & 7, rest = w >> 3, bg = rest % nbg, G = (rest / nbg) * 8 + g8;
+    const int X = (int)(N / 512);
+    if (G >= X * nI) return;
+    const int yi = G / X, xb = G % X;
+    const int I = Imap[yi];
+    const int kI = I == l ? K - 1 : I;
+    const DevPrime pr = primes[kI];
+    const u64 k0 = (u64)xb * 512 + 2 * threadIdx.x;  // this thread's coefficients k0, k0 + 1
+    const u32 gs = galois_src((u32)k0, elt, logN);    // gal(k0 + 1) = gs ^ 1
+    const u64 sp = gs & ~1u;
+    const bool swp = gs & 1;
+    const ulonglong2 wv = *(const ulonglong2 *)(W + ((u64)kI << logN) + k0);
+    const int b0 = bg * BT;
+    U128 a0[BT][2], a1[BT][2];
+#pragma unroll
+    for (int t = 0; t < BT; ++t) a0[t][0] = a0[t][1] = a1[t][0] = a1[t][1] = U128{0, 0};
+    for (int J = 0; J < l; ++J) {
+        const ulonglong2 key0 = *(const ulonglong2 *)(key + (((u64)(J * 2 + 0) * K + kI) << logN) + k0);
+        const ulonglong2 key1 = *(const ulonglong2 *)(key + (((u64)(J * 2 + 1) * K + kI) << logN) + k0);
+        const u64 c = cji[J * K + kI];
+        const u64 cw0 = J == I ? 0 : mulmod(c, wv.x, pr), cw1 = J == I ? 0 : mulmod(c, wv.y, pr);
+#pragma unroll
+        for (int t = 0; t < BT; ++t) {
+            const int b = b0 + t;
+            if (b >= B) break;
+            const u64 *src = J == I ? X1.p + b * X1.sb + ((u64)J << logN)
+                                    : E + (((u64)((b * (l + 1) + I) * l + J)) << logN);
+            const ulonglong2 v = *(const ulonglong2 *)(src + sp);
+            u64 e0 = swp ? v.y : v.x, e1 = swp ? v.x : v.y;
+            if (J != I) {
+                e0 = addmod(e0, cw0, pr.q);
+                e1 = addmod(e1, cw1, pr.q);
+                const int *z = zl + (b * l + J) * (HEC_ZCAP + 1);
+                const int nz = min(z[0], HEC_ZCAP);
+                for (int zi = 0; zi < nz; ++zi) {  // zeros of D_J landing negated in this child (rare)
+                    u64 tt = ((u64)z[1 + zi] * elt) & (2 * N - 1);
+                    if (tt < N) continue;
+                    tt -= N;
+                    const u64 ex0 = ((2 * (u64)bitrev((u32)k0, logN) + 1) * tt) & (2 * N - 1);
+                    const u64 ex1 = ((2 * (u64)bitrev((u32)k0 + 1, logN) + 1) * tt) & (2 * N - 1);
+                    e0 = submod(e0, mulmod(c, psipow[((u64)kI << (logN + 1)) + ex0], pr), pr.q);
+                    e1 = submod(e1, mulmod(c, psipow[((u64)kI << (logN + 1)) + ex1], pr), pr.q);
+                }
+            }
+            mac128(a0[t][0], e0, key0.x);
+            mac128(a0[t][1], e1, key0.y);
+            mac128(a1[t][0], e0, key1.x);
+            mac128(a1[t][1], e1, key1.y);
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < BT; ++t) {
+        const int b = b0 + t;
+        if (b >= B) break;
+        *(ulonglong2 *)(ACC + (((u64)((b * 2 + 0) * (l + 1) + I)) << logN) + k0) =
+            ulonglong2{barrett128(a0[t][0].lo, a0[t][0].hi, pr.q, pr.r0, pr.r1),
+                       barrett128(a0[t][1].lo, a0[t][1].hi, pr.q, pr.r0, pr.r1)};
+        *(ulonglong2 *)(ACC + (((u64)((b * 2 + 1) * (l + 1) + I)) << logN) + k0) =
+            ulonglong2{barrett128(a1[t][0].lo, a1[t][0].hi, pr.q, pr.r0, pr.r1),
+                       barrett128(a1[t][1].lo, a1[t][1].hi, pr.q, pr.r0, pr.r1)};
+    }
+}
+
+void hoisted_mac(Ctx &c, PolyArr X1, const u64 *E, const u64 *W, const int *zl, const u64 *key, u64 *ACC, int B,
+                 int l, u32 elt)
+{
+    constexpr int BT = 4;
+    const int nbg = (B + BT - 1) / BT, X = (int)(c.N / 512), gpad = (X * (l + 1) + 7) / 8 * 8;
+    k_hmac<BT><<<dim3((unsigned)(gpad * nbg)), 256, 0, c.stream>>>(X1, E, W, zl, key, ACC, B, l, (int)c.K, c.logN,
+                                                                    c.primes, c.imap_at(l), l + 1, c.cji, c.psipow,
+                                                                    elt, gpad);
+    HEC_HIP(hipGetLastError());
 }
 
 void fan_divide_round(Ctx &c, const u64 *Y, u64 ysb, u64 ysk, u64 *Z, int B, int nk, int nl, int last_idx)

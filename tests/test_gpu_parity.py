@@ -277,7 +277,8 @@ def test_cfg3_matvec_small_n_bitexact(env15):
                                  {"HEC_FUSE_GALOIS": "0"}, {"HEC_FUSE_GALOIS": "0", "HEC_FUSED_MODUP_MAC": "0"},
                                  {"HEC_SPLIT_CLASSES": "1"}, {"HEC_SPLIT_CLASSES": "2"},
                                  {"HEC_TENSOR_DEFER": "1"}, {"HEC_TENSOR_BUFS": "1"}, {"HEC_TENSOR_DEFER": "3"},
-                                 {"HEC_FAN": "0"}, {"HEC_FAN": "1", "HEC_FUSE_GALOIS": "0"}])
+                                 {"HEC_FAN": "0"}, {"HEC_FAN": "1", "HEC_FUSE_GALOIS": "0"},
+                                 {"HEC_HOIST": "0"}, {"HEC_HOIST_MIN": "1"}, {"HEC_HOIST_MIN": "1", "HEC_FAN": "0"}])
 def test_keyswitch_variants_bitexact(orc, hecdna, env):
     """The engine's alternative key-switch schedules (separate mod-up pass B + MAC kernels; the fused
     kernel's key-load placements) give the same bits as the oracle."""
@@ -396,3 +397,28 @@ def test_matvec_partial_sum_of_all_singletons(env11):
     for j in reversed(range(n)):
         acc = (acc + e.ctx.matmul_diag_col_partial_set(gA, [j], gX, e.gk)[0].download()) % q
     assert np.array_equal(acc, full)
+
+
+def _with_coeff_zeros(e, ct, limbs_zeros):
+    """Copy of ct whose c1 has zero coefficients (coefficient form) at the given positions per limb."""
+    d = ct.data.copy()
+    for J, pos in limbs_zeros.items():
+        coef = e.o.ntt_inv(J, d[1][J])
+        coef[np.asarray(pos)] = 0
+        d[1][J] = e.o.ntt_fwd(J, coef)
+    return e.orc.Ct(d, ct.scale)
+
+
+@pytest.mark.parametrize("nzeros", [3, 40])  # 40 > HEC_ZCAP: the hoisted walk recomputes without hoisting
+def test_hoisted_modup_zero_coefficients(env11, nzeros):
+    """The hoisted mod-up corrects for zero digit coefficients that the Galois automorphism negates
+    (SEAL maps -0 to 0, not to q_J); a limb with more zeros than the kernels list falls back."""
+    e = env11
+    rng = np.random.default_rng(nzeros)
+    X = [_with_coeff_zeros(e, e.enc(seed=1100 + i), {0: rng.choice(e.N, nzeros, replace=False),
+                                                     2: rng.choice(e.N, 2, replace=False)}) for i in range(2)]
+    A = [e.enc(seed=1200 + j) for j in range(12)]
+    exp = e.o.matmul_diag_col(A, X, e.rk_h, e.gk_h)
+    got = e.ctx.matmul_diag_col([e.up(a) for a in A], [e.up(x) for x in X], e.rk, e.gk)
+    for g, c in zip(got, exp):
+        e.same(g, c)
