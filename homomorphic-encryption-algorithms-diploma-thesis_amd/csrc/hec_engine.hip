@@ -359,14 +359,14 @@ struct Hoist {
 };
 std::size_t hoist_words(const Ctx &c, std::size_t B, std::size_t l)
 {
-    return c.N * B * (l + (l + 1) * l) + (B * l * (HEC_ZCAP + 1) * sizeof(int) + 7) / 8 + 3 * 64;
+    return c.N * B * (l + (l + 1) * l) + ((1 + B * l * (HEC_ZCAP + 1)) * sizeof(int) + 7) / 8 + 3 * 64;
 }
 Hoist hoist_alloc(const Ctx &c, Scratch &s, int B, int l)
 {
     Hoist h;
     h.D = s.take((u64)B * l * c.N);
     h.E = s.take((u64)B * (l + 1) * l * c.N);
-    h.zl = reinterpret_cast<int *>(s.take(((u64)B * l * (HEC_ZCAP + 1) * sizeof(int) + 7) / 8));
+    h.zl = reinterpret_cast<int *>(s.take(((1 + (u64)B * l * (HEC_ZCAP + 1)) * sizeof(int) + 7) / 8));
     return h;
 }
 void hoist_node(Ctx &c, PolyArr X, int B, int l, const Hoist &h)

@@ -648,6 +648,7 @@ void fan_modup(Ctx &c, const u64 *D, u64 *E, int B, int l, bool direct)
 // per key.  Every term is exact mod q_I, so each child's key-switch input equals SEAL's bit for bit,
 // while the node's mod-up NTTs are shared by all its children.  Zero positions are listed per (b, J)
 // by k_zscan (at most HEC_ZCAP; more raises zflag and the caller recomputes without hoisting).
+// zl layout: zl[0] = zeros in the node (any limb), then per limb: count, HEC_ZCAP positions
 __global__ void __launch_bounds__(256) k_zscan(const u64 *__restrict__ D, int *__restrict__ zl, int *zflag, int logN)
 {
     const u64 N = 1ull << logN;
@@ -655,7 +656,8 @@ __global__ void __launch_bounds__(256) k_zscan(const u64 *__restrict__ D, int *_
     if (g >= N) return;
     const int limb = blockIdx.y;
     if (D[((u64)limb << logN) + g] == 0) {
-        int *z = zl + limb * (HEC_ZCAP + 1);
+        atomicAdd(zl, 1);
+        int *z = zl + 1 + limb * (HEC_ZCAP + 1);
         const int k = atomicAdd(z, 1);
         if (k < HEC_ZCAP) z[1 + k] = (int)g;
         else atomicOr(zflag, 1);
@@ -664,7 +666,7 @@ __global__ void __launch_bounds__(256) k_zscan(const u64 *__restrict__ D, int *_
 
 void zero_scan(Ctx &c, const u64 *D, int nlimbs, int *zl)
 {
-    HEC_HIP(hipMemsetAsync(zl, 0, (std::size_t)nlimbs * (HEC_ZCAP + 1) * sizeof(int), c.stream));
+    HEC_HIP(hipMemsetAsync(zl, 0, (1 + (std::size_t)nlimbs * (HEC_ZCAP + 1)) * sizeof(int), c.stream));
     k_zscan<<<dim3((unsigned)(c.N / 256), nlimbs), 256, 0, c.stream>>>(D, zl, c.zflag, c.logN);
     HEC_HIP(hipGetLastError());
 }
@@ -673,6 +675,111 @@ void zero_scan(Ctx &c, const u64 *D, int nlimbs, int *zl)
 // NTT-form digits E[b][I][J] (J != I) through the child's permutation plus the sign-mask term above,
 // and the child's own NTT-form target T = gal(c1) for J == I.  A thread owns two adjacent coefficients
 // (their sources are adjacent too) for BT batch entries, so each key and W word is read once per BT.
+// Grid: 1-D, XCD-aware like k_bmac (the batch groups of one (coefficient block, I) share an XCD).
+// zero corrections for the (b, J) digit of coefficients k0, k0 + 1 (rare: only zeros of D_J that this
+// child negates)
+__device__ __forceinline__ void hmac_zero_fix(u64 &e0, u64 &e1, const int *z, u64 c, u64 k0, u32 elt, int logN,
+                                              const u64 *__restrict__ pp, const DevPrime &pr)
+{
+    const u64 N = 1ull << logN;
+    const int nz = min(z[0], HEC_ZCAP);
+    for (int zi = 0; zi < nz; ++zi) {
+        u64 tt = ((u64)z[1 + zi] * elt) & (2 * N - 1);
+        if (tt < N) continue;
+        tt -= N;
+        const u64 ex0 = ((2 * (u64)bitrev((u32)k0, logN) + 1) * tt) & (2 * N - 1);
+        const u64 ex1 = ((2 * (u64)bitrev((u32)k0 + 1, logN) + 1) * tt) & (2 * N - 1);
+        e0 = submod(e0, mulmod(c, pp[ex0], pr), pr.q);
+        e1 = submod(e1, mulmod(c, pp[ex1], pr), pr.q);
+    }
+}
+
+template <int BT, bool FP>
+__device__ __forceinline__ void hmac_body(PolyArr X1, const u64 *__restrict__ E, const u64 *__restrict__ W,
+                                          const int *__restrict__ zl, const u64 *__restrict__ key,
+                                          u64 *__restrict__ ACC, int B, int l, int K, int logN, const DevPrime &pr,
+                                          int I, int kI, u64 k0, int b0, const u64 *__restrict__ cji,
+                                          const u64 *__restrict__ psipow, u32 elt)
+{
+    const u32 gs = galois_src((u32)k0, elt, logN);  // gal(k0 + 1) = gs ^ 1
+    const u64 sp = gs & ~1u;
+    const bool swp = gs & 1;
+    const ulonglong2 wv = *(const ulonglong2 *)(W + ((u64)kI << logN) + k0);
+    const bool zeros = zl[0] != 0;  // any zero coefficient in the node's digits (rare)
+    const u64 *pp = psipow + ((u64)kI << (logN + 1));
+    double f0[FP ? BT : 1][2], f1[FP ? BT : 1][2];
+    U128 a0[FP ? 1 : BT][2], a1[FP ? 1 : BT][2];
+#pragma unroll
+    for (int t = 0; t < BT; ++t) {
+        if constexpr (FP) f0[t][0] = f0[t][1] = f1[t][0] = f1[t][1] = 0.0;
+        else a0[t][0] = a0[t][1] = a1[t][0] = a1[t][1] = U128{0, 0};
+    }
+    for (int J = 0; J < l; ++J) {
+        const ulonglong2 key0 = *(const ulonglong2 *)(key + (((u64)(J * 2 + 0) * K + kI) << logN) + k0);
+        const ulonglong2 key1 = *(const ulonglong2 *)(key + (((u64)(J * 2 + 1) * K + kI) << logN) + k0);
+        const u64 c = cji[J * K + kI];
+        u64 cw0 = 0, cw1 = 0;
+        double cf0 = 0, cf1 = 0, k00 = 0, k01 = 0, k10 = 0, k11 = 0;
+        if constexpr (FP) {
+            if (J != I) {
+                cf0 = fp_mulmod(u2d(c), u2d(wv.x), pr.qd, pr.qinv);
+                cf1 = fp_mulmod(u2d(c), u2d(wv.y), pr.qd, pr.qinv);
+            }
+            k00 = u2d(key0.x); k01 = u2d(key0.y); k10 = u2d(key1.x); k11 = u2d(key1.y);
+        } else if (J != I) {
+            cw0 = mulmod(c, wv.x, pr);
+            cw1 = mulmod(c, wv.y, pr);
+        }
+#pragma unroll
+        for (int t = 0; t < BT; ++t) {
+            const int b = b0 + t;
+            if (b >= B) break;
+            const u64 *src = J == I ? X1.p + b * X1.sb + ((u64)J << logN)
+                                    : E + (((u64)((b * (l + 1) + I) * l + J)) << logN);
+            const ulonglong2 v = *(const ulonglong2 *)(src + sp);
+            u64 e0 = swp ? v.y : v.x, e1 = swp ? v.x : v.y;
+            if (J != I && zeros) hmac_zero_fix(e0, e1, zl + 1 + (b * l + J) * (HEC_ZCAP + 1), c, k0, elt, logN, pp, pr);
+            if constexpr (FP) {
+                const double d0 = u2d(e0) + cf0, d1 = u2d(e1) + cf1;  // |d| < 1.6 q
+                f0[t][0] += fp_mulmod(d0, k00, pr.qd, pr.qinv);
+                f0[t][1] += fp_mulmod(d1, k01, pr.qd, pr.qinv);
+                f1[t][0] += fp_mulmod(d0, k10, pr.qd, pr.qinv);
+                f1[t][1] += fp_mulmod(d1, k11, pr.qd, pr.qinv);
+            } else {
+                if (J != I) {
+                    e0 = addmod(e0, cw0, pr.q);
+                    e1 = addmod(e1, cw1, pr.q);
+                }
+                mac128(a0[t][0], e0, key0.x);
+                mac128(a0[t][1], e1, key0.y);
+                mac128(a1[t][0], e0, key1.x);
+                mac128(a1[t][1], e1, key1.y);
+            }
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < BT; ++t) {
+        const int b = b0 + t;
+        if (b >= B) break;
+        u64 *o0 = ACC + (((u64)((b * 2 + 0) * (l + 1) + I)) << logN) + k0;
+        u64 *o1 = ACC + (((u64)((b * 2 + 1) * (l + 1) + I)) << logN) + k0;
+        if constexpr (FP) {
+            *(ulonglong2 *)o0 = ulonglong2{fp_canon(f0[t][0], pr.qd, pr.qinv), fp_canon(f0[t][1], pr.qd, pr.qinv)};
+            *(ulonglong2 *)o1 = ulonglong2{fp_canon(f1[t][0], pr.qd, pr.qinv), fp_canon(f1[t][1], pr.qd, pr.qinv)};
+        } else {
+            *(ulonglong2 *)o0 = ulonglong2{barrett128(a0[t][0].lo, a0[t][0].hi, pr.q, pr.r0, pr.r1),
+                                           barrett128(a0[t][1].lo, a0[t][1].hi, pr.q, pr.r0, pr.r1)};
+            *(ulonglong2 *)o1 = ulonglong2{barrett128(a1[t][0].lo, a1[t][0].hi, pr.q, pr.r0, pr.r1),
+                                           barrett128(a1[t][1].lo, a1[t][1].hi, pr.q, pr.r0, pr.r1)};
+        }
+    }
+}
+
+// The hoisted key MAC of one child: ACC[b][k][I] = sum_J e_J[I] key[J][k][I] over the node's canonical
+// NTT-form digits E[b][I][J] (J != I) through the child's permutation plus the sign-mask term above,
+// and the child's own NTT-form target T = gal(c1) for J == I.  A thread owns two adjacent coefficients
+// (their sources are adjacent too) for BT batch entries, so each key and W word is read once per BT.
+// FP64 primes accumulate exact fp_mulmod products, 60-bit primes 128-bit sums (SEAL's lazy MAC).
 // Grid: 1-D, XCD-aware like k_bmac (the batch groups of one (coefficient block, I) share an XCD).
 template <int BT>
 __global__ void __launch_bounds__(256)
@@ -692,59 +799,10 @@ __global__ void __launch_bounds__(256)
     const int kI = I == l ? K - 1 : I;
     const DevPrime pr = primes[kI];
     const u64 k0 = (u64)xb * 512 + 2 * threadIdx.x;  // this thread's coefficients k0, k0 + 1
-    const u32 gs = galois_src((u32)k0, elt, logN);    // gal(k0 + 1) = gs ^ 1
-    const u64 sp = gs & ~1u;
-    const bool swp = gs & 1;
-    const ulonglong2 wv = *(const ulonglong2 *)(W + ((u64)kI << logN) + k0);
-    const int b0 = bg * BT;
-    U128 a0[BT][2], a1[BT][2];
-#pragma unroll
-    for (int t = 0; t < BT; ++t) a0[t][0] = a0[t][1] = a1[t][0] = a1[t][1] = U128{0, 0};
-    for (int J = 0; J < l; ++J) {
-        const ulonglong2 key0 = *(const ulonglong2 *)(key + (((u64)(J * 2 + 0) * K + kI) << logN) + k0);
-        const ulonglong2 key1 = *(const ulonglong2 *)(key + (((u64)(J * 2 + 1) * K + kI) << logN) + k0);
-        const u64 c = cji[J * K + kI];
-        const u64 cw0 = J == I ? 0 : mulmod(c, wv.x, pr), cw1 = J == I ? 0 : mulmod(c, wv.y, pr);
-#pragma unroll
-        for (int t = 0; t < BT; ++t) {
-            const int b = b0 + t;
-            if (b >= B) break;
-            const u64 *src = J == I ? X1.p + b * X1.sb + ((u64)J << logN)
-                                    : E + (((u64)((b * (l + 1) + I) * l + J)) << logN);
-            const ulonglong2 v = *(const ulonglong2 *)(src + sp);
-            u64 e0 = swp ? v.y : v.x, e1 = swp ? v.x : v.y;
-            if (J != I) {
-                e0 = addmod(e0, cw0, pr.q);
-                e1 = addmod(e1, cw1, pr.q);
-                const int *z = zl + (b * l + J) * (HEC_ZCAP + 1);
-                const int nz = min(z[0], HEC_ZCAP);
-                for (int zi = 0; zi < nz; ++zi) {  // zeros of D_J landing negated in this child (rare)
-                    u64 tt = ((u64)z[1 + zi] * elt) & (2 * N - 1);
-                    if (tt < N) continue;
-                    tt -= N;
-                    const u64 ex0 = ((2 * (u64)bitrev((u32)k0, logN) + 1) * tt) & (2 * N - 1);
-                    const u64 ex1 = ((2 * (u64)bitrev((u32)k0 + 1, logN) + 1) * tt) & (2 * N - 1);
-                    e0 = submod(e0, mulmod(c, psipow[((u64)kI << (logN + 1)) + ex0], pr), pr.q);
-                    e1 = submod(e1, mulmod(c, psipow[((u64)kI << (logN + 1)) + ex1], pr), pr.q);
-                }
-            }
-            mac128(a0[t][0], e0, key0.x);
-            mac128(a0[t][1], e1, key0.y);
-            mac128(a1[t][0], e0, key1.x);
-            mac128(a1[t][1], e1, key1.y);
-        }
-    }
-#pragma unroll
-    for (int t = 0; t < BT; ++t) {
-        const int b = b0 + t;
-        if (b >= B) break;
-        *(ulonglong2 *)(ACC + (((u64)((b * 2 + 0) * (l + 1) + I)) << logN) + k0) =
-            ulonglong2{barrett128(a0[t][0].lo, a0[t][0].hi, pr.q, pr.r0, pr.r1),
-                       barrett128(a0[t][1].lo, a0[t][1].hi, pr.q, pr.r0, pr.r1)};
-        *(ulonglong2 *)(ACC + (((u64)((b * 2 + 1) * (l + 1) + I)) << logN) + k0) =
-            ulonglong2{barrett128(a1[t][0].lo, a1[t][0].hi, pr.q, pr.r0, pr.r1),
-                       barrett128(a1[t][1].lo, a1[t][1].hi, pr.q, pr.r0, pr.r1)};
-    }
+    if (pr.fp)
+        hmac_body<BT, true>(X1, E, W, zl, key, ACC, B, l, K, logN, pr, I, kI, k0, bg * BT, cji, psipow, elt);
+    else
+        hmac_body<BT, false>(X1, E, W, zl, key, ACC, B, l, K, logN, pr, I, kI, k0, bg * BT, cji, psipow, elt);
 }
 
 void hoisted_mac(Ctx &c, PolyArr X1, const u64 *E, const u64 *W, const int *zl, const u64 *key, u64 *ACC, int B,
