@@ -353,13 +353,16 @@ void keyswitch(Ctx &c, Scratch &s, PolyArr T, const u64 *key, PolyArr IN, int in
 
 // hoisted mod-up data of one trie node (B targets at level l): D = INTT(c1) (canonical coefficient form),
 // E[b][I][J] = NTT_I(D_J mod q_I) (canonical NTT form, J != I), zero lists of D (see hec_kernels.hip)
+constexpr int HOIST_GROUP = 4;  // sibling rotations per fused hoisted MAC launch
 struct Hoist {
     u64 *D = nullptr, *E = nullptr;
     int *zl = nullptr;
+    u64 *acc[HOIST_GROUP] = {};  // key-switch accumulators of a sibling group (live across recursion)
 };
 std::size_t hoist_words(const Ctx &c, std::size_t B, std::size_t l)
 {
-    return c.N * B * (l + (l + 1) * l) + ((1 + B * l * (HEC_ZCAP + 1)) * sizeof(int) + 7) / 8 + 3 * 64;
+    return c.N * B * (l + (l + 1) * l + HOIST_GROUP * 2 * (l + 1)) + ((1 + B * l * (HEC_ZCAP + 1)) * sizeof(int) + 7) / 8 +
+           (3 + HOIST_GROUP) * 64;
 }
 Hoist hoist_alloc(const Ctx &c, Scratch &s, int B, int l)
 {
@@ -367,6 +370,7 @@ Hoist hoist_alloc(const Ctx &c, Scratch &s, int B, int l)
     h.D = s.take((u64)B * l * c.N);
     h.E = s.take((u64)B * (l + 1) * l * c.N);
     h.zl = reinterpret_cast<int *>(s.take(((1 + (u64)B * l * (HEC_ZCAP + 1)) * sizeof(int) + 7) / 8));
+    for (int q = 0; q < HOIST_GROUP; ++q) h.acc[q] = s.take((u64)B * 2 * (l + 1) * c.N);
     return h;
 }
 void hoist_node(Ctx &c, PolyArr X, int B, int l, const Hoist &h)
@@ -565,16 +569,43 @@ void walk_trie_hoisted(Ctx &c, Scratch &s, const RotTrie &t, int node, PolyArr s
 {
     for (std::size_t tag : t.nodes[node].terminals) visit(tag, src);
     const auto &ch = t.nodes[node].children;
-    const bool hoisted = (int)ch.size() >= min_children;
-    if (hoisted) hoist_node(c, src, B, l, hs[depth]);
-    for (int cn : ch) {
-        const u32 e = t.nodes[cn].elt;
-        const PolyArr dst{bufs.take(depth + 1), stride, (u64)l * c.N};
-        before_write(dst.p);
-        if (hoisted) hoisted_child(c, s, src, hs[depth], galois_negw(ctx, gk, e), gk.keys.at(e), dst, B, l, e);
-        else galois_ks(c, s, src, dst, B, l, e, gk.keys.at(e));
-        walk_trie_hoisted(c, s, t, cn, dst, depth + 1, B, l, ctx, gk, bufs, hs, stride, min_children, visit,
-                          before_write);
+    if ((int)ch.size() < min_children) {
+        for (int cn : ch) {
+            const u32 e = t.nodes[cn].elt;
+            const PolyArr dst{bufs.take(depth + 1), stride, (u64)l * c.N};
+            before_write(dst.p);
+            galois_ks(c, s, src, dst, B, l, e, gk.keys.at(e));
+            walk_trie_hoisted(c, s, t, cn, dst, depth + 1, B, l, ctx, gk, bufs, hs, stride, min_children, visit,
+                              before_write);
+        }
+        return;
+    }
+    const Hoist &h = hs[depth];
+    hoist_node(c, src, B, l, h);
+    const u64 N = c.N;
+    const std::size_t grp = (std::size_t)hoisted_group(c);
+    for (std::size_t g0 = 0; g0 < ch.size(); g0 += grp) {
+        const int ng = (int)std::min<std::size_t>(grp, ch.size() - g0);
+        HChildSpec kids[HOIST_GROUP];
+        for (int q = 0; q < ng; ++q) {
+            const u32 e = t.nodes[ch[g0 + q]].elt;
+            kids[q] = HChildSpec{e, (u32)invm(e, 2 * N), gk.keys.at(e), galois_negw(ctx, gk, e), h.acc[q]};
+        }
+        {
+            ProfScope ps(c, "ks_hmac");
+            hoisted_mac_multi(c, PolyArr{src.p + src.sk, src.sb, 0}, h.E, h.zl, kids, ng, B, l);
+        }
+        for (int q = 0; q < ng; ++q) {
+            const int cn = ch[g0 + q];
+            const PolyArr dst{bufs.take(depth + 1), stride, (u64)l * N};
+            before_write(dst.p);
+            const std::size_t top = s.top;
+            u64 *Z = s.take((u64)B * 2 * l * N);
+            moddown(c, h.acc[q], Z, PolyArr{src.p, src.sb, src.sk}, 1, dst, B, l, kids[q].elt);
+            s.top = top;
+            walk_trie_hoisted(c, s, t, cn, dst, depth + 1, B, l, ctx, gk, bufs, hs, stride, min_children, visit,
+                              before_write);
+        }
     }
 }
 
@@ -788,6 +819,7 @@ int hec_context_create(uint64_t N, const uint64_t *mod, uint64_t K, int device, 
         if (const char *f = std::getenv("HEC_FUSE_GALOIS")) c.fuse_galois = f[0] != '0';
         if (const char *f = std::getenv("HEC_FAN")) c.fan_out = f[0] != '0';
         if (const char *f = std::getenv("HEC_HOIST")) c.hoist = f[0] != '0';
+        if (const char *f = std::getenv("HEC_HMAC")) c.hmac_cfg = f[0] - '0';
         if (const char *f = std::getenv("HEC_HOIST_MIN")) c.hoist_min_children = std::max(1, std::atoi(f));
         if (const char *f = std::getenv("HEC_SPLIT_CLASSES")) c.split_classes = f[0] - '0';
         if (const char *f = std::getenv("HEC_TENSOR_DEFER")) c.tensor_defer_max = std::max(1, std::atoi(f));

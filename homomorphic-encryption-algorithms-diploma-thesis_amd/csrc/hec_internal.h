@@ -77,7 +77,9 @@ struct Ctx {
     int tensor_defer_max = 12;     // HEC_TENSOR_DEFER: terminals per deferred tensor batch (1 = immediate)
     int tensor_defer_bufs = 8;     // HEC_TENSOR_BUFS: rotation buffers per trie depth
     bool hoist = true;             // HEC_HOIST=0: no hoisted mod-up in the rotation trie walk
-    int hoist_min_children = 2;    // HEC_HOIST_MIN: children a trie node needs to be hoisted
+    int hoist_min_children = 2;
+    int hmac_cfg = 3;              // HEC_HMAC: 0 one hoisted MAC per child; siblings fused: 1 (4 x 1 batch),
+                                   // 2 (2 x 2), 3 (2 x 4, default), 4 (3 x 2) children x batch entries per thread    // HEC_HOIST_MIN: children a trie node needs to be hoisted
     bool fan_out = true;           // HEC_FAN=0: separate INTT pass A (fan-out fuses it into the forward passes A)
     bool fuse_galois = true;       // HEC_FUSE_GALOIS=0: materialise apply_galois before the key switch
     bool fused_modup_mac = true;  // HEC_FUSED_MODUP_MAC=0: separate mod-up pass B and key MAC kernels
@@ -130,6 +132,15 @@ void fan_modup(Ctx &c, const u64 *D, u64 *E, int B, int l, bool direct = false);
 void zero_scan(Ctx &c, const u64 *D, int nlimbs, int *zl);
 void hoisted_mac(Ctx &c, PolyArr X1, const u64 *E, const u64 *W, const int *zl, const u64 *key, u64 *ACC, int B,
                  int l, u32 elt);
+// the same for up to 4 sibling rotations at once (the node's digits read once for all of them)
+struct HChildSpec {
+    u32 elt, einv;  // Galois element and its inverse mod 2N
+    const u64 *key, *W;
+    u64 *ACC;
+};
+void hoisted_mac_multi(Ctx &c, PolyArr X1, const u64 *E, const int *zl, const HChildSpec *kids, int nkids, int B,
+                       int l);
+int hoisted_group(const Ctx &c);  // children per hoisted_mac_multi call for c.hmac_cfg
 void fan_divide_round(Ctx &c, const u64 *Y, u64 ysb, u64 ysk, u64 *Z, int B, int nk, int nl, int last_idx);
 void galois_permute(Ctx &c, PolyArr in, PolyArr out, int B, int nk, int nl, u32 elt);
 void tensor_acc(Ctx &c, PolyArr R, const u64 *A, u64 a_sk, PolyArr ACC, int B, int l, bool assign);

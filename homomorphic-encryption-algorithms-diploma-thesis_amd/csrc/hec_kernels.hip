@@ -816,6 +816,198 @@ void hoisted_mac(Ctx &c, PolyArr X1, const u64 *E, const u64 *W, const int *zl, 
     HEC_HIP(hipGetLastError());
 }
 
+// Sibling-fused hoisted MAC: the thread owns two adjacent SOURCE positions s, s + 1 of the node's digits
+// (read once, contiguous) and scatters their products to up to CG children: child c's output position is
+// k_c = gal_c^-1(s) (the inverse permutation is the Galois map of elt^-1), its key, sign-mask and zero
+// terms are gathered there.  The digits, the largest stream, are read once per CG children.
+struct HChild {
+    u32 elt, einv;
+    const u64 *key, *W;
+    u64 *ACC;
+};
+template <int CG>
+struct HChildren {
+    HChild c[CG];
+    int n;
+};
+
+template <int BT, int CG, bool FP>
+__device__ __forceinline__ void hmacm_body(PolyArr X1, const u64 *__restrict__ E, const int *__restrict__ zl,
+                                           const HChildren<CG> &ch, int B, int l, int K, int logN, const DevPrime &pr,
+                                           int I, int kI, u64 s0, int b0, const u64 *__restrict__ cji,
+                                           const u64 *__restrict__ psipow)
+{
+    const bool zeros = zl[0] != 0;
+    const u64 *pp = psipow + ((u64)kI << (logN + 1));
+    u64 kc[CG];       // even slot of child c's output pair
+    bool sw[CG];      // output pair swapped
+    ulonglong2 wv[CG];
+#pragma unroll
+    for (int q = 0; q < CG; ++q) {
+        if (q >= ch.n) break;
+        const u32 t = galois_src((u32)s0, ch.c[q].einv, logN);
+        kc[q] = t & ~1u;
+        sw[q] = t & 1;
+        const ulonglong2 w = *(const ulonglong2 *)(ch.c[q].W + ((u64)kI << logN) + kc[q]);
+        wv[q] = sw[q] ? ulonglong2{w.y, w.x} : w;  // in source order
+    }
+    double f[FP ? CG : 1][FP ? BT : 1][4];
+    U128 a[FP ? 1 : CG][FP ? 1 : BT][4];
+#pragma unroll
+    for (int q = 0; q < CG; ++q)
+#pragma unroll
+        for (int t = 0; t < BT; ++t)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                if constexpr (FP) f[q][t][r] = 0.0;
+                else a[q][t][r] = U128{0, 0};
+            }
+    for (int J = 0; J < l; ++J) {
+        u64 ev[BT][2];
+#pragma unroll
+        for (int t = 0; t < BT; ++t) {
+            const int b = b0 + t;
+            const u64 *src = J == I ? X1.p + b * X1.sb + ((u64)J << logN)
+                                    : E + (((u64)((b * (l + 1) + I) * l + J)) << logN);
+            const ulonglong2 v = b < B ? *(const ulonglong2 *)(src + s0) : ulonglong2{0, 0};
+            ev[t][0] = v.x;
+            ev[t][1] = v.y;
+        }
+        const u64 cj = cji[J * K + kI];
+#pragma unroll
+        for (int q = 0; q < CG; ++q) {
+            if (q >= ch.n) break;
+            const u64 *kp = ch.c[q].key + (((u64)(J * 2) * K + kI) << logN) + kc[q];
+            ulonglong2 k0 = *(const ulonglong2 *)kp, k1 = *(const ulonglong2 *)(kp + ((u64)K << logN));
+            if (sw[q]) {
+                k0 = ulonglong2{k0.y, k0.x};
+                k1 = ulonglong2{k1.y, k1.x};
+            }
+            u64 cw0 = 0, cw1 = 0;
+            if (J != I) {
+                cw0 = mulmod(cj, wv[q].x, pr);
+                cw1 = mulmod(cj, wv[q].y, pr);
+            }
+#pragma unroll
+            for (int t = 0; t < BT; ++t) {
+                if (b0 + t >= B) break;
+                u64 e0 = ev[t][0], e1 = ev[t][1];
+                if (J != I) {
+                    e0 = addmod(e0, cw0, pr.q);
+                    e1 = addmod(e1, cw1, pr.q);
+                    if (zeros) {  // output slots (in source order) of this child: kc ^ sw, kc ^ !sw
+                        const u64 ko0 = kc[q] | (u64)sw[q], ko1 = kc[q] | (u64)!sw[q];
+                        const int *z = zl + 1 + ((b0 + t) * l + J) * (HEC_ZCAP + 1);
+                        const int nz = min(z[0], HEC_ZCAP);
+                        const u64 N = 1ull << logN;
+                        for (int zi = 0; zi < nz; ++zi) {
+                            u64 tt = ((u64)z[1 + zi] * ch.c[q].elt) & (2 * N - 1);
+                            if (tt < N) continue;
+                            tt -= N;
+                            const u64 ex0 = ((2 * (u64)bitrev((u32)ko0, logN) + 1) * tt) & (2 * N - 1);
+                            const u64 ex1 = ((2 * (u64)bitrev((u32)ko1, logN) + 1) * tt) & (2 * N - 1);
+                            e0 = submod(e0, mulmod(cj, pp[ex0], pr), pr.q);
+                            e1 = submod(e1, mulmod(cj, pp[ex1], pr), pr.q);
+                        }
+                    }
+                }
+                if constexpr (FP) {
+                    const double d0 = u2d(e0), d1 = u2d(e1);
+                    f[q][t][0] += fp_mulmod(d0, u2d(k0.x), pr.qd, pr.qinv);
+                    f[q][t][1] += fp_mulmod(d1, u2d(k0.y), pr.qd, pr.qinv);
+                    f[q][t][2] += fp_mulmod(d0, u2d(k1.x), pr.qd, pr.qinv);
+                    f[q][t][3] += fp_mulmod(d1, u2d(k1.y), pr.qd, pr.qinv);
+                } else {
+                    mac128(a[q][t][0], e0, k0.x);
+                    mac128(a[q][t][1], e1, k0.y);
+                    mac128(a[q][t][2], e0, k1.x);
+                    mac128(a[q][t][3], e1, k1.y);
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < CG; ++q) {
+        if (q >= ch.n) break;
+#pragma unroll
+        for (int t = 0; t < BT; ++t) {
+            const int b = b0 + t;
+            if (b >= B) break;
+            u64 r[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                if constexpr (FP) r[i] = fp_canon(f[q][t][i], pr.qd, pr.qinv);
+                else r[i] = barrett128(a[q][t][i].lo, a[q][t][i].hi, pr.q, pr.r0, pr.r1);
+            }
+            u64 *o0 = ch.c[q].ACC + (((u64)((b * 2 + 0) * (l + 1) + I)) << logN) + kc[q];
+            u64 *o1 = ch.c[q].ACC + (((u64)((b * 2 + 1) * (l + 1) + I)) << logN) + kc[q];
+            *(ulonglong2 *)o0 = sw[q] ? ulonglong2{r[1], r[0]} : ulonglong2{r[0], r[1]};
+            *(ulonglong2 *)o1 = sw[q] ? ulonglong2{r[3], r[2]} : ulonglong2{r[2], r[3]};
+        }
+    }
+}
+
+template <int BT, int CG>
+__global__ void __launch_bounds__(256)
+    k_hmacm(PolyArr X1, const u64 *__restrict__ E, const int *__restrict__ zl, const HChildren<CG> ch, int B, int l,
+            int K, int logN, const DevPrime *__restrict__ primes, const int *__restrict__ Imap, int nI,
+            const u64 *__restrict__ cji, const u64 *__restrict__ psipow, int gpad)
+{
+    const u64 N = 1ull << logN;
+    const int nbg = (B + BT - 1) / BT;
+    const int w = blockIdx.x;
+    const int g8 = w & 7, rest = w >> 3, bg = rest % nbg, G = (rest / nbg) * 8 + g8;
+    const int X = (int)(N / 512);
+    if (G >= X * nI) return;
+    const int yi = G / X, xb = G % X;
+    const int I = Imap[yi];
+    const int kI = I == l ? K - 1 : I;
+    const DevPrime pr = primes[kI];
+    const u64 s0 = (u64)xb * 512 + 2 * threadIdx.x;
+    if (pr.fp)
+        hmacm_body<BT, CG, true>(X1, E, zl, ch, B, l, K, logN, pr, I, kI, s0, bg * BT, cji, psipow);
+    else
+        hmacm_body<BT, CG, false>(X1, E, zl, ch, B, l, K, logN, pr, I, kI, s0, bg * BT, cji, psipow);
+}
+
+template <int BT, int CG>
+static void launch_hmacm(Ctx &c, PolyArr X1, const u64 *E, const int *zl, const HChildSpec *kids, int nkids, int B,
+                         int l)
+{
+    HChildren<CG> ch{};
+    ch.n = nkids;
+    for (int q = 0; q < nkids; ++q)
+        ch.c[q] = HChild{kids[q].elt, kids[q].einv, kids[q].key, kids[q].W, kids[q].ACC};
+    const int nbg = (B + BT - 1) / BT, X = (int)(c.N / 512), gpad = (X * (l + 1) + 7) / 8 * 8;
+    k_hmacm<BT, CG><<<dim3((unsigned)(gpad * nbg)), 256, 0, c.stream>>>(X1, E, zl, ch, B, l, (int)c.K, c.logN,
+                                                                         c.primes, c.imap_at(l), l + 1, c.cji,
+                                                                         c.psipow, gpad);
+    HEC_HIP(hipGetLastError());
+}
+
+int hoisted_group(const Ctx &c)
+{
+    switch (c.hmac_cfg) {
+    case 1: return 4;
+    case 2: case 3: return 2;
+    case 4: return 3;
+    default: return 1;
+    }
+}
+
+void hoisted_mac_multi(Ctx &c, PolyArr X1, const u64 *E, const int *zl, const HChildSpec *kids, int nkids, int B,
+                       int l)
+{
+    if (nkids < 1 || nkids > hoisted_group(c)) throw std::invalid_argument("hoisted_mac_multi: group size");
+    switch (c.hmac_cfg) {
+    case 1: launch_hmacm<1, 4>(c, X1, E, zl, kids, nkids, B, l); break;
+    case 2: launch_hmacm<2, 2>(c, X1, E, zl, kids, nkids, B, l); break;
+    case 3: launch_hmacm<4, 2>(c, X1, E, zl, kids, nkids, B, l); break;
+    case 4: launch_hmacm<2, 3>(c, X1, E, zl, kids, nkids, B, l); break;
+    default: hoisted_mac(c, X1, E, kids[0].W, zl, kids[0].key, kids[0].ACC, B, l, kids[0].elt); break;
+    }
+}
+
 void fan_divide_round(Ctx &c, const u64 *Y, u64 ysb, u64 ysk, u64 *Z, int B, int nk, int nl, int last_idx)
 {
     if (nl > HEC_MAXL) throw std::invalid_argument("too many limbs");

@@ -278,7 +278,8 @@ def test_cfg3_matvec_small_n_bitexact(env15):
                                  {"HEC_SPLIT_CLASSES": "1"}, {"HEC_SPLIT_CLASSES": "2"},
                                  {"HEC_TENSOR_DEFER": "1"}, {"HEC_TENSOR_BUFS": "1"}, {"HEC_TENSOR_DEFER": "3"},
                                  {"HEC_FAN": "0"}, {"HEC_FAN": "1", "HEC_FUSE_GALOIS": "0"},
-                                 {"HEC_HOIST": "0"}, {"HEC_HOIST_MIN": "1"}, {"HEC_HOIST_MIN": "1", "HEC_FAN": "0"}])
+                                 {"HEC_HOIST": "0"}, {"HEC_HOIST_MIN": "1"}, {"HEC_HOIST_MIN": "1", "HEC_FAN": "0"},
+                                 {"HEC_HMAC": "0"}, {"HEC_HMAC": "1"}, {"HEC_HMAC": "2"}, {"HEC_HMAC": "4"}])
 def test_keyswitch_variants_bitexact(orc, hecdna, env):
     """The engine's alternative key-switch schedules (separate mod-up pass B + MAC kernels; the fused
     kernel's key-load placements) give the same bits as the oracle."""
