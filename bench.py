@@ -52,15 +52,16 @@ def algorithmic_bytes_per_matvec(N, l, n, B, ks):
     return (n * s_ct + ks * s_key + s_key) / B + ks * 2 * s_ct + n * s_ct + s_ct3 + s_ct
 
 
-def pmc_traffic(cls, B, logn, level):
+def pmc_traffic(kernel, B, logn, level, n):
     """HBM bytes per launch of the roofline kernel from the committed rocprofv3 PMC passes
-    (profiles/r01_pmc_k_bmac.json: FETCH_SIZE and WRITE_SIZE in separate passes, gfx950 FETCH x2
-    correction for its 16-B/lane reads), when they were taken at this configuration; else None."""
-    path = os.path.join(ROOT, "profiles", f"r01_pmc_k_bmac_B{B}.json")
-    if cls != "ks_bmac" or not os.path.exists(path):
+    (profiles/r01_pmc_<kernel>_B<B>.json, written by tools/pmc_summary.py: FETCH_SIZE and WRITE_SIZE in
+    separate passes, gfx950 FETCH x2 correction for 16-B/lane reads) when they were taken on this
+    configuration; else None."""
+    path = os.path.join(ROOT, "profiles", f"r01_pmc_{kernel}_B{B}.json")
+    if not os.path.exists(path):
         return None
     p = json.load(open(path))
-    if (p["batch"], p["logN"], p["level"]) != (B, logn, level):
+    if (p["batch"], p["logN"], p["level"], p.get("n")) != (B, logn, level, n):
         return None
     return p["traffic_bytes_per_dispatch"]
 
@@ -213,38 +214,37 @@ def main():
                 breakdown[cls] = {"ms": round(ms, 3), "launch_groups": cnt}
         ctx.profile(0)
 
-    # roofline for the dominant phase: algorithmic bytes of one launch group (compulsory reads + writes,
-    # SURVEY §8(d) units: limb = N*8 B, B targets, level l, K = l+1 key moduli) / its average duration
+    # roofline of the dominant single-kernel phase: its algorithmic bytes (compulsory reads + writes,
+    # SURVEY §8(d) units: limb = N*8 B, B targets, level l, K = l+1 key moduli) / its measured time.
+    #   ks_hmac = k_hmacm, the hoisted key MAC of a group of sibling rotations: per launch
+    #     the node's digits E (B l^2 limbs) + its c1 (B l), and per child the key (2 l K), the sign-mask
+    #     NTTs W (K) and the ACC output (2 B K); summed over the phase's launches and children
+    #   ks_bmac = k_bmac, fused mod-up pass B + key MAC of one non-hoisted rotation
     K = L + 1
     limb = N * 8
     Bt = args.batch
-    algo_limbs = {
-        "ks_intt": 2 * Bt * L,                                   # target limbs in, coefficient limbs out
-        "ks_modup_a": Bt * L + Bt * L * L,                       # D in, l^2 pass-A digit limbs out
-        "ks_bmac": Bt * L * L + Bt * L + 2 * L * K + 2 * Bt * K,  # pass-A digits + T + key in, ACC out
-        "ks_modup": Bt * L + Bt * L * L,                         # D in, l^2 NTT-form digits out
-        "ks_mac": Bt * L * L + Bt * L + 2 * L * K + 2 * Bt * K,   # digits + T + key in, ACC out
-        "ks_modup_h": Bt * L + Bt * L * L,                       # hoisted node: D in, l^2 NTT-form digits out
-        "ks_hmac": Bt * L * L + Bt * L + K + 2 * L * K + 2 * Bt * K,  # node digits + T + W + key in, ACC out
-        "ks_moddown": 2 * Bt * K + Bt * L + 2 * Bt * L,           # ACC + c0 in, rotated ct out
-        "galois": 4 * Bt * L,
-    }
+    from _helpers import rotation_trie_stats
+    _, _, h_children, _ = rotation_trie_stats(N, args.n)
+    phases = {}
+    if "ks_hmac" in breakdown:
+        nl = breakdown["ks_hmac"]["launch_groups"]
+        phases["ks_hmac"] = ("k_hmacm", nl * Bt * (L * L + L) + h_children * (2 * L * K + K + 2 * Bt * K))
+    if "ks_bmac" in breakdown:
+        nl = breakdown["ks_bmac"]["launch_groups"]
+        phases["ks_bmac"] = ("k_bmac", nl * (Bt * L * L + Bt * L + 2 * L * K + 2 * Bt * K))
     roof = None
-    cand = [c for c in algo_limbs if c in breakdown]
-    if cand:
-        dom = max(cand, key=lambda c: breakdown[c]["ms"])
+    if phases:
+        dom = max(phases, key=lambda c: breakdown[c]["ms"])
+        kern, limbs = phases[dom]
         bm = breakdown[dom]
         per = bm["ms"] / bm["launch_groups"]
-        algo = algo_limbs[dom] * limb
+        algo = limbs * limb / bm["launch_groups"]
         ach = algo / (per * 1e-3) / 1e9
-        kern = {"ks_bmac": "k_bmac (mod-up pass B + key MAC, fused)", "ks_modup": "k_ntt mod-up pass A+B",
-                "ks_hmac": "k_hmac (hoisted key MAC of one rotation)",
-                "ks_modup_h": "k_fan + k_ntt pass B (hoisted mod-up of a trie node)",
-                "ks_modup_a": "k_ntt mod-up pass A", "ks_mac": "k_ks_mac"}.get(dom, dom)
         roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(dom, args.batch, args.logn, L),
-                "kernel": kern,
-                "avg_ms": round(per, 4), "algorithmic_bytes_per_launch": algo}
+                "frac": round(ach / HBM_PEAK_GBS, 4),
+                "traffic": pmc_traffic(kern, args.batch, args.logn, L, args.n),
+                "kernel": kern, "avg_ms": round(per, 4), "algorithmic_bytes_per_launch": int(algo),
+                "launches_per_step": bm["launch_groups"]}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not ctpt:

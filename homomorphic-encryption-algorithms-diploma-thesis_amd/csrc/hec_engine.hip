@@ -15,6 +15,7 @@
 //   (5) OUT[b][k][i] = IN[b][k][i] + (ACC[b][k][i] - NTT_i(round(y))) * P^-1     divide_round
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <limits>
@@ -51,6 +52,20 @@ struct hec_galois_keys {
     hec_context *ctx = nullptr;
     std::map<u32, u64 *> keys;
     std::map<u32, u64 *> negw;  // hoisted mod-up: W_elt[I] = NTT_I(sign mask of elt), built on first use
+    // hoisted MAC: KW[elt, l][k][I] = sum_{J<l, J!=I} (q_J mod q_I) key_elt[J][k][I] mod q_I, built on first
+    // use per level, dropped when the key is replaced
+    std::map<std::pair<u32, int>, u64 *> kw;
+    void drop_kw(u32 elt)
+    {
+        for (auto it = kw.begin(); it != kw.end();) {
+            if (it->first.first == elt) {
+                (void)hipFree(it->second);
+                it = kw.erase(it);
+            } else {
+                ++it;
+            }
+        }
+    }
 };
 
 namespace {
@@ -428,6 +443,18 @@ const u64 *galois_negw(hec_context *ctx, hec_galois_keys &gk, u32 elt)
     return W;
 }
 
+// the sign-mask key sums of a Galois key at level l (built on first use, see k_keyw)
+const u64 *galois_kw(hec_context *ctx, hec_galois_keys &gk, u32 elt, int l)
+{
+    auto it = gk.kw.find({elt, l});
+    if (it != gk.kw.end()) return it->second;
+    Ctx &c = ctx->c;
+    u64 *KW = dalloc((std::size_t)2 * (l + 1) * c.N);
+    key_wsum(c, gk.keys.at(elt), KW, l);
+    gk.kw[{elt, l}] = KW;
+    return KW;
+}
+
 // X (size 2) -> OUT = apply_galois(X, elt) followed by key switching (SEAL apply_galois_inplace).
 // When OUT does not alias X the permutation is applied inside the key switch's loads (the INTT of c1,
 // the target reuse in the MAC, the c0 add in the mod-down) and never materialised; otherwise X is
@@ -589,7 +616,8 @@ void walk_trie_hoisted(Ctx &c, Scratch &s, const RotTrie &t, int node, PolyArr s
         HChildSpec kids[HOIST_GROUP];
         for (int q = 0; q < ng; ++q) {
             const u32 e = t.nodes[ch[g0 + q]].elt;
-            kids[q] = HChildSpec{e, (u32)invm(e, 2 * N), gk.keys.at(e), galois_negw(ctx, gk, e), h.acc[q]};
+            kids[q] = HChildSpec{e, (u32)invm(e, 2 * N), gk.keys.at(e), galois_negw(ctx, gk, e), h.acc[q],
+                                 galois_kw(ctx, gk, e, l)};
         }
         {
             ProfScope ps(c, "ks_hmac");
@@ -697,7 +725,10 @@ void matvec_core(hec_context *ctx, const hec_ciphertext *const *diags, const hec
     };
     if (hoist) {
         hec_galois_keys &gkm = const_cast<hec_galois_keys &>(*gk);  // negw is a per-key cache
-        for (std::size_t nd = 1; nd < trie.nodes.size(); ++nd) galois_negw(ctx, gkm, trie.nodes[nd].elt);
+        for (std::size_t nd = 1; nd < trie.nodes.size(); ++nd) {
+            galois_negw(ctx, gkm, trie.nodes[nd].elt);
+            galois_kw(ctx, gkm, trie.nodes[nd].elt, (int)l);
+        }
         std::vector<Hoist> hs(D);
         for (int d = 0; d < D; ++d) hs[d] = hoist_alloc(c, s, (int)p, (int)l);
         HEC_HIP(hipMemsetAsync(c.zflag, 0, sizeof(int), c.stream));
@@ -818,6 +849,8 @@ int hec_context_create(uint64_t N, const uint64_t *mod, uint64_t K, int device, 
         if (const char *f = std::getenv("HEC_BMAC_KEYS")) c.bmac_keys = f[0] - '0';
         if (const char *f = std::getenv("HEC_FUSE_GALOIS")) c.fuse_galois = f[0] != '0';
         if (const char *f = std::getenv("HEC_FAN")) c.fan_out = f[0] != '0';
+        if (const char *f = std::getenv("HEC_FANG"))
+            std::sscanf(f, "%d,%d,%d", &c.fan_groups_moddown, &c.fan_groups_modup, &c.fan_groups_hoist);
         if (const char *f = std::getenv("HEC_HOIST")) c.hoist = f[0] != '0';
         if (const char *f = std::getenv("HEC_HMAC")) c.hmac_cfg = f[0] - '0';
         if (const char *f = std::getenv("HEC_HOIST_MIN")) c.hoist_min_children = std::max(1, std::atoi(f));
@@ -1253,6 +1286,7 @@ int hec_galois_keys_add(hec_galois_keys *gk, uint32_t elt, const uint64_t *host)
         gk_check_elt(c, elt);
         u64 *&d = gk->keys[elt];
         if (!d) d = dalloc(key_words(c));
+        gk->drop_kw(elt);
         HEC_HIP(hipMemcpy(d, host, key_words(c) * sizeof(u64), hipMemcpyHostToDevice));
     });
 }
@@ -1265,6 +1299,7 @@ int hec_galois_keys_add_uniform(hec_galois_keys *gk, uint32_t elt, uint64_t seed
         gk_check_elt(c, elt);
         u64 *&d = gk->keys[elt];
         if (!d) d = dalloc(key_words(c));
+        gk->drop_kw(elt);
         fill_uniform(c, d, (int)(c.L * 2), (int)c.K, 0, 0, seed);
         HEC_HIP(hipStreamSynchronize(c.stream));
     });
@@ -1277,6 +1312,7 @@ int hec_galois_keys_destroy(hec_galois_keys *gk)
         (void)hipStreamSynchronize(gk->ctx->c.stream);
         for (auto &kv : gk->keys) (void)hipFree(kv.second);
         for (auto &kv : gk->negw) (void)hipFree(kv.second);
+        for (auto &kv : gk->kw) (void)hipFree(kv.second);
         delete gk;
     });
 }

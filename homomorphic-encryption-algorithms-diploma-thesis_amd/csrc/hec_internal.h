@@ -80,6 +80,9 @@ struct Ctx {
     int hoist_min_children = 2;
     int hmac_cfg = 3;              // HEC_HMAC: 0 one hoisted MAC per child; siblings fused: 1 (4 x 1 batch),
                                    // 2 (2 x 2), 3 (2 x 4, default), 4 (3 x 2) children x batch entries per thread    // HEC_HOIST_MIN: children a trie node needs to be hoisted
+    int fan_groups_moddown = 1;    // HEC_FANG="moddown,modup,hoist": target groups per k_fan source (blocks
+    int fan_groups_modup = 1;      // per launch x groups; the source's inverse pass is repeated per group)
+    int fan_groups_hoist = 1;
     bool fan_out = true;           // HEC_FAN=0: separate INTT pass A (fan-out fuses it into the forward passes A)
     bool fuse_galois = true;       // HEC_FUSE_GALOIS=0: materialise apply_galois before the key switch
     bool fused_modup_mac = true;  // HEC_FUSED_MODUP_MAC=0: separate mod-up pass B and key MAC kernels
@@ -137,7 +140,10 @@ struct HChildSpec {
     u32 elt, einv;  // Galois element and its inverse mod 2N
     const u64 *key, *W;
     u64 *ACC;
+    const u64 *KW;  // key_wsum of the child's key at this level
 };
+// KW[k][I] = sum_{J<l, J!=I} (q_J mod q_I) key[J][k][I] mod q_I, I in [0, l] (I == l: P), k in {0, 1}
+void key_wsum(Ctx &c, const u64 *key, u64 *KW, int l);
 void hoisted_mac_multi(Ctx &c, PolyArr X1, const u64 *E, const int *zl, const HChildSpec *kids, int nkids, int B,
                        int l);
 int hoisted_group(const Ctx &c);  // children per hoisted_mac_multi call for c.hmac_cfg

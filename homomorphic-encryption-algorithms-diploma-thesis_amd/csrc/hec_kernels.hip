@@ -586,8 +586,10 @@ __global__ void __launch_bounds__(NSEG *(1 << LOGP) / 16)
             else d[it] = shoup(v, ps.ninv, ps.ninv_q, ps.q);
         }
     }
-    const int nt = fan.ntargets();
-    for (int t = 0; t < nt; ++t) {
+    // target group blockIdx.z of gridDim.z: more blocks per launch when the job count is small (the
+    // source pass is then repeated per group)
+    const int nt = fan.ntargets(), t0 = blockIdx.z * nt / gridDim.z, t1 = (blockIdx.z + 1) * nt / gridDim.z;
+    for (int t = t0; t < t1; ++t) {
         const auto tg = fan.tgt(blockIdx.y, t);
         if (!tg.valid) continue;
         const DevPrime pt = primes[tg.prime];
@@ -608,32 +610,34 @@ __global__ void __launch_bounds__(NSEG *(1 << LOGP) / 16)
 }
 
 template <int LOGR, int LOGC, int NA, class FAN>
-static void run_fan(Ctx &c, int njobs, const FAN &fan)
+static void run_fan(Ctx &c, int njobs, const FAN &fan, int groups)
 {
     constexpr int R = 1 << LOGR, C = 1 << LOGC;
     const TwTables fwd{c.tw, c.twb, c.twf, c.twbf}, inv{c.itw, c.itwb, c.itwf, c.itwbf};
-    k_fan<LOGR, NA><<<dim3(C / NA, njobs), NA * R / 16, 0, c.stream>>>(fan, inv, fwd, c.primes, c.logN);
+    k_fan<LOGR, NA><<<dim3(C / NA, njobs, groups), NA * R / 16, 0, c.stream>>>(fan, inv, fwd, c.primes, c.logN);
     HEC_HIP(hipGetLastError());
 }
 template <class FAN>
-static void fan_dispatch(Ctx &c, int njobs, const FAN &fan)
+static void fan_dispatch(Ctx &c, int njobs, const FAN &fan, int groups = 1)
 {
+    groups = std::max(1, groups);
     switch (c.logN) {
-    case 10: run_fan<5, 5, 32>(c, njobs, fan); break;
-    case 11: run_fan<6, 5, 32>(c, njobs, fan); break;
-    case 12: run_fan<6, 6, 64>(c, njobs, fan); break;
-    case 13: run_fan<7, 6, 32>(c, njobs, fan); break;
-    case 14: run_fan<7, 7, 32>(c, njobs, fan); break;
-    case 15: run_fan<8, 7, 16>(c, njobs, fan); break;
-    case 16: run_fan<8, 8, 16>(c, njobs, fan); break;
+    case 10: run_fan<5, 5, 32>(c, njobs, fan, groups); break;
+    case 11: run_fan<6, 5, 32>(c, njobs, fan, groups); break;
+    case 12: run_fan<6, 6, 64>(c, njobs, fan, groups); break;
+    case 13: run_fan<7, 6, 32>(c, njobs, fan, groups); break;
+    case 14: run_fan<7, 7, 32>(c, njobs, fan, groups); break;
+    case 15: run_fan<8, 7, 16>(c, njobs, fan, groups); break;
+    case 16: run_fan<8, 8, 16>(c, njobs, fan, groups); break;
     default: throw std::invalid_argument("poly_modulus_degree must be 2^10 .. 2^16");
     }
 }
 
 void fan_modup(Ctx &c, const u64 *D, u64 *E, int B, int l, bool direct)
 {
-    if (direct) fan_dispatch(c, B * l, FanModUpT<true>{D, E, l, c.logN, (int)c.K - 1, c.primes});
-    else fan_dispatch(c, B * l, FanModUp{D, E, l, c.logN, (int)c.K - 1, c.primes});
+    const int g = std::min(direct ? c.fan_groups_hoist : c.fan_groups_modup, l + 1);
+    if (direct) fan_dispatch(c, B * l, FanModUpT<true>{D, E, l, c.logN, (int)c.K - 1, c.primes}, g);
+    else fan_dispatch(c, B * l, FanModUp{D, E, l, c.logN, (int)c.K - 1, c.primes}, g);
 }
 
 // ================================================================================ hoisted mod-up ==
@@ -824,6 +828,7 @@ struct HChild {
     u32 elt, einv;
     const u64 *key, *W;
     u64 *ACC;
+    const u64 *KW;
 };
 template <int CG>
 struct HChildren {
@@ -831,6 +836,10 @@ struct HChildren {
     int n;
 };
 
+// The sign-mask term is linear in the digits, so it leaves the digit loop:
+//   ACC = sum_J key_J (E_J o gal - c_J Z_J) + W_elt KW,  KW = sum_{J != I} c_J key_J  (k_keyw, per key and level)
+// with c_J = q_J mod q_I and Z_J the (rare) zero corrections: one modular product per child and output word
+// instead of one per digit.  Every term is exact mod q_I, so the canonical result is unchanged.
 template <int BT, int CG, bool FP>
 __device__ __forceinline__ void hmacm_body(PolyArr X1, const u64 *__restrict__ E, const int *__restrict__ zl,
                                            const HChildren<CG> &ch, int B, int l, int K, int logN, const DevPrime &pr,
@@ -841,7 +850,7 @@ __device__ __forceinline__ void hmacm_body(PolyArr X1, const u64 *__restrict__ E
     const u64 *pp = psipow + ((u64)kI << (logN + 1));
     u64 kc[CG];       // even slot of child c's output pair
     bool sw[CG];      // output pair swapped
-    ulonglong2 wv[CG];
+    u64 wk[CG][4];    // W KW in source order: (k = 0: s0, s0 + 1), (k = 1: s0, s0 + 1)
 #pragma unroll
     for (int q = 0; q < CG; ++q) {
         if (q >= ch.n) break;
@@ -849,7 +858,16 @@ __device__ __forceinline__ void hmacm_body(PolyArr X1, const u64 *__restrict__ E
         kc[q] = t & ~1u;
         sw[q] = t & 1;
         const ulonglong2 w = *(const ulonglong2 *)(ch.c[q].W + ((u64)kI << logN) + kc[q]);
-        wv[q] = sw[q] ? ulonglong2{w.y, w.x} : w;  // in source order
+        const ulonglong2 m0 = *(const ulonglong2 *)(ch.c[q].KW + ((u64)I << logN) + kc[q]);
+        const ulonglong2 m1 = *(const ulonglong2 *)(ch.c[q].KW + ((u64)(l + 1 + I) << logN) + kc[q]);
+        wk[q][0] = mulmod(w.x, m0.x, pr);
+        wk[q][1] = mulmod(w.y, m0.y, pr);
+        wk[q][2] = mulmod(w.x, m1.x, pr);
+        wk[q][3] = mulmod(w.y, m1.y, pr);
+        if (sw[q]) {
+            u64 x = wk[q][0]; wk[q][0] = wk[q][1]; wk[q][1] = x;
+            x = wk[q][2]; wk[q][2] = wk[q][3]; wk[q][3] = x;
+        }
     }
     double f[FP ? CG : 1][FP ? BT : 1][4];
     U128 a[FP ? 1 : CG][FP ? 1 : BT][4];
@@ -859,8 +877,9 @@ __device__ __forceinline__ void hmacm_body(PolyArr X1, const u64 *__restrict__ E
         for (int t = 0; t < BT; ++t)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                if constexpr (FP) f[q][t][r] = 0.0;
-                else a[q][t][r] = U128{0, 0};
+                const u64 w0 = q < ch.n ? wk[q][r] : 0;
+                if constexpr (FP) f[q][t][r] = u2d(w0);
+                else a[q][t][r] = U128{w0, 0};
             }
     for (int J = 0; J < l; ++J) {
         u64 ev[BT][2];
@@ -883,32 +902,23 @@ __device__ __forceinline__ void hmacm_body(PolyArr X1, const u64 *__restrict__ E
                 k0 = ulonglong2{k0.y, k0.x};
                 k1 = ulonglong2{k1.y, k1.x};
             }
-            u64 cw0 = 0, cw1 = 0;
-            if (J != I) {
-                cw0 = mulmod(cj, wv[q].x, pr);
-                cw1 = mulmod(cj, wv[q].y, pr);
-            }
 #pragma unroll
             for (int t = 0; t < BT; ++t) {
                 if (b0 + t >= B) break;
                 u64 e0 = ev[t][0], e1 = ev[t][1];
-                if (J != I) {
-                    e0 = addmod(e0, cw0, pr.q);
-                    e1 = addmod(e1, cw1, pr.q);
-                    if (zeros) {  // output slots (in source order) of this child: kc ^ sw, kc ^ !sw
-                        const u64 ko0 = kc[q] | (u64)sw[q], ko1 = kc[q] | (u64)!sw[q];
-                        const int *z = zl + 1 + ((b0 + t) * l + J) * (HEC_ZCAP + 1);
-                        const int nz = min(z[0], HEC_ZCAP);
-                        const u64 N = 1ull << logN;
-                        for (int zi = 0; zi < nz; ++zi) {
-                            u64 tt = ((u64)z[1 + zi] * ch.c[q].elt) & (2 * N - 1);
-                            if (tt < N) continue;
-                            tt -= N;
-                            const u64 ex0 = ((2 * (u64)bitrev((u32)ko0, logN) + 1) * tt) & (2 * N - 1);
-                            const u64 ex1 = ((2 * (u64)bitrev((u32)ko1, logN) + 1) * tt) & (2 * N - 1);
-                            e0 = submod(e0, mulmod(cj, pp[ex0], pr), pr.q);
-                            e1 = submod(e1, mulmod(cj, pp[ex1], pr), pr.q);
-                        }
+                if (J != I && zeros) {  // output slots (in source order) of this child: kc ^ sw, kc ^ !sw
+                    const u64 ko0 = kc[q] | (u64)sw[q], ko1 = kc[q] | (u64)!sw[q];
+                    const int *z = zl + 1 + ((b0 + t) * l + J) * (HEC_ZCAP + 1);
+                    const int nz = min(z[0], HEC_ZCAP);
+                    const u64 N = 1ull << logN;
+                    for (int zi = 0; zi < nz; ++zi) {
+                        u64 tt = ((u64)z[1 + zi] * ch.c[q].elt) & (2 * N - 1);
+                        if (tt < N) continue;
+                        tt -= N;
+                        const u64 ex0 = ((2 * (u64)bitrev((u32)ko0, logN) + 1) * tt) & (2 * N - 1);
+                        const u64 ex1 = ((2 * (u64)bitrev((u32)ko1, logN) + 1) * tt) & (2 * N - 1);
+                        e0 = submod(e0, mulmod(cj, pp[ex0], pr), pr.q);
+                        e1 = submod(e1, mulmod(cj, pp[ex1], pr), pr.q);
                     }
                 }
                 if constexpr (FP) {
@@ -947,6 +957,30 @@ __device__ __forceinline__ void hmacm_body(PolyArr X1, const u64 *__restrict__ E
     }
 }
 
+// KW[k][I][t] = sum_{J<l, J != I} (q_J mod q_I) key[J][k][I][t] mod q_I (128-bit lazy sum, one Barrett)
+__global__ void __launch_bounds__(256) k_keyw(const u64 *__restrict__ key, u64 *__restrict__ KW, int l, int K,
+                                              int logN, const DevPrime *__restrict__ primes,
+                                              const u64 *__restrict__ cji)
+{
+    const u64 N = 1ull << logN;
+    const u64 t = (u64)blockIdx.x * 256 + threadIdx.x;
+    const int I = blockIdx.y, k = blockIdx.z;
+    if (t >= N) return;
+    const int kI = I == l ? K - 1 : I;
+    const DevPrime pr = primes[kI];
+    U128 acc{0, 0};
+    for (int J = 0; J < l; ++J)
+        if (J != I) mac128(acc, cji[J * K + kI], key[(((u64)(J * 2 + k) * K + kI) << logN) + t]);
+    KW[((u64)(k * (l + 1) + I) << logN) + t] = barrett128(acc.lo, acc.hi, pr.q, pr.r0, pr.r1);
+}
+
+void key_wsum(Ctx &c, const u64 *key, u64 *KW, int l)
+{
+    k_keyw<<<dim3((unsigned)(c.N / 256), l + 1, 2), 256, 0, c.stream>>>(key, KW, l, (int)c.K, c.logN, c.primes,
+                                                                        c.cji);
+    HEC_HIP(hipGetLastError());
+}
+
 template <int BT, int CG>
 __global__ void __launch_bounds__(256)
     k_hmacm(PolyArr X1, const u64 *__restrict__ E, const int *__restrict__ zl, const HChildren<CG> ch, int B, int l,
@@ -977,7 +1011,7 @@ static void launch_hmacm(Ctx &c, PolyArr X1, const u64 *E, const int *zl, const 
     HChildren<CG> ch{};
     ch.n = nkids;
     for (int q = 0; q < nkids; ++q)
-        ch.c[q] = HChild{kids[q].elt, kids[q].einv, kids[q].key, kids[q].W, kids[q].ACC};
+        ch.c[q] = HChild{kids[q].elt, kids[q].einv, kids[q].key, kids[q].W, kids[q].ACC, kids[q].KW};
     const int nbg = (B + BT - 1) / BT, X = (int)(c.N / 512), gpad = (X * (l + 1) + 7) / 8 * 8;
     k_hmacm<BT, CG><<<dim3((unsigned)(gpad * nbg)), 256, 0, c.stream>>>(X1, E, zl, ch, B, l, (int)c.K, c.logN,
                                                                          c.primes, c.imap_at(l), l + 1, c.cji,
@@ -1015,7 +1049,7 @@ void fan_divide_round(Ctx &c, const u64 *Y, u64 ysb, u64 ysk, u64 *Z, int B, int
     f.Y = Y; f.ysb = ysb; f.ysk = ysk; f.Z = Z; f.nk = nk; f.nl = nl; f.logN = c.logN; f.last_idx = last_idx;
     f.last = c.q[last_idx]; f.half = f.last >> 1; f.primes = c.primes;
     for (int i = 0; i < nl; ++i) f.fix[i] = c.q[i] - (f.half % c.q[i]);
-    fan_dispatch(c, B * nk, f);
+    fan_dispatch(c, B * nk, f, std::min(c.fan_groups_moddown, nl));
 }
 
 // ====================================================================== fused mod-up B + MAC ==

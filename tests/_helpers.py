@@ -62,6 +62,34 @@ def ks_count(N, n, elts=None):
     return sum(count(j) for j in range(1, n))
 
 
+def rotation_trie_stats(N, n, min_children=2):
+    """The engine's rotation prefix trie for j = 1..n-1 (csrc/hec_engine.hip RotTrie): SEAL's key-switch
+    sequence per rotation (one key for +-2^i, else the NAF terms, least significant first).  Returns
+    (key switches, hoisted nodes, children of hoisted nodes, children of the other nodes); a node is
+    hoisted when it has at least min_children children (HEC_HOIST_MIN)."""
+    def naf(v):
+        res, i = [], 0
+        while v:
+            z = (2 - (v & 3)) if v & 1 else 0
+            v = (v - z) >> 1
+            if z:
+                res.append(z << i)
+            i += 1
+        return res
+    kids = {(): 0}
+    for j in range(1, n):
+        seq = [j] if j & (j - 1) == 0 else [s for s in naf(j) if abs(s) != N // 2]
+        p = ()
+        for e in seq:
+            c = p + (e,)
+            if c not in kids:
+                kids[c] = 0
+                kids[p] += 1
+            p = c
+    hoisted = [k for k in kids.values() if k >= min_children]
+    return len(kids) - 1, len(hoisted), sum(hoisted), sum(k for k in kids.values() if 0 < k < min_children)
+
+
 def reference_matrix(n):
     """The reference's demo data (src/demos/matrix_operations.cpp:1079-1087): column c, row r ->
     2 + n*c + r.  Returned as M[r][c]."""

@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round-end measurement: bench line (with CPU baseline), rocprofv3 kernel-trace stats of the same
-# workload, and FETCH_SIZE / WRITE_SIZE PMC passes (separate passes, gfx950 slot limits) on k_bmac.
+# workload, and FETCH_SIZE / WRITE_SIZE PMC passes (separate passes, gfx950 slot limits) on the
+# roofline kernels k_hmacm and k_bmac, summarised into gpurun_out/<tag>/pmc_<kernel>_B32.json.
 # usage: bash tools/gpu_profile.sh <tag>
 set -o pipefail
 TAG=${1:-r01}
@@ -11,6 +12,10 @@ timeout -k 10 400 python bench.py > $OUT/bench.json 2> $OUT/bench.err || { tail 
 tail -1 $OUT/bench.json | cut -c1-400
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -T --output-format csv -d $OUT/trace -o run -- python3 $GRAFT_REPO_ROOT/bench.py --no-cpu-baseline > $OUT/trace.log 2>&1 || { tail $OUT/trace.log; exit 1; }
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex k_bmac --output-format csv -d $OUT/pmc_fetch -o run -- python3 $GRAFT_REPO_ROOT/bench.py --n 256 --no-cpu-baseline --no-profile --steps 1 --warmup 1 > $OUT/pmc_fetch.log 2>&1 || { tail $OUT/pmc_fetch.log; exit 1; }
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex k_bmac --output-format csv -d $OUT/pmc_write -o run -- python3 $GRAFT_REPO_ROOT/bench.py --n 256 --no-cpu-baseline --no-profile --steps 1 --warmup 1 > $OUT/pmc_write.log 2>&1 || { tail $OUT/pmc_write.log; exit 1; }
-find $OUT -name "*.csv" | head -20
+PMCARGS="--no-cpu-baseline --no-profile --steps 1 --warmup 0"
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "k_hmacm|k_bmac" --output-format csv -d $OUT/pmc_fetch -o run -- python3 $GRAFT_REPO_ROOT/bench.py $PMCARGS > $OUT/pmc_fetch.log 2>&1 || { tail $OUT/pmc_fetch.log; exit 1; }
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "k_hmacm|k_bmac" --output-format csv -d $OUT/pmc_write -o run -- python3 $GRAFT_REPO_ROOT/bench.py $PMCARGS > $OUT/pmc_write.log 2>&1 || { tail $OUT/pmc_write.log; exit 1; }
+cd $GRAFT_REPO_ROOT
+for k in k_hmacm k_bmac; do
+  python tools/pmc_summary.py $OUT/pmc_fetch/run_counter_collection.csv $OUT/pmc_write/run_counter_collection.csv $k 32 15 10 4096 $OUT/pmc_${k}_B32.json "rocprofv3 --pmc FETCH_SIZE (then WRITE_SIZE, separate pass) --kernel-include-regex 'k_hmacm|k_bmac' -- python3 bench.py $PMCARGS" || exit 1
+done
