@@ -368,7 +368,7 @@ void keyswitch(Ctx &c, Scratch &s, PolyArr T, const u64 *key, PolyArr IN, int in
 
 // hoisted mod-up data of one trie node (B targets at level l): D = INTT(c1) (canonical coefficient form),
 // E[b][I][J] = NTT_I(D_J mod q_I) (canonical NTT form, J != I), zero lists of D (see hec_kernels.hip)
-constexpr int HOIST_GROUP = 4;  // sibling rotations per fused hoisted MAC launch
+constexpr int HOIST_GROUP = 6;  // sibling rotations per fused hoisted MAC launch
 struct Hoist {
     u64 *D = nullptr, *E = nullptr;
     int *zl = nullptr;
@@ -852,7 +852,7 @@ int hec_context_create(uint64_t N, const uint64_t *mod, uint64_t K, int device, 
         if (const char *f = std::getenv("HEC_FANG"))
             std::sscanf(f, "%d,%d,%d", &c.fan_groups_moddown, &c.fan_groups_modup, &c.fan_groups_hoist);
         if (const char *f = std::getenv("HEC_HOIST")) c.hoist = f[0] != '0';
-        if (const char *f = std::getenv("HEC_HMAC")) c.hmac_cfg = f[0] - '0';
+        if (const char *f = std::getenv("HEC_HMAC")) c.hmac_cfg = std::atoi(f);
         if (const char *f = std::getenv("HEC_HOIST_MIN")) c.hoist_min_children = std::max(1, std::atoi(f));
         if (const char *f = std::getenv("HEC_SPLIT_CLASSES")) c.split_classes = f[0] - '0';
         if (const char *f = std::getenv("HEC_TENSOR_DEFER")) c.tensor_defer_max = std::max(1, std::atoi(f));

@@ -142,6 +142,7 @@ struct HChildSpec {
     u64 *ACC;
     const u64 *KW;  // key_wsum of the child's key at this level
 };
+constexpr int HMAC_MAX_CHILDREN = 6;  // largest hoisted_group()
 // KW[k][I] = sum_{J<l, J!=I} (q_J mod q_I) key[J][k][I] mod q_I, I in [0, l] (I == l: P), k in {0, 1}
 void key_wsum(Ctx &c, const u64 *key, u64 *KW, int l);
 void hoisted_mac_multi(Ctx &c, PolyArr X1, const u64 *E, const int *zl, const HChildSpec *kids, int nkids, int B,

@@ -883,6 +883,7 @@ __device__ __forceinline__ void hmacm_body(PolyArr X1, const u64 *__restrict__ E
             }
     for (int J = 0; J < l; ++J) {
         u64 ev[BT][2];
+        double dv[FP ? BT : 1][2];  // FP64 class: the digits as doubles, converted once for all children
 #pragma unroll
         for (int t = 0; t < BT; ++t) {
             const int b = b0 + t;
@@ -891,6 +892,10 @@ __device__ __forceinline__ void hmacm_body(PolyArr X1, const u64 *__restrict__ E
             const ulonglong2 v = b < B ? *(const ulonglong2 *)(src + s0) : ulonglong2{0, 0};
             ev[t][0] = v.x;
             ev[t][1] = v.y;
+            if constexpr (FP) {
+                dv[t][0] = u2d(v.x);
+                dv[t][1] = u2d(v.y);
+            }
         }
         const u64 cj = cji[J * K + kI];
 #pragma unroll
@@ -906,6 +911,11 @@ __device__ __forceinline__ void hmacm_body(PolyArr X1, const u64 *__restrict__ E
             for (int t = 0; t < BT; ++t) {
                 if (b0 + t >= B) break;
                 u64 e0 = ev[t][0], e1 = ev[t][1];
+                double d0 = 0, d1 = 0;
+                if constexpr (FP) {
+                    d0 = dv[t][0];
+                    d1 = dv[t][1];
+                }
                 if (J != I && zeros) {  // output slots (in source order) of this child: kc ^ sw, kc ^ !sw
                     const u64 ko0 = kc[q] | (u64)sw[q], ko1 = kc[q] | (u64)!sw[q];
                     const int *z = zl + 1 + ((b0 + t) * l + J) * (HEC_ZCAP + 1);
@@ -920,9 +930,12 @@ __device__ __forceinline__ void hmacm_body(PolyArr X1, const u64 *__restrict__ E
                         e0 = submod(e0, mulmod(cj, pp[ex0], pr), pr.q);
                         e1 = submod(e1, mulmod(cj, pp[ex1], pr), pr.q);
                     }
+                    if constexpr (FP) {
+                        d0 = u2d(e0);
+                        d1 = u2d(e1);
+                    }
                 }
                 if constexpr (FP) {
-                    const double d0 = u2d(e0), d1 = u2d(e1);
                     f[q][t][0] += fp_mulmod(d0, u2d(k0.x), pr.qd, pr.qinv);
                     f[q][t][1] += fp_mulmod(d1, u2d(k0.y), pr.qd, pr.qinv);
                     f[q][t][2] += fp_mulmod(d0, u2d(k1.x), pr.qd, pr.qinv);
@@ -981,30 +994,35 @@ void key_wsum(Ctx &c, const u64 *key, u64 *KW, int l)
     HEC_HIP(hipGetLastError());
 }
 
-template <int BT, int CG>
-__global__ void __launch_bounds__(256)
+// Two grid segments: the integer-arithmetic targets (Imap[0, nint), 128-bit accumulators) with BTI batch
+// entries per thread, then the FP64 targets with BTF, so neither class carries the other's register
+// budget.  Each segment is XCD-aware: the batch groups of one (coefficient block, I) share an XCD.
+template <int BTF, int BTI, int CG, int MINW>
+__global__ void __launch_bounds__(256, MINW)  // MINW waves per SIMD: 3 -> <= 168 VGPRs, 2 -> <= 256
     k_hmacm(PolyArr X1, const u64 *__restrict__ E, const int *__restrict__ zl, const HChildren<CG> ch, int B, int l,
-            int K, int logN, const DevPrime *__restrict__ primes, const int *__restrict__ Imap, int nI,
-            const u64 *__restrict__ cji, const u64 *__restrict__ psipow, int gpad)
+            int K, int logN, const DevPrime *__restrict__ primes, const int *__restrict__ Imap, int nI, int nint,
+            const u64 *__restrict__ cji, const u64 *__restrict__ psipow, int wsplit)
 {
     const u64 N = 1ull << logN;
-    const int nbg = (B + BT - 1) / BT;
-    const int w = blockIdx.x;
-    const int g8 = w & 7, rest = w >> 3, bg = rest % nbg, G = (rest / nbg) * 8 + g8;
     const int X = (int)(N / 512);
-    if (G >= X * nI) return;
-    const int yi = G / X, xb = G % X;
+    const bool integer = (int)blockIdx.x < wsplit;
+    const int bt = integer ? BTI : BTF;
+    const int nbg = (B + bt - 1) / bt;
+    const int w = integer ? blockIdx.x : blockIdx.x - wsplit;
+    const int g8 = w & 7, rest = w >> 3, bg = rest % nbg, G = (rest / nbg) * 8 + g8;
+    if (G >= X * (integer ? nint : nI - nint)) return;
+    const int yi = G / X + (integer ? 0 : nint), xb = G % X;
     const int I = Imap[yi];
     const int kI = I == l ? K - 1 : I;
     const DevPrime pr = primes[kI];
     const u64 s0 = (u64)xb * 512 + 2 * threadIdx.x;
-    if (pr.fp)
-        hmacm_body<BT, CG, true>(X1, E, zl, ch, B, l, K, logN, pr, I, kI, s0, bg * BT, cji, psipow);
+    if (!integer)
+        hmacm_body<BTF, CG, true>(X1, E, zl, ch, B, l, K, logN, pr, I, kI, s0, bg * BTF, cji, psipow);
     else
-        hmacm_body<BT, CG, false>(X1, E, zl, ch, B, l, K, logN, pr, I, kI, s0, bg * BT, cji, psipow);
+        hmacm_body<BTI, CG, false>(X1, E, zl, ch, B, l, K, logN, pr, I, kI, s0, bg * BTI, cji, psipow);
 }
 
-template <int BT, int CG>
+template <int BTF, int BTI, int CG, int MINW = (BTF * CG <= 8 && BTI * CG <= 8) ? 3 : 2>
 static void launch_hmacm(Ctx &c, PolyArr X1, const u64 *E, const int *zl, const HChildSpec *kids, int nkids, int B,
                          int l)
 {
@@ -1012,19 +1030,22 @@ static void launch_hmacm(Ctx &c, PolyArr X1, const u64 *E, const int *zl, const 
     ch.n = nkids;
     for (int q = 0; q < nkids; ++q)
         ch.c[q] = HChild{kids[q].elt, kids[q].einv, kids[q].key, kids[q].W, kids[q].ACC, kids[q].KW};
-    const int nbg = (B + BT - 1) / BT, X = (int)(c.N / 512), gpad = (X * (l + 1) + 7) / 8 * 8;
-    k_hmacm<BT, CG><<<dim3((unsigned)(gpad * nbg)), 256, 0, c.stream>>>(X1, E, zl, ch, B, l, (int)c.K, c.logN,
-                                                                         c.primes, c.imap_at(l), l + 1, c.cji,
-                                                                         c.psipow, gpad);
+    const int nint = c.imap_nint[l], X = (int)(c.N / 512);
+    const int gI = (X * nint + 7) / 8 * 8, gF = (X * (l + 1 - nint) + 7) / 8 * 8;
+    const int wsplit = gI * ((B + BTI - 1) / BTI), total = wsplit + gF * ((B + BTF - 1) / BTF);
+    k_hmacm<BTF, BTI, CG, MINW><<<dim3((unsigned)total), 256, 0, c.stream>>>(X1, E, zl, ch, B, l, (int)c.K, c.logN,
+                                                                        c.primes, c.imap_at(l), l + 1, nint, c.cji,
+                                                                        c.psipow, wsplit);
     HEC_HIP(hipGetLastError());
 }
 
 int hoisted_group(const Ctx &c)
 {
     switch (c.hmac_cfg) {
-    case 1: return 4;
-    case 2: case 3: return 2;
-    case 4: return 3;
+    case 1: case 9: case 10: case 11: return 4;
+    case 12: return 6;
+    case 2: case 3: case 5: case 6: case 8: case 13: case 14: return 2;
+    case 4: case 7: return 3;
     default: return 1;
     }
 }
@@ -1034,10 +1055,20 @@ void hoisted_mac_multi(Ctx &c, PolyArr X1, const u64 *E, const int *zl, const HC
 {
     if (nkids < 1 || nkids > hoisted_group(c)) throw std::invalid_argument("hoisted_mac_multi: group size");
     switch (c.hmac_cfg) {
-    case 1: launch_hmacm<1, 4>(c, X1, E, zl, kids, nkids, B, l); break;
-    case 2: launch_hmacm<2, 2>(c, X1, E, zl, kids, nkids, B, l); break;
-    case 3: launch_hmacm<4, 2>(c, X1, E, zl, kids, nkids, B, l); break;
-    case 4: launch_hmacm<2, 3>(c, X1, E, zl, kids, nkids, B, l); break;
+    case 1: launch_hmacm<1, 1, 4>(c, X1, E, zl, kids, nkids, B, l); break;
+    case 2: launch_hmacm<2, 2, 2>(c, X1, E, zl, kids, nkids, B, l); break;
+    case 3: launch_hmacm<4, 2, 2>(c, X1, E, zl, kids, nkids, B, l); break;
+    case 4: launch_hmacm<2, 2, 3>(c, X1, E, zl, kids, nkids, B, l); break;
+    case 5: launch_hmacm<4, 4, 2>(c, X1, E, zl, kids, nkids, B, l); break;
+    case 6: launch_hmacm<4, 1, 2>(c, X1, E, zl, kids, nkids, B, l); break;
+    case 7: launch_hmacm<4, 2, 3>(c, X1, E, zl, kids, nkids, B, l); break;
+    case 8: launch_hmacm<8, 2, 2>(c, X1, E, zl, kids, nkids, B, l); break;
+    case 9: launch_hmacm<2, 1, 4>(c, X1, E, zl, kids, nkids, B, l); break;
+    case 10: launch_hmacm<2, 2, 4>(c, X1, E, zl, kids, nkids, B, l); break;
+    case 11: launch_hmacm<4, 1, 4>(c, X1, E, zl, kids, nkids, B, l); break;
+    case 12: launch_hmacm<2, 1, 6>(c, X1, E, zl, kids, nkids, B, l); break;
+    case 13: launch_hmacm<4, 2, 2, 2>(c, X1, E, zl, kids, nkids, B, l); break;
+    case 14: launch_hmacm<2, 2, 2, 4>(c, X1, E, zl, kids, nkids, B, l); break;
     default: hoisted_mac(c, X1, E, kids[0].W, zl, kids[0].key, kids[0].ACC, B, l, kids[0].elt); break;
     }
 }

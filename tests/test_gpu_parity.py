@@ -279,7 +279,11 @@ def test_cfg3_matvec_small_n_bitexact(env15):
                                  {"HEC_TENSOR_DEFER": "1"}, {"HEC_TENSOR_BUFS": "1"}, {"HEC_TENSOR_DEFER": "3"},
                                  {"HEC_FAN": "0"}, {"HEC_FAN": "1", "HEC_FUSE_GALOIS": "0"},
                                  {"HEC_HOIST": "0"}, {"HEC_HOIST_MIN": "1"}, {"HEC_HOIST_MIN": "1", "HEC_FAN": "0"},
-                                 {"HEC_HMAC": "0"}, {"HEC_HMAC": "1"}, {"HEC_HMAC": "2"}, {"HEC_HMAC": "4"}])
+                                 {"HEC_HMAC": "0"}, {"HEC_HMAC": "1"}, {"HEC_HMAC": "2"}, {"HEC_HMAC": "4"},
+                                 {"HEC_HMAC": "5"}, {"HEC_HMAC": "6"}, {"HEC_HMAC": "7"}, {"HEC_HMAC": "8"},
+                                 {"HEC_HMAC": "9"}, {"HEC_HMAC": "10"}, {"HEC_HMAC": "11"}, {"HEC_HMAC": "12"},
+                                 {"HEC_HMAC": "13"}, {"HEC_HMAC": "14"},
+                                 {"HEC_FANG": "5,2,3"}])
 def test_keyswitch_variants_bitexact(orc, hecdna, env):
     """The engine's alternative key-switch schedules (separate mod-up pass B + MAC kernels; the fused
     kernel's key-load placements) give the same bits as the oracle."""
