@@ -326,6 +326,26 @@ void moddown(Ctx &c, u64 *ACC, u64 *Z, PolyArr IN, int in_nk, PolyArr OUT, int B
                  OUT, B, 2, l, (int)c.K - 1, c.p_inv.data(), c.p_inv_q.data(), Z, elt, fan ? 2 : 3);
 }
 
+// The mod-downs of ng sibling rotations of one node at once: ACC[q] = ACC + q B 2 (l+1) N (contiguous), IN the
+// node's ciphertexts read through each child's permutation.  The P-limb INTT pass and the fan-out (small,
+// latency-bound launches) run over all ng B entries in one launch each; divide_round's pass B per child.
+void moddown_group(Ctx &c, u64 *ACC, u64 *Z, PolyArr IN, const PolyArr *OUT, const u32 *elts, int ng, int B, int l)
+{
+    const u64 N = c.N, sacc = (u64)B * 2 * (l + 1) * N, sz = (u64)B * 2 * l * N;
+    if (!c.fan_out || ng == 1) {
+        for (int q = 0; q < ng; ++q) moddown(c, ACC + q * sacc, Z, IN, 1, OUT[q], B, l, elts[q]);
+        return;
+    }
+    ProfScope ps(c, "ks_moddown");
+    const int pP[1] = {(int)c.K - 1};
+    ntt_strided(c, true, ACC + l * N, (l + 1) * N, ACC + l * N, (l + 1) * N, 1, pP, 2 * B * ng, 1, 1);
+    fan_divide_round(c, ACC + l * N, 2 * (l + 1) * N, (l + 1) * N, Z, B * ng, 2, l, (int)c.K - 1);
+    for (int q = 0; q < ng; ++q)
+        divide_round(c, ACC + q * sacc + l * N, 2 * (l + 1) * N, (l + 1) * N,
+                     PolyArr{ACC + q * sacc, 2 * (l + 1) * N, (l + 1) * N}, IN, 1, OUT[q], B, 2, l, (int)c.K - 1,
+                     c.p_inv.data(), c.p_inv_q.data(), Z + q * sz, elts[q], 2);
+}
+
 // T (the target polys) and IN (added to the output) are read through the Galois permutation of elt
 // (elt = 1: as they are).  OUT must not overlap T or IN when elt != 1 (the reads gather).
 void keyswitch(Ctx &c, Scratch &s, PolyArr T, const u64 *key, PolyArr IN, int in_nk, PolyArr OUT, int B, int l,
@@ -385,7 +405,8 @@ Hoist hoist_alloc(const Ctx &c, Scratch &s, int B, int l)
     h.D = s.take((u64)B * l * c.N);
     h.E = s.take((u64)B * (l + 1) * l * c.N);
     h.zl = reinterpret_cast<int *>(s.take(((1 + (u64)B * l * (HEC_ZCAP + 1)) * sizeof(int) + 7) / 8));
-    for (int q = 0; q < HOIST_GROUP; ++q) h.acc[q] = s.take((u64)B * 2 * (l + 1) * c.N);
+    h.acc[0] = s.take((u64)HOIST_GROUP * B * 2 * (l + 1) * c.N);  // contiguous: moddown_group
+    for (int q = 1; q < HOIST_GROUP; ++q) h.acc[q] = h.acc[q - 1] + (u64)B * 2 * (l + 1) * c.N;
     return h;
 }
 void hoist_node(Ctx &c, PolyArr X, int B, int l, const Hoist &h)
@@ -418,7 +439,7 @@ void hoisted_child(Ctx &c, Scratch &s, PolyArr X, const Hoist &h, const u64 *W, 
 }
 std::size_t hoisted_child_words(const Ctx &c, std::size_t B, std::size_t l)
 {
-    return c.N * B * (2 * (l + 1) + 2 * l) + 2 * 64;
+    return c.N * B * std::max(2 * (l + 1) + 2 * l, (std::size_t)HOIST_GROUP * 2 * l) + 2 * 64;
 }
 
 // the sign-mask NTTs of a Galois key (built on first use): W[I] = NTT_I(m), m[t] = 1 iff coefficient t of
@@ -623,17 +644,35 @@ void walk_trie_hoisted(Ctx &c, Scratch &s, const RotTrie &t, int node, PolyArr s
             ProfScope ps(c, "ks_hmac");
             hoisted_mac_multi(c, PolyArr{src.p + src.sk, src.sb, 0}, h.E, h.zl, kids, ng, B, l);
         }
-        for (int q = 0; q < ng; ++q) {
-            const int cn = ch[g0 + q];
-            const PolyArr dst{bufs.take(depth + 1), stride, (u64)l * N};
-            before_write(dst.p);
-            const std::size_t top = s.top;
-            u64 *Z = s.take((u64)B * 2 * l * N);
-            moddown(c, h.acc[q], Z, PolyArr{src.p, src.sb, src.sk}, 1, dst, B, l, kids[q].elt);
-            s.top = top;
-            walk_trie_hoisted(c, s, t, cn, dst, depth + 1, B, l, ctx, gk, bufs, hs, stride, min_children, visit,
-                              before_write);
+        if ((int)bufs.b[depth + 1].size() < ng) {  // too few rotation buffers to hold the group at once
+            for (int q = 0; q < ng; ++q) {
+                const PolyArr dst{bufs.take(depth + 1), stride, (u64)l * N};
+                before_write(dst.p);
+                const std::size_t top = s.top;
+                u64 *Z = s.take((u64)B * 2 * l * N);
+                moddown(c, h.acc[q], Z, PolyArr{src.p, src.sb, src.sk}, 1, dst, B, l, kids[q].elt);
+                s.top = top;
+                walk_trie_hoisted(c, s, t, ch[g0 + q], dst, depth + 1, B, l, ctx, gk, bufs, hs, stride,
+                                  min_children, visit, before_write);
+            }
+            continue;
         }
+        PolyArr dst[HOIST_GROUP];
+        u32 elts[HOIST_GROUP];
+        for (int q = 0; q < ng; ++q) {
+            dst[q] = PolyArr{bufs.take(depth + 1), stride, (u64)l * N};
+            before_write(dst[q].p);
+            elts[q] = kids[q].elt;
+        }
+        {
+            const std::size_t top = s.top;
+            u64 *Z = s.take((u64)ng * B * 2 * l * N);
+            moddown_group(c, h.acc[0], Z, PolyArr{src.p, src.sb, src.sk}, dst, elts, ng, B, l);
+            s.top = top;
+        }
+        for (int q = 0; q < ng; ++q)
+            walk_trie_hoisted(c, s, t, ch[g0 + q], dst[q], depth + 1, B, l, ctx, gk, bufs, hs, stride, min_children,
+                              visit, before_write);
     }
 }
 
