@@ -17,5 +17,5 @@ timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "k_hmacm|k_b
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "k_hmacm|k_bmac" --output-format csv -d $OUT/pmc_write -o run -- python3 $GRAFT_REPO_ROOT/bench.py $PMCARGS > $OUT/pmc_write.log 2>&1 || { tail $OUT/pmc_write.log; exit 1; }
 cd $GRAFT_REPO_ROOT
 for k in k_hmacm k_bmac; do
-  python tools/pmc_summary.py $OUT/pmc_fetch/run_counter_collection.csv $OUT/pmc_write/run_counter_collection.csv $k 32 15 10 4096 $OUT/pmc_${k}_B32.json "rocprofv3 --pmc FETCH_SIZE (then WRITE_SIZE, separate pass) --kernel-include-regex 'k_hmacm|k_bmac' -- python3 bench.py $PMCARGS" || exit 1
+  python tools/pmc_summary.py $OUT/pmc_fetch/run_counter_collection.csv $OUT/pmc_write/run_counter_collection.csv $k 64 15 10 4096 $OUT/pmc_${k}_B64.json "rocprofv3 --pmc FETCH_SIZE (then WRITE_SIZE, separate pass) --kernel-include-regex 'k_hmacm|k_bmac' -- python3 bench.py $PMCARGS" || exit 1
 done
