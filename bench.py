@@ -154,7 +154,10 @@ def main():
     if ctpt and sharded:
         raise SystemExit("--variant ctpt runs in throughput mode")
     if ctpt:
-        diags = [hec.Plaintext(ctx, None, scale).fill_uniform(L, scale, 10_000 + j) for j in range(args.n)]
+        # plaintext diagonals: synthetic U[-1,1] slot values encoded on the GPU (hec_encode), untimed setup
+        vals = np.random.default_rng(10_000).uniform(-1, 1, (args.n, N // 2))
+        diags = ctx.encode(vals, scale, L)
+        del vals
     else:
         diags = [ctx.ciphertext().fill_uniform(2, L, scale, 10_000 + j) if j in held else None
                  for j in range(args.n)]

@@ -94,6 +94,10 @@ def lib():
             "hec_matmul_diag_col": [vp, vp, C.c_uint64, vp, C.c_uint64, vp, vp, vp],
             "hec_matmul_diagpt_col": [vp, vp, C.c_uint64, vp, C.c_uint64, vp, vp],
             "hec_plaintext_fill_uniform": [vp, C.c_uint64, C.c_double, C.c_uint64],
+            "hec_plaintext_download": [vp, u64p],
+            "hec_plaintext_info": [vp, u64p, C.POINTER(C.c_double)],
+            "hec_encode": [vp, C.POINTER(C.c_double), C.POINTER(C.c_double), C.c_uint64, C.c_uint64, C.c_double,
+                           C.c_uint64, vp],
             "hec_matmul_diag_col_partial": [vp, vp, C.c_uint64, C.c_uint64, C.c_uint64, vp, C.c_uint64, vp, vp],
             "hec_matmul_diag_col_partial_set": [vp, vp, C.c_uint64, vp, C.c_uint64, vp, C.c_uint64, vp, vp],
             "hec_matmul_finish": [vp, vp, C.c_uint64, vp, vp],
@@ -206,6 +210,23 @@ class Context:
 
     def plaintext(self, data, scale):
         return Plaintext(self, data, scale)
+
+    def encode(self, values, scale, level=None):
+        """seal::CKKSEncoder::encode on the GPU (hec_encode): `values` is one slot vector or a 2-D array of
+        `count` vectors (real or complex, at most N/2 slots each) -> list of NTT-form Plaintexts (a single
+        Plaintext for a 1-D input)."""
+        v = np.asarray(values)
+        single = v.ndim == 1
+        v = v.reshape(1, -1) if single else v
+        level = level or (self.K - 1)
+        re = np.ascontiguousarray(v.real, dtype=np.float64)
+        im = np.ascontiguousarray(v.imag, dtype=np.float64) if np.iscomplexobj(v) else None
+        pts = [Plaintext(self, None, scale) for _ in range(v.shape[0])]
+        arr = (C.c_void_p * len(pts))(*[p.h.value for p in pts])
+        dp = C.POINTER(C.c_double)
+        _check(lib().hec_encode(self.h, re.ctypes.data_as(dp), im.ctypes.data_as(dp) if im is not None else None,
+                                v.shape[1], v.shape[0], float(scale), level, arr))
+        return pts[0] if single else pts
 
     def relin_key(self, data=None, seed=None):
         return KSwitchKey(self, data, seed)
@@ -427,6 +448,17 @@ class Plaintext:
     def fill_uniform(self, level, scale, seed):
         _check(lib().hec_plaintext_fill_uniform(self.h, level, float(scale), seed))
         return self
+
+    def info(self):
+        lv, sc = C.c_uint64(), C.c_double()
+        _check(lib().hec_plaintext_info(self.h, C.byref(lv), C.byref(sc)))
+        return lv.value, sc.value
+
+    def download(self):
+        lv, _ = self.info()
+        out = np.empty((lv, self.ctx.N), dtype=np.uint64)
+        _check(lib().hec_plaintext_download(self.h, _p(out)))
+        return out
 
     def __del__(self):
         try:

@@ -15,6 +15,7 @@
 //   (5) OUT[b][k][i] = IN[b][k][i] + (ACC[b][k][i] - NTT_i(round(y))) * P^-1     divide_round
 #include <algorithm>
 #include <cmath>
+#include <complex>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -1042,6 +1043,8 @@ int hec_context_destroy(hec_context *ctx)
         (void)hipFree(c.twb);
         (void)hipFree(c.itwb);
         for (double *p : {c.twf, c.itwf, c.twbf, c.itwbf}) (void)hipFree(p);
+        (void)hipFree(c.enc_map);
+        for (double *p : {c.enc_tw, c.enc_twist}) (void)hipFree(p);
         if (c.own_stream) (void)hipStreamDestroy(c.stream);
         (void)hipStreamDestroy(c.side);
         (void)hipEventDestroy(c.ev_fork);
@@ -1262,6 +1265,134 @@ int hec_plaintext_upload(hec_plaintext *pt, const uint64_t *host, uint64_t level
         HEC_HIP(hipMemcpyAsync(pt->d, host, w * sizeof(u64), hipMemcpyHostToDevice, c.stream));
         HEC_HIP(hipStreamSynchronize(c.stream));
         pt->level = level; pt->scale = scale;
+    });
+}
+
+int hec_plaintext_download(const hec_plaintext *pt, uint64_t *host)
+{
+    return guard([&] {
+        need(pt && host, "null argument");
+        need(pt->d != nullptr, "plain is not valid for encryption parameters");
+        Ctx &c = pt->ctx->c;
+        set_device(pt->ctx);
+        HEC_HIP(hipMemcpyAsync(host, pt->d, pt->level * c.N * sizeof(u64), hipMemcpyDeviceToHost, c.stream));
+        HEC_HIP(hipStreamSynchronize(c.stream));
+    });
+}
+
+int hec_plaintext_info(const hec_plaintext *pt, uint64_t *level, double *scale)
+{
+    return guard([&] {
+        need(pt != nullptr, "null argument");
+        if (level) *level = pt->level;
+        if (scale) *scale = pt->scale;
+    });
+}
+
+// ------------------------------------------------------------------ CKKS encoder ----------
+namespace {
+// host tables of the GPU encoder (hec_encode.hip), built once per context: the slot map of SEAL's
+// matrix_reps_index_map_ (generator 3) with the FFT's bit reversal folded in, the FFT stage twiddles
+// polar(1, (-2 pi / len) j) and the twist polar(1, -pi k / N), as std::polar over glibc cos/sin
+void encoder_tables(Ctx &c)
+{
+    if (c.enc_map) return;
+    constexpr double kPi = 3.14159265358979323846;
+    const u64 N = c.N, slots = N / 2, m = 2 * N;
+    std::vector<u32> map(N);
+    u64 pos = 1;
+    for (u64 i = 0; i < slots; ++i) {
+        map[i] = brev((u32)((pos - 1) >> 1), c.logN);
+        map[slots + i] = brev((u32)((m - pos - 1) >> 1), c.logN);
+        pos = (pos * 3) & (m - 1);
+    }
+    std::vector<double> tw(2 * (N - 1)), twist(2 * N);
+    const int sign = -1;
+    for (u64 len = 2; len <= N; len <<= 1) {
+        const double ang = sign * 2 * kPi / (double)len;
+        for (u64 j = 0; j < len / 2; ++j) {
+            const std::complex<double> w = std::polar(1.0, ang * (double)j);
+            tw[2 * (len / 2 - 1 + j)] = w.real();
+            tw[2 * (len / 2 - 1 + j) + 1] = w.imag();
+        }
+    }
+    for (u64 k = 0; k < N; ++k) {
+        const std::complex<double> z = std::polar(1.0, -kPi * (double)k / (double)N);
+        twist[2 * k] = z.real();
+        twist[2 * k + 1] = z.imag();
+    }
+    u32 *dm = nullptr;
+    double *dt = nullptr, *dz = nullptr;
+    HEC_HIP(hipMalloc(&dm, N * sizeof(u32)));
+    HEC_HIP(hipMalloc(&dt, tw.size() * sizeof(double)));
+    HEC_HIP(hipMalloc(&dz, twist.size() * sizeof(double)));
+    HEC_HIP(hipMemcpyAsync(dm, map.data(), N * sizeof(u32), hipMemcpyHostToDevice, c.stream));
+    HEC_HIP(hipMemcpyAsync(dt, tw.data(), tw.size() * sizeof(double), hipMemcpyHostToDevice, c.stream));
+    HEC_HIP(hipMemcpyAsync(dz, twist.data(), twist.size() * sizeof(double), hipMemcpyHostToDevice, c.stream));
+    HEC_HIP(hipStreamSynchronize(c.stream));  // the host tables go out of scope
+    c.enc_map = dm;
+    c.enc_tw = dt;
+    c.enc_twist = dz;
+}
+}  // namespace
+
+int hec_encode(hec_context *ctx, const double *re, const double *im, uint64_t n_values, uint64_t count, double scale,
+               uint64_t level, hec_plaintext *const *out)
+{
+    return guard([&] {
+        need(ctx && out && (re || n_values == 0), "null argument");
+        Ctx &c = ctx->c;
+        set_device(ctx);
+        // argument checks in SEAL CKKSEncoder::encode_internal's order
+        if (n_values > c.N / 2) throw std::invalid_argument("values has invalid size");
+        if (level < 1 || level > c.L) throw std::invalid_argument("parms_id is not valid for encryption parameters");
+        if (scale <= 0 || (int)std::log2(scale) >= c.total_bits(level)) throw std::invalid_argument("scale out of bounds");
+        for (u64 v = 0; v < count; ++v) need(out[v] && out[v]->ctx == ctx, "plain is not valid for encryption parameters");
+        if (count == 0) return;
+        encoder_tables(c);
+        const u64 N = c.N, nv = n_values;
+        // chunks of vectors: the work area (2N doubles + level N residues per vector) stays under ~2 GiB
+        const u64 per = 2 * N + level * N + 2 * nv + 1;
+        const u64 chunk = std::max<u64>(1, std::min<u64>(count, (u64(1) << 28) / per));
+        std::vector<u64> mx(chunk);
+        for (u64 v0 = 0; v0 < count; v0 += chunk) {
+            const u64 cnt = std::min(chunk, count - v0);
+            Scratch s(c, cnt * per + 5 * 64);
+            double *dre = reinterpret_cast<double *>(s.take(std::max<u64>(cnt * nv, 1)));
+            double *dim = im ? reinterpret_cast<double *>(s.take(std::max<u64>(cnt * nv, 1))) : nullptr;
+            double *work = reinterpret_cast<double *>(s.take(cnt * 2 * N));
+            u64 *res = s.take(cnt * level * N), *dmx = s.take(cnt);
+            if (nv) {
+                HEC_HIP(hipMemcpyAsync(dre, re + v0 * nv, cnt * nv * sizeof(double), hipMemcpyHostToDevice, c.stream));
+                if (im)
+                    HEC_HIP(hipMemcpyAsync(dim, im + v0 * nv, cnt * nv * sizeof(double), hipMemcpyHostToDevice,
+                                           c.stream));
+            }
+            encode_batch(c, dre, dim, nv, (int)cnt, scale, (int)level, work, res, dmx);
+            HEC_HIP(hipMemcpyAsync(mx.data(), dmx, cnt * sizeof(u64), hipMemcpyDeviceToHost, c.stream));
+            HEC_HIP(hipStreamSynchronize(c.stream));
+            for (u64 v = 0; v < cnt; ++v) {
+                double maxabs;
+                std::memcpy(&maxabs, &mx[v], sizeof(double));
+                // ceil(log2(max(max |coeff|, 1))) + 1 >= total coeff-modulus bits -> throw (SEAL encode_internal)
+                const int max_bits = (int)std::ceil(std::log2(std::max(maxabs, 1.0))) + 1;
+                if (max_bits >= c.total_bits(level) || maxabs >= 0x1.0p62)
+                    throw std::invalid_argument("encoded values are too large");
+            }
+            for (u64 v = 0; v < cnt; ++v) {
+                hec_plaintext *pt = out[v0 + v];
+                const std::size_t w = level * N;
+                if (pt->cap < w) {
+                    if (pt->d) HEC_HIP(hipFree(pt->d));
+                    pt->d = dalloc(w);
+                    pt->cap = w;
+                }
+                d2d(c, pt->d, res + v * w, w);
+                pt->level = level;
+                pt->scale = scale;
+            }
+            HEC_HIP(hipStreamSynchronize(c.stream));  // the next chunk reuses the workspace
+        }
     });
 }
 

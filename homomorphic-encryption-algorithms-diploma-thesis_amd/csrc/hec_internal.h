@@ -67,6 +67,10 @@ struct Ctx {
     u64 *cji = nullptr;
     int *zflag = nullptr;
     int logR = 0;                   // pass split N = R x C, R = 2^ceil(logN/2)
+    // CKKS encoder tables (hec_encode.hip), built on first encode: slot -> bit-reversed FFT position
+    // (u32[N]), FFT stage twiddles (complex[N - 1], stage len at len/2 - 1) and the twist polar(1, -pi k/N)
+    u32 *enc_map = nullptr;
+    double *enc_tw = nullptr, *enc_twist = nullptr;
     Workspace ws;
     // host-side constants
     std::vector<u64> p_inv, p_inv_q, p_half_mod;            // key switch mod-down (per data prime)
@@ -169,5 +173,10 @@ void ew_dyadic(Ctx &c, const u64 *a, const u64 *b, u64 *out, int limb0, int nl, 
 void ct_multiply(Ctx &c, const u64 *a, int sa, const u64 *b, int sb, u64 *out, int nl);
 void ew_reduce(Ctx &c, u64 *p, int npoly, int nl);
 void fill_uniform(Ctx &c, u64 *p, int npoly, int nl, int limb_prime0, int special_last, u64 seed);
+// CKKS encode of `count` slot vectors (hec_encode.hip): re/im device [count][nv] (im may be null), work
+// device doubles [count][2N], out [count][level][N] NTT form, maxabs[count] = max |coefficient| (bits
+// of a double)
+void encode_batch(Ctx &c, const double *re, const double *im, u64 nv, int count, double scale, int level, double *work,
+                  u64 *out, u64 *maxabs);
 
 }  // namespace hec

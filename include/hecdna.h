@@ -86,6 +86,17 @@ int hec_plaintext_destroy(hec_plaintext *pt);
 int hec_plaintext_upload(hec_plaintext *pt, const uint64_t *host, uint64_t level, double scale);
 /* synthetic NTT-form plaintext: uniform residues mod q_i from a seeded device generator (benchmarks) */
 int hec_plaintext_fill_uniform(hec_plaintext *pt, uint64_t level, double scale, uint64_t seed);
+int hec_plaintext_download(const hec_plaintext *pt, uint64_t *host); /* u64[level][N], synchronises */
+int hec_plaintext_info(const hec_plaintext *pt, uint64_t *level, double *scale);
+/* seal::CKKSEncoder::encode(values, [parms_id,] scale, destination) on the GPU, for `count` slot vectors at
+ * once — the reference encodes every matrix column / diagonal this way before encryption
+ * (src/demos/matrix_operations.cpp:1106-1108, client.cpp:228-230, he_math.cpp:32-53 through
+ * he_util.h:33-36).  re / im: host doubles, count rows of n_values (n_values <= N/2; missing slots are
+ * zero); im = NULL encodes real values (SEAL's vector<double> overload).  out[v] receives an NTT-form
+ * plaintext at `level` with `scale`.  Errors as SEAL: "values has invalid size", "scale out of bounds",
+ * "encoded values are too large". */
+int hec_encode(hec_context *ctx, const double *re, const double *im, uint64_t n_values, uint64_t count, double scale,
+               uint64_t level, hec_plaintext *const *out);
 
 /* ---------------------------------------------------------------- keys -------------------- */
 /* RelinKeys (KeyGenerator::create_relin_keys, matrix_operations.cpp:1061-1062): data u64[L][2][K][N] */

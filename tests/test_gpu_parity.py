@@ -273,6 +273,28 @@ def test_cfg3_matvec_small_n_bitexact(env15):
         e.same(g, c)
 
 
+def test_cfg5_params_matvec_bitexact(orc, hecdna):
+    """BASELINE cfg5 parameters, N = 2^16 with the 17-prime chain {60, 40 x 15, 60} (l = 16, K = 17;
+    SURVEY §8 table): rotations and a small diag x col matvec (hoisted root, NAF rotations, lazy
+    relinearize + rescale) bit-exact against the oracle.  Keys only for steps +-1, 2, 4 (a full default
+    key set is 8.8 GB on the host)."""
+    N = 1 << 16
+    bits = [60] + [40] * 15 + [60]
+    o = orc.Oracle(N, orc.Oracle.create_coeff_modulus(N, bits))
+    elts = [o.elt_from_step(s) for s in (1, -1, 2, 4)]
+    e = Env(orc, hecdna, N, bits, seed=161, elts=elts)
+    assert len(e.m) == 17
+    a = e.enc(seed=1)
+    for steps in (1, 3, 5):
+        e.same(e.ctx.rotate_vector(e.up(a), steps, e.gk), e.o.rotate(a, steps, e.gk_h))
+    A = [e.enc(seed=170 + j) for j in range(5)]
+    X = [e.enc(seed=180 + i) for i in range(2)]
+    exp = e.o.matmul_diag_col(A, X, e.rk_h, e.gk_h, nthreads=8)
+    got = e.ctx.matmul_diag_col([e.up(x) for x in A], [e.up(x) for x in X], e.rk, e.gk)
+    for g, c in zip(got, exp):
+        e.same(g, c)
+
+
 @pytest.mark.parametrize("env", [{"HEC_FUSED_MODUP_MAC": "0"}, {"HEC_BMAC_KEYS": "0"}, {"HEC_BMAC_KEYS": "2"},
                                  {"HEC_FUSE_GALOIS": "0"}, {"HEC_FUSE_GALOIS": "0", "HEC_FUSED_MODUP_MAC": "0"},
                                  {"HEC_SPLIT_CLASSES": "1"}, {"HEC_SPLIT_CLASSES": "2"},
