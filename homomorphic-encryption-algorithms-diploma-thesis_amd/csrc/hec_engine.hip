@@ -389,7 +389,7 @@ void keyswitch(Ctx &c, Scratch &s, PolyArr T, const u64 *key, PolyArr IN, int in
 
 // hoisted mod-up data of one trie node (B targets at level l): D = INTT(c1) (canonical coefficient form),
 // E[b][I][J] = NTT_I(D_J mod q_I) (canonical NTT form, J != I), zero lists of D (see hec_kernels.hip)
-constexpr int HOIST_GROUP = 6;  // sibling rotations per fused hoisted MAC launch
+constexpr int HOIST_GROUP = 6;  // sibling rotations per accumulator set / grouped mod-down
 struct Hoist {
     u64 *D = nullptr, *E = nullptr;
     int *zl = nullptr;
@@ -632,9 +632,11 @@ void walk_trie_hoisted(Ctx &c, Scratch &s, const RotTrie &t, int node, PolyArr s
     const Hoist &h = hs[depth];
     hoist_node(c, src, B, l, h);
     const u64 N = c.N;
-    const std::size_t grp = (std::size_t)hoisted_group(c);
-    for (std::size_t g0 = 0; g0 < ch.size(); g0 += grp) {
-        const int ng = (int)std::min<std::size_t>(grp, ch.size() - g0);
+    // children in groups of up to HOIST_GROUP: one sibling-fused MAC launch per hoisted_group() of them
+    // (accumulators h.acc[q], contiguous), then the group's mod-downs share their small launches
+    const std::size_t grp = (std::size_t)hoisted_group(c), sup = std::max<std::size_t>(grp, HOIST_GROUP / grp * grp);
+    for (std::size_t g0 = 0; g0 < ch.size(); g0 += sup) {
+        const int ng = (int)std::min<std::size_t>(sup, ch.size() - g0);
         HChildSpec kids[HOIST_GROUP];
         for (int q = 0; q < ng; ++q) {
             const u32 e = t.nodes[ch[g0 + q]].elt;
@@ -643,7 +645,9 @@ void walk_trie_hoisted(Ctx &c, Scratch &s, const RotTrie &t, int node, PolyArr s
         }
         {
             ProfScope ps(c, "ks_hmac");
-            hoisted_mac_multi(c, PolyArr{src.p + src.sk, src.sb, 0}, h.E, h.zl, kids, ng, B, l);
+            for (int q0 = 0; q0 < ng; q0 += (int)grp)
+                hoisted_mac_multi(c, PolyArr{src.p + src.sk, src.sb, 0}, h.E, h.zl, kids + q0,
+                                  std::min((int)grp, ng - q0), B, l);
         }
         if ((int)bufs.b[depth + 1].size() < ng) {  // too few rotation buffers to hold the group at once
             for (int q = 0; q < ng; ++q) {
