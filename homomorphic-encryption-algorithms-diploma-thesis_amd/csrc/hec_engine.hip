@@ -643,11 +643,10 @@ void walk_trie_hoisted(Ctx &c, Scratch &s, const RotTrie &t, int node, PolyArr s
             kids[q] = HChildSpec{e, (u32)invm(e, 2 * N), gk.keys.at(e), galois_negw(ctx, gk, e), h.acc[q],
                                  galois_kw(ctx, gk, e, l)};
         }
-        {
+        for (int q0 = 0; q0 < ng; q0 += (int)grp) {  // one profile scope per launch (bench.py's roofline)
             ProfScope ps(c, "ks_hmac");
-            for (int q0 = 0; q0 < ng; q0 += (int)grp)
-                hoisted_mac_multi(c, PolyArr{src.p + src.sk, src.sb, 0}, h.E, h.zl, kids + q0,
-                                  std::min((int)grp, ng - q0), B, l);
+            hoisted_mac_multi(c, PolyArr{src.p + src.sk, src.sb, 0}, h.E, h.zl, kids + q0,
+                              std::min((int)grp, ng - q0), B, l);
         }
         if ((int)bufs.b[depth + 1].size() < ng) {  // too few rotation buffers to hold the group at once
             for (int q = 0; q < ng; ++q) {
