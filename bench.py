@@ -105,7 +105,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--batch", type=int, default=64, help="input vectors per GPU per step (p)")
+    ap.add_argument("--batch", type=int, default=96,
+                    help="input vectors per GPU per step (p); the engine runs them as 3 concurrent lanes of 32")
     ap.add_argument("--n", type=int, default=4096, help="matrix dimension (diagonals)")
     ap.add_argument("--logn", type=int, default=15)
     ap.add_argument("--no-cpu-baseline", action="store_true")

@@ -19,7 +19,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <exception>
 #include <limits>
+#include <thread>
 
 #include "hec_internal.h"
 #include "hecdna.h"
@@ -30,6 +32,9 @@ using u128 = unsigned __int128;
 // =============================================================================== objects ===
 struct hec_context {
     Ctx c;
+    // batch lanes (matvec_lanes): contexts sharing this one's device tables, each with its own HIP
+    // stream, workspace and zero flag, built on first use
+    std::vector<hec_context *> lanes;
 };
 struct hec_ciphertext {
     hec_context *ctx = nullptr;
@@ -689,9 +694,10 @@ void walk_trie_hoisted(Ctx &c, Scratch &s, const RotTrie &t, int node, PolyArr s
 // no relinearization) — exactly one is non-null.
 void matvec_core(hec_context *ctx, const hec_ciphertext *const *diags, const hec_plaintext *const *pdiags,
                  std::size_t n, const std::vector<std::size_t> &js, const hec_ciphertext *const *cols, std::size_t p,
-                 const hec_kswitch_key *rk, const hec_galois_keys *gk, bool finish, hec_ciphertext *const *out)
+                 const hec_kswitch_key *rk, const hec_galois_keys *gk, bool finish, hec_ciphertext *const *out,
+                 Ctx *exec = nullptr)  // exec: the lane context that runs it (objects still belong to ctx)
 {
-    Ctx &c = ctx->c;
+    Ctx &c = exec ? *exec : ctx->c;
     const bool pt = pdiags != nullptr;
     need(n >= 1 && p >= 1 && !js.empty(), "empty matrix operand");
     for (std::size_t j : js) need(j < n, "diagonal index out of range");
@@ -788,7 +794,7 @@ void matvec_core(hec_context *ctx, const hec_ciphertext *const *diags, const hec
         if (zf) {
             c.hoist = false;
             try {
-                matvec_core(ctx, diags, pdiags, n, js, cols, p, rk, gk, finish, out);
+                matvec_core(ctx, diags, pdiags, n, js, cols, p, rk, gk, finish, out, exec);
             } catch (...) {
                 c.hoist = true;
                 throw;
@@ -821,6 +827,98 @@ void matvec_core(hec_context *ctx, const hec_ciphertext *const *diags, const hec
     }
 }
 
+
+// ---------------------------------------------------------------- batch lanes
+// The engine's kernels leave issue slots and bandwidth idle (they wait on memory for most of their
+// cycles), so the batch of a matvec is split into up to c.lanes sub-batches of at least
+// c.lane_min_batch vectors that run the same trie walk concurrently, each from its own host thread on its
+// own HIP stream and workspace.  Outputs are independent per input vector, so the bits are unchanged.
+hec_context *make_lane(hec_context *parent)
+{
+    auto *l = new hec_context();
+    Ctx &c = l->c;
+    c = parent->c;  // shared device tables (twiddles, primes, maps), host constants and knobs
+    c.ws = Workspace{};
+    c.prof_mode = 0;
+    c.prof_tab.clear();
+    c.prof_pend.clear();
+    c.ev_pool.clear();
+    c.ev_used = 0;
+    c.stream = c.side = nullptr;
+    c.ev_fork = c.ev_join = nullptr;
+    c.zflag = nullptr;
+    HEC_HIP(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
+    c.own_stream = true;
+    HEC_HIP(hipStreamCreateWithFlags(&c.side, hipStreamNonBlocking));
+    HEC_HIP(hipEventCreateWithFlags(&c.ev_fork, hipEventDisableTiming));
+    HEC_HIP(hipEventCreateWithFlags(&c.ev_join, hipEventDisableTiming));
+    HEC_HIP(hipMalloc(&c.zflag, sizeof(int)));
+    return l;
+}
+void free_lane(hec_context *l)
+{
+    Ctx &c = l->c;
+    (void)hipStreamSynchronize(c.stream);
+    c.ws.release();
+    (void)hipFree(c.zflag);
+    (void)hipStreamDestroy(c.stream);
+    (void)hipStreamDestroy(c.side);
+    (void)hipEventDestroy(c.ev_fork);
+    (void)hipEventDestroy(c.ev_join);
+    delete l;
+}
+
+void matvec_lanes(hec_context *ctx, const hec_ciphertext *const *diags, const hec_plaintext *const *pdiags,
+                  std::size_t n, const std::vector<std::size_t> &js, const hec_ciphertext *const *cols, std::size_t p,
+                  const hec_kswitch_key *rk, const hec_galois_keys *gk, bool finish, hec_ciphertext *const *out)
+{
+    Ctx &c = ctx->c;
+    const int nl = (int)std::min<std::size_t>((std::size_t)std::max(1, c.lanes), p / std::max(1, c.lane_min_batch));
+    if (nl <= 1 || c.prof_mode != 0) {  // profiling: the single-stream schedule, one phase at a time
+        matvec_core(ctx, diags, pdiags, n, js, cols, p, rk, gk, finish, out);
+        return;
+    }
+    need(gk && gk->ctx == ctx, "galois_keys is not valid for encryption parameters");
+    check_ct(ctx, cols[0]);
+    if (c.hoist) {  // the lazily built per-key tables, before the lanes only read them
+        auto &gkm = const_cast<hec_galois_keys &>(*gk);
+        for (auto &kv : gkm.keys) {
+            galois_negw(ctx, gkm, kv.first);
+            galois_kw(ctx, gkm, kv.first, (int)cols[0]->level);
+        }
+    }
+    while ((int)ctx->lanes.size() < nl) ctx->lanes.push_back(make_lane(ctx));
+    hipEvent_t start;
+    HEC_HIP(hipEventCreateWithFlags(&start, hipEventDisableTiming));
+    HEC_HIP(hipEventRecord(start, c.stream));  // the inputs were produced on the context's stream
+    std::vector<hipEvent_t> done(nl, nullptr);
+    std::vector<std::exception_ptr> err(nl);
+    std::vector<std::thread> th;
+    for (int i = 0; i < nl; ++i) {
+        const std::size_t b0 = p * i / nl, b1 = p * (i + 1) / nl;
+        th.emplace_back([&, i, b0, b1] {
+            try {
+                Ctx &lc = ctx->lanes[i]->c;
+                HEC_HIP(hipSetDevice(lc.device));
+                HEC_HIP(hipEventCreateWithFlags(&done[i], hipEventDisableTiming));
+                HEC_HIP(hipStreamWaitEvent(lc.stream, start, 0));
+                matvec_core(ctx, diags, pdiags, n, js, cols + b0, b1 - b0, rk, gk, finish, out + b0, &lc);
+                HEC_HIP(hipEventRecord(done[i], lc.stream));
+            } catch (...) {
+                err[i] = std::current_exception();
+            }
+        });
+    }
+    for (auto &t : th) t.join();
+    for (int i = 0; i < nl; ++i)
+        if (done[i]) {
+            HEC_HIP(hipStreamWaitEvent(c.stream, done[i], 0));  // later work on the context sees the outputs
+            (void)hipEventDestroy(done[i]);
+        }
+    (void)hipEventDestroy(start);
+    for (auto &e : err)
+        if (e) std::rethrow_exception(e);
+}
 }  // namespace
 
 // =============================================================================== workspace ==
@@ -892,6 +990,7 @@ int hec_context_create(uint64_t N, const uint64_t *mod, uint64_t K, int device, 
         if (const char *f = std::getenv("HEC_BMAC_KEYS")) c.bmac_keys = f[0] - '0';
         if (const char *f = std::getenv("HEC_FUSE_GALOIS")) c.fuse_galois = f[0] != '0';
         if (const char *f = std::getenv("HEC_FAN")) c.fan_out = f[0] != '0';
+        if (const char *f = std::getenv("HEC_LANES")) c.lanes = std::max(1, std::atoi(f));
         if (const char *f = std::getenv("HEC_NTT1")) c.ntt1 = std::atoi(f);
         if (const char *f = std::getenv("HEC_FANG"))
             std::sscanf(f, "%d,%d,%d", &c.fan_groups_moddown, &c.fan_groups_modup, &c.fan_groups_hoist);
@@ -1035,6 +1134,7 @@ int hec_context_destroy(hec_context *ctx)
         if (!ctx) return;
         Ctx &c = ctx->c;
         (void)hipSetDevice(c.device);
+        for (hec_context *l : ctx->lanes) free_lane(l);
         (void)hipStreamSynchronize(c.stream);
         c.ws.release();
         (void)hipFree(c.primes);
@@ -1704,7 +1804,7 @@ int hec_matmul_diag_col(hec_context *ctx, const hec_ciphertext *const *diags, ui
         need(diags && cols && out, "null argument");
         std::vector<std::size_t> js(n);
         for (std::size_t j = 0; j < n; ++j) js[j] = j;
-        matvec_core(ctx, diags, nullptr, n, js, cols, p, rk, gk, true, out);
+        matvec_lanes(ctx, diags, nullptr, n, js, cols, p, rk, gk, true, out);
     });
 }
 
@@ -1718,7 +1818,7 @@ int hec_matmul_diag_col_partial(hec_context *ctx, const hec_ciphertext *const *d
         need(j_begin < j_end && j_end <= n, "empty matrix operand");
         std::vector<std::size_t> js;
         for (uint64_t j = j_begin; j < j_end; ++j) js.push_back(j);
-        matvec_core(ctx, diags, nullptr, n, js, cols, p, nullptr, gk, false, acc_out);
+        matvec_lanes(ctx, diags, nullptr, n, js, cols, p, nullptr, gk, false, acc_out);
     });
 }
 
@@ -1732,7 +1832,7 @@ int hec_matmul_diag_col_partial_set(hec_context *ctx, const hec_ciphertext *cons
         std::vector<std::size_t> js(j_idx, j_idx + nj);
         std::sort(js.begin(), js.end());
         need(std::adjacent_find(js.begin(), js.end()) == js.end(), "duplicate diagonal index");
-        matvec_core(ctx, diags, nullptr, n, js, cols, p, nullptr, gk, false, acc_out);
+        matvec_lanes(ctx, diags, nullptr, n, js, cols, p, nullptr, gk, false, acc_out);
     });
 }
 
@@ -1745,7 +1845,7 @@ int hec_matmul_diagpt_col(hec_context *ctx, const hec_plaintext *const *diags, u
         need(diags && cols && out, "null argument");
         std::vector<std::size_t> js(n);
         for (std::size_t j = 0; j < n; ++j) js[j] = j;
-        matvec_core(ctx, nullptr, diags, n, js, cols, p, nullptr, gk, true, out);
+        matvec_lanes(ctx, nullptr, diags, n, js, cols, p, nullptr, gk, true, out);
     });
 }
 

@@ -89,6 +89,8 @@ struct Ctx {
     int fan_groups_hoist = 1;
     bool fan_out = true;           // HEC_FAN=0: separate INTT pass A (fan-out fuses it into the forward passes A)
     int ntt1 = 0;                  // HEC_NTT1: single-pass (one workgroup per limb) N = 2^15 NTT kernels
+    int lanes = 3;                 // HEC_LANES: concurrent batch lanes of a matvec (hec_engine.hip matvec_lanes)
+    int lane_min_batch = 16;       // input vectors per lane at least
     bool fuse_galois = true;       // HEC_FUSE_GALOIS=0: materialise apply_galois before the key switch
     bool fused_modup_mac = true;  // HEC_FUSED_MODUP_MAC=0: separate mod-up pass B and key MAC kernels
     // profiling (ProfScope in hec_engine.hip)

@@ -214,6 +214,23 @@ def test_matvec_batched_equals_single_and_oracle(env11):
     e.same(one, exp[1])
 
 
+def test_matvec_batch_lanes_bitexact(env11):
+    """A batch of >= 32 vectors runs as concurrent lanes (one host thread, HIP stream and workspace per
+    lane, hec_engine.hip matvec_lanes): 48 columns -> 3 lanes of 16; every output equals the oracle's."""
+    e = env11
+    n = 10
+    A = [e.enc(seed=3000 + j) for j in range(n)]
+    X = [e.enc(seed=3100 + i) for i in range(48)]
+    exp = e.o.matmul_diag_col(A, X, e.rk_h, e.gk_h, nthreads=8)
+    got = e.ctx.matmul_diag_col([e.up(a) for a in A], [e.up(x) for x in X], e.rk, e.gk)
+    for g, c in zip(got, exp):
+        e.same(g, c)
+    # a second call reuses the lanes (their streams, workspaces and the per-key tables)
+    got2 = e.ctx.matmul_diag_col([e.up(a) for a in A], [e.up(x) for x in X[:33]], e.rk, e.gk)
+    for g, c in zip(got2, exp[:33]):
+        e.same(g, c)
+
+
 def test_matvec_partial_finish_equals_full(env11):
     e = env11
     n = 10
