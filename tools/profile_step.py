@@ -1,0 +1,29 @@
+"""rocprofv3 kernel-trace average of the roofline kernel over bench.py's profile step only (development
+tool).  bench.py times its steps with the batch split into concurrent lanes, then runs one extra step as a
+single lane with HIP event pairs (the roofline's avg_ms); that step's dispatches are the roofline kernel's
+last `launches_per_step` dispatches in the trace.
+usage: python tools/profile_step.py <run_kernel_trace.csv> <bench.json> <out.json>"""
+import csv
+import json
+import sys
+
+trace, bench, out = sys.argv[1:4]
+line = json.loads(open(bench).read().strip().splitlines()[-1])
+roof = line["roofline"]
+kern, nlast = roof["kernel"], roof["launches_per_step"]
+durs = []
+for r in csv.DictReader(open(trace)):
+    name = r["Kernel_Name"]
+    base = name[name.find("k_"):].split("<")[0].split("(")[0] if "k_" in name else name
+    if base == kern:
+        durs.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]) - int(r["Start_Timestamp"])))
+durs.sort()
+last = [d for _, d in durs[-nlast:]]
+res = {"kernel": kern, "profile_step_dispatches": len(last),
+       "profile_step_avg_us": round(sum(last) / len(last) / 1e3, 2),
+       "event_timed_avg_us": round(roof["avg_ms"] * 1e3, 2),
+       "all_dispatches": len(durs), "all_dispatch_avg_us": round(sum(d for _, d in durs) / len(durs) / 1e3, 2),
+       "note": "timed steps run the batch as concurrent lanes (smaller, overlapping launches); the profile "
+               "step runs one lane, as the event-timed roofline does"}
+json.dump(res, open(out, "w"), indent=1)
+print(json.dumps(res))
