@@ -9,6 +9,11 @@
 //          batched_col    (COL_OR_DIAG = 0: A col-batched x A^T)
 //          ops            (operator expressions: ((eval%gk%c0) << 5) * c1, relin, rescale, + c2 ...)
 //          matrix         (Matrix 2x2 elementwise-ciphertext matmul, he_linalg.cpp:202-236)
+//          encode         (the demo's plaintexts: CKKSEncoder::encode of mat1's columns, the data of
+//                          matrix_operations.cpp:1079-1087 at dim = #ciphertexts in the input, scale 2^40,
+//                          matrix_operations.cpp:1106-1108; written as size-1 entries)
+#include <cmath>
+#include <complex>
 #include <cstdio>
 #include <cstring>
 #include <fstream>
@@ -101,7 +106,7 @@ void write_output(const char *path, const std::vector<const Ciphertext *> &cts)
 int main(int argc, char **argv)
 {
     if (argc != 4) {
-        std::cout << "usage: he_demo <batched_diag|batched_col|ops|matrix> <in.bin> <out.bin>\n";
+        std::cout << "usage: he_demo <batched_diag|batched_col|ops|matrix|encode> <in.bin> <out.bin>\n";
         return 1;
     }
     const std::string mode = argv[1];
@@ -160,6 +165,38 @@ int main(int argc, char **argv)
         Matrix B(2, 2, std::vector<Ciphertext>(cts.begin() + 4, cts.begin() + 8));
         Matrix C = A.matmul(eval, rk, B);
         for (const auto &c : C.get_elems()) keep.push_back(c);
+    } else if (mode == "encode") {
+        // matrix_operations.cpp:1079-1087: mat1[c][r] = 2 + dim c + r; each column replicated over the
+        // slots as BatchedVector does; CKKSEncoder cencd(ctx); cencd.encode(mat1[i], scale, pt[i])
+        const std::size_t dim = cts.size(), slots = ctx.slot_count();
+        std::vector<std::vector<std::complex<double>>> mat1(dim, std::vector<std::complex<double>>(slots));
+        int counter = 2;
+        for (std::size_t c = 0; c < dim; ++c) {
+            for (std::size_t r = 0; r < slots; ++r) mat1[c][r] = std::complex<double>(counter + r % dim, 0);
+            counter += (int)dim;
+        }
+        hecdna::CKKSEncoder cencd(ctx);
+        std::vector<hecdna::Plaintext> pts(dim);
+        for (std::size_t i = 0; i + 1 < dim; ++i) cencd.encode(mat1[i], std::pow(2.0, 40), pts[i]);
+        std::vector<double> lastcol(slots);  // the last column through the batched real-valued form
+        for (std::size_t r = 0; r < slots; ++r) lastcol[r] = mat1[dim - 1][r].real();
+        std::vector<hecdna::Plaintext> last;
+        cencd.encode_batch({lastcol}, std::pow(2.0, 40), last);
+        pts[dim - 1] = last[0];
+        std::ofstream f(argv[3], std::ios::binary);
+        const std::uint64_t n = dim;
+        f.write(reinterpret_cast<const char *>(&n), 8);
+        for (const auto &p : pts) {
+            const std::uint64_t s = 1, l = p.level();
+            const double sc = p.scale();
+            const auto d = p.download();
+            f.write(reinterpret_cast<const char *>(&s), 8);
+            f.write(reinterpret_cast<const char *>(&l), 8);
+            f.write(reinterpret_cast<const char *>(&sc), 8);
+            f.write(reinterpret_cast<const char *>(d.data()), d.size() * 8);
+        }
+        std::cout << "he_demo encode: wrote " << dim << " plaintexts\n";
+        return 0;
     } else {
         std::cout << "No such demo for " << mode << ".\n";
         return 1;

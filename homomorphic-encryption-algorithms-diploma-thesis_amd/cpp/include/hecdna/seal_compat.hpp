@@ -8,11 +8,14 @@
 //                                                copy = deep device copy, like SEAL)
 //   seal::RelinKeys / GaloisKeys              -> hecdna::RelinKeys / GaloisKeys
 //   seal::CoeffModulus::Create                -> hecdna::CoeffModulus::Create
+//   seal::CKKSEncoder::encode                 -> hecdna::CKKSEncoder::encode (on the GPU, hec_encode;
+//                                                SEAL's parms_id argument is the level here)
 //
 // Errors are rethrown with SEAL's exception types and messages (std::invalid_argument,
 // std::logic_error); HIP failures as std::runtime_error.  Objects live on the context's GPU.
 #pragma once
 
+#include <complex>
 #include <cstddef>
 #include <cstdint>
 #include <memory>
@@ -163,17 +166,84 @@ private:
 class Plaintext {
 public:
     Plaintext() = default;
-    Plaintext(const Context &ctx, const std::uint64_t *data, std::size_t level, double scale)
+    explicit Plaintext(const Context &ctx) : ctx_(&ctx) { create(); }
+    Plaintext(const Context &ctx, const std::uint64_t *data, std::size_t level, double scale) : ctx_(&ctx)
     {
-        hec_plaintext *p = nullptr;
-        check(hec_plaintext_create(ctx.get(), &p));
-        h_.reset(p, [](hec_plaintext *x) { hec_plaintext_destroy(x); });
-        check(hec_plaintext_upload(p, data, level, scale));
+        create();
+        check(hec_plaintext_upload(h_.get(), data, level, scale));
     }
     hec_plaintext *get() const { return h_.get(); }
+    // bind a default-constructed plaintext to a context (CKKSEncoder::encode's destination)
+    void bind(const Context &ctx)
+    {
+        if (!h_ || ctx_ != &ctx) { ctx_ = &ctx; create(); }
+    }
+    std::size_t level() const { std::uint64_t l = 0; check(hec_plaintext_info(h_.get(), &l, nullptr)); return l; }
+    double scale() const { double s = 0; check(hec_plaintext_info(h_.get(), nullptr, &s)); return s; }
+    // SEAL layout u64[level][N] (seal::Plaintext::data() of an NTT-form CKKS plaintext)
+    std::vector<std::uint64_t> download() const
+    {
+        std::vector<std::uint64_t> v(level() * ctx_->poly_modulus_degree());
+        check(hec_plaintext_download(h_.get(), v.data()));
+        return v;
+    }
 
 private:
+    void create()
+    {
+        hec_plaintext *p = nullptr;
+        check(hec_plaintext_create(ctx_->get(), &p));
+        h_.reset(p, [](hec_plaintext *x) { hec_plaintext_destroy(x); });
+    }
+    const Context *ctx_ = nullptr;
     std::shared_ptr<hec_plaintext> h_;
+};
+
+// seal::CKKSEncoder (reference: `CKKSEncoder cencd(ctx); cencd.encode(mat1[i], scale, pt)`,
+// src/demos/matrix_operations.cpp:1106-1108) — encoding runs on the GPU (hec_encode); encode_batch
+// encodes many slot vectors in one call.  Without a level the top level (all data primes) is used,
+// as SEAL's first parms_id.
+class CKKSEncoder {
+public:
+    explicit CKKSEncoder(const Context &ctx) : ctx_(&ctx) {}
+    std::size_t slot_count() const { return ctx_->slot_count(); }
+    void encode(const std::vector<double> &values, double scale, Plaintext &destination) const
+    {
+        encode(values, top(), scale, destination);
+    }
+    void encode(const std::vector<double> &values, std::size_t level, double scale, Plaintext &destination) const
+    {
+        destination.bind(*ctx_);
+        hec_plaintext *p = destination.get();
+        check(hec_encode(ctx_->get(), values.data(), nullptr, values.size(), 1, scale, level, &p));
+    }
+    void encode(const std::vector<std::complex<double>> &values, double scale, Plaintext &destination) const
+    {
+        std::vector<double> re(values.size()), im(values.size());
+        for (std::size_t i = 0; i < values.size(); ++i) { re[i] = values[i].real(); im[i] = values[i].imag(); }
+        destination.bind(*ctx_);
+        hec_plaintext *p = destination.get();
+        check(hec_encode(ctx_->get(), re.data(), im.data(), values.size(), 1, scale, top(), &p));
+    }
+    // every row must have the same length (at most slot_count())
+    void encode_batch(const std::vector<std::vector<double>> &rows, double scale, std::vector<Plaintext> &destination) const
+    {
+        const std::size_t nv = rows.empty() ? 0 : rows[0].size();
+        std::vector<double> flat;
+        flat.reserve(rows.size() * nv);
+        for (const auto &r : rows) {
+            if (r.size() != nv) throw std::invalid_argument("values has invalid size");
+            flat.insert(flat.end(), r.begin(), r.end());
+        }
+        destination.resize(rows.size());
+        std::vector<hec_plaintext *> ps(rows.size());
+        for (std::size_t i = 0; i < rows.size(); ++i) { destination[i].bind(*ctx_); ps[i] = destination[i].get(); }
+        check(hec_encode(ctx_->get(), flat.data(), nullptr, nv, rows.size(), scale, top(), ps.data()));
+    }
+
+private:
+    std::size_t top() const { return ctx_->coeff_modulus().size() - 1; }
+    const Context *ctx_;
 };
 
 class RelinKeys {

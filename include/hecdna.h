@@ -19,7 +19,8 @@
  *
  * Objects are device-resident on the context's GPU; every call is ordered on the context's HIP
  * stream (hec_context_set_stream), downloads synchronise.  One context per device, one host
- * thread per context.  No torch types cross this boundary.
+ * thread per context (a matvec over >= 32 vectors runs as concurrent lanes on engine-owned threads and
+ * streams, joined before it returns).  No torch types cross this boundary.
  */
 #ifndef HECDNA_H
 #define HECDNA_H

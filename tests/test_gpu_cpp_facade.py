@@ -110,6 +110,23 @@ def test_demo_operator_surface(demo, small, tmp_path):
         same(g, e)
 
 
+def test_demo_ckks_encoder(demo, orc, tmp_path):
+    """hecdna::CKKSEncoder (the GPU encoder behind seal::CKKSEncoder's encode) on the reference demo's
+    plaintexts (matrix_operations.cpp:1079-1108) at cfg1 parameters equals the oracle's encode()."""
+    from _helpers import reference_matrix, col_vector
+    N = 1 << 13
+    m = orc.Oracle.create_coeff_modulus(N, [60, 40, 40, 60])
+    o = orc.Oracle(N, m)
+    dim = 16  # the demo encodes #ciphertexts columns; the ciphertexts themselves are not read
+    dummy = [orc.Ct(np.zeros((1, 3, N), dtype=np.uint64), 1.0) for _ in range(dim)]
+    out = run(demo, "encode", tmp_path, N, m, dummy, None, {})
+    M = reference_matrix(dim)
+    assert len(out) == dim
+    for c, (d, sc) in enumerate(out):
+        assert sc == 2.0**40
+        assert np.array_equal(d[0], o.encode(col_vector(M[:, c], N // 2), 2.0**40, 3))
+
+
 def test_demo_matrix_matmul(demo, small, tmp_path):
     N, m, o, rk, gk, cts = small
     out = run(demo, "matrix", tmp_path, N, m, cts[:8], rk, gk)
