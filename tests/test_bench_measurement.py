@@ -1,0 +1,55 @@
+"""bench.py's measurement formulas (CPU): the algorithmic bytes per matvec restate SURVEY §8(d), the
+key-switch counts are SEAL's NAF schedule and the trie's, and tools/profile_step.py picks the profile
+step's dispatches out of a kernel trace."""
+import csv
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+@pytest.fixture(scope="module")
+def bench():
+    import bench as b
+    return b
+
+
+@pytest.mark.parametrize("B,gb", [(1, 1283.76), (8, 346.29), (64, 229.11)])
+def test_algorithmic_bytes_match_survey(bench, B, gb):
+    # cfg3, KS = 18,204 -> 1,283.76 / 346.29 / 229.11 GB per matvec at B = 1 / 8 / 64
+    assert round(bench.algorithmic_bytes_per_matvec(1 << 15, 10, 4096, B, 18204) / 1e9, 2) == gb
+
+
+def test_key_switch_counts(bench):
+    from _helpers import rotation_trie_stats
+    assert bench.ks_total(1 << 15, 4096) == 18204  # SEAL's schedule, SURVEY §8(a)
+    assert bench.ks_total(1 << 13, 64) == 156
+    ks, hoisted, children, others = rotation_trie_stats(1 << 15, 4096)
+    assert (ks, hoisted, children, others) == (5460, 1024, 4436, 1024)
+    assert rotation_trie_stats(1 << 16, 1024)[0] == 1364  # cfg5
+
+
+def test_profile_step_tool(tmp_path):
+    # 3 timed steps x 2 dispatches (lanes) then a 2-dispatch profile step of 10 us each
+    trace = tmp_path / "trace.csv"
+    with open(trace, "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(["Kernel_Name", "Start_Timestamp", "End_Timestamp"])
+        t = 0
+        for d in [30_000] * 6 + [10_000, 10_000]:
+            w.writerow(["void hec::k_hmacm<4, 2, 2, 3>(...)", t, t + d])
+            w.writerow(["void hec::k_ntt<...>(...)", t + d, t + d + 5])
+            t += d + 100
+    benchj = tmp_path / "bench.json"
+    benchj.write_text(json.dumps({"roofline": {"kernel": "k_hmacm", "launches_per_step": 2, "avg_ms": 0.0101}}))
+    out = tmp_path / "out.json"
+    subprocess.check_call([sys.executable, os.path.join(ROOT, "tools", "profile_step.py"), str(trace), str(benchj),
+                           str(out)], stdout=subprocess.DEVNULL)
+    r = json.load(open(out))
+    assert r["profile_step_dispatches"] == 2 and r["profile_step_avg_us"] == 10.0
+    assert r["all_dispatches"] == 8 and r["event_timed_avg_us"] == 10.1
