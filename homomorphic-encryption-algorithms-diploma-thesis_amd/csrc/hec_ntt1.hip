@@ -15,6 +15,8 @@
 //     every register index stays compile-time);
 //   exchange 2 (m <-> l inside each group of 32 threads with the same h): waves with a4 == P in phase P.
 // Padded strides (33 words) keep both access patterns of each exchange free of bank conflicts.
+#include <mutex>
+
 #include "hec_internal.h"
 
 namespace hec {
@@ -166,14 +168,12 @@ bool ntt1_forward_strided(Ctx &c, const u64 *src, u64 ps_src, u64 *dst, u64 ps_d
     for (int i = 0; i < nl; ++i) (c.hprimes[pmap[i]].fp ? anyfp : anyint) = true;
     const int cls = anyfp && anyint ? 0 : anyfp ? 1 : 2;
     constexpr int bytes = NTT1_LDS_WORDS * 8;
-    static bool attr[3] = {false, false, false};
+    static std::once_flag attr[3];  // lanes may launch from several host threads
     const void *fn = cls == 0 ? reinterpret_cast<const void *>(&k_ntt1_fwd<0>)
                      : cls == 1 ? reinterpret_cast<const void *>(&k_ntt1_fwd<1>)
                                 : reinterpret_cast<const void *>(&k_ntt1_fwd<2>);
-    if (!attr[cls]) {
-        HEC_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
-        attr[cls] = true;
-    }
+    std::call_once(attr[cls],
+                   [&] { HEC_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes)); });
     const u64 *twi = reinterpret_cast<const u64 *>(c.tw), *twf = reinterpret_cast<const u64 *>(c.twf);
     const dim3 g((unsigned)njobs);
     if (cls == 0) k_ntt1_fwd<0><<<g, 1024, bytes, c.stream>>>(io, twi, twf, c.primes);
