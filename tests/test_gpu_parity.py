@@ -371,6 +371,19 @@ def test_matvec_ct_x_pt_bitexact(request, which, n):
         e.same(g, c)
 
 
+def test_matvec_ct_x_pt_batch_lanes(env11):
+    """The ct x pt form over 40 vectors (2 concurrent lanes of 20) equals the oracle's SEAL flow."""
+    e = env11
+    L = len(e.m) - 1
+    pscale = 2.0**40
+    P = [e.o.encode(e.rng.uniform(-1, 1, e.N // 2), pscale, L) for _ in range(7)]
+    X = [e.enc(seed=3300 + i) for i in range(40)]
+    exp = _ctpt_oracle(e, P, pscale, X)
+    got = e.ctx.matmul_diagpt_col([e.ctx.plaintext(p, pscale) for p in P], [e.up(x) for x in X], e.gk)
+    for g, c in zip(got, exp):
+        e.same(g, c)
+
+
 def test_matvec_ct_x_pt_errors(env11, hecdna):
     e = env11
     L = len(e.m) - 1
