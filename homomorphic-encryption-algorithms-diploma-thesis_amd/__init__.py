@@ -345,6 +345,18 @@ class Context:
         _check(fn(self.h, buf.p, limb0, nl, npolys))
         return buf.download(a.shape)
 
+    def dyadic_multiply(self, a: np.ndarray, b: np.ndarray, limb0=0):
+        """a, b host u64[npolys][nlimbs][N] -> (a * b) mod q_(limb0 + limb) (device round trip)."""
+        a = np.ascontiguousarray(a, dtype=np.uint64)
+        b = np.ascontiguousarray(b, dtype=np.uint64)
+        if a.shape != b.shape or a.ndim != 3:
+            raise InvalidArgument(1, "operands must have the same shape u64[npolys][nlimbs][N]")
+        bufs = [DeviceBuffer(self, a.nbytes) for _ in range(3)]
+        bufs[0].upload(a)
+        bufs[1].upload(b)
+        _check(lib().hec_dyadic_multiply(self.h, bufs[0].p, bufs[1].p, bufs[2].p, limb0, a.shape[1], a.shape[0]))
+        return bufs[2].download(a.shape)
+
     def profile(self, mode=1):
         """0 off, 1 synchronous per phase, 2 asynchronous event pairs (resolved by profile_read)."""
         _check(lib().hec_profile_enable(self.h, int(mode)))

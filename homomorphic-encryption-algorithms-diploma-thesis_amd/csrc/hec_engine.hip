@@ -685,6 +685,53 @@ void walk_trie_hoisted(Ctx &c, Scratch &s, const RotTrie &t, int node, PolyArr s
     }
 }
 
+// The argument checks SEAL runs along the reference loop (rotate_internal, multiply[_plain]_inplace's
+// scale bound, add_inplace's are_close, relinearize / rescale at the end of the chain), in its order, on
+// the host.  Returns the product scale of every output.  matvec_lanes runs it on the calling thread over
+// the whole batch before any lane starts, so a failing call writes no output (as in SEAL).
+std::vector<double> matvec_check(hec_context *ctx, const hec_ciphertext *const *diags, const hec_plaintext *const *pdiags,
+                                 std::size_t n, const std::vector<std::size_t> &js, const hec_ciphertext *const *cols,
+                                 std::size_t p, const hec_kswitch_key *rk, const hec_galois_keys *gk, bool finish)
+{
+    const Ctx &c = ctx->c;
+    const bool pt = pdiags != nullptr;
+    need(n >= 1 && p >= 1 && !js.empty(), "empty matrix operand");
+    for (std::size_t j : js) need(j < n, "diagonal index out of range");
+    need(gk && gk->ctx == ctx, "galois_keys is not valid for encryption parameters");
+    if (finish && !pt) need(rk && rk->ctx == ctx, "relin_keys is not valid for encryption parameters");
+    const std::size_t l = cols[0]->level;
+    for (std::size_t i = 0; i < p; ++i) check_ct(ctx, cols[i]);
+    for (std::size_t i = 0; i < p; ++i) need(cols[i]->size == 2, "encrypted size must be 2");
+    for (std::size_t i = 0; i < p; ++i) need(cols[i]->level == l, "encrypted1 and encrypted2 parameter mismatch");
+    if (pt) {
+        for (std::size_t j : js)
+            need(pdiags[j] && pdiags[j]->ctx == ctx && pdiags[j]->d, "plain is not valid for encryption parameters");
+        for (std::size_t j : js) need(pdiags[j]->level == l, "encrypted_ntt and plain_ntt parameter mismatch");
+    } else {
+        for (std::size_t j : js) check_ct(ctx, diags[j]);
+        for (std::size_t j : js) need(diags[j]->size == 2, "encrypted size must be 2");
+        for (std::size_t j : js) need(diags[j]->level == l, "encrypted1 and encrypted2 parameter mismatch");
+    }
+    auto dscale = [&](std::size_t j) { return pt ? pdiags[j]->scale : diags[j]->scale; };
+    // scale bookkeeping exactly as multiply[_plain]_inplace (bound) + add_inplace (are_close) would see it
+    std::vector<double> ps(p);
+    for (std::size_t i = 0; i < p; ++i) {
+        for (std::size_t k = 0; k < js.size(); ++k) {
+            const double sc = cols[i]->scale * dscale(js[k]);
+            need(scale_ok(c, sc, l), "scale out of bounds");
+            if (k == 0) ps[i] = sc;
+            else need(are_close(ps[i], sc), "scale mismatch");
+        }
+    }
+    if (finish && l < 2) throw std::invalid_argument("end of modulus switching chain reached");
+    std::vector<u32> seq;  // rotate_internal's own errors ("step count too large", "Galois key not present")
+    for (std::size_t j : js) {
+        seq.clear();
+        rotation_elts(c, (int)j, *gk, seq);
+    }
+    return ps;
+}
+
 // BatchedMatrix::matmul diag x col (he_linalg.cpp:943-1006) for the p columns at once, diagonals
 // [jb, je).  The loop over i (output column) is interchanged with the loop over j so that one
 // rotation launch sequence and one key read serve all p columns, and the rotations run over the
@@ -699,36 +746,9 @@ void matvec_core(hec_context *ctx, const hec_ciphertext *const *diags, const hec
 {
     Ctx &c = exec ? *exec : ctx->c;
     const bool pt = pdiags != nullptr;
-    need(n >= 1 && p >= 1 && !js.empty(), "empty matrix operand");
-    for (std::size_t j : js) need(j < n, "diagonal index out of range");
-    need(gk && gk->ctx == ctx, "galois_keys is not valid for encryption parameters");
-    if (finish && !pt) need(rk && rk->ctx == ctx, "relin_keys is not valid for encryption parameters");
+    const std::vector<double> ps = matvec_check(ctx, diags, pdiags, n, js, cols, p, rk, gk, finish);
     const std::size_t l = cols[0]->level, N = c.N;
-    for (std::size_t i = 0; i < p; ++i) check_ct(ctx, cols[i]);
-    for (std::size_t i = 0; i < p; ++i) need(cols[i]->size == 2, "encrypted size must be 2");
-    for (std::size_t i = 0; i < p; ++i) need(cols[i]->level == l, "encrypted1 and encrypted2 parameter mismatch");
-    if (pt) {
-        for (std::size_t j : js)
-            need(pdiags[j] && pdiags[j]->ctx == ctx && pdiags[j]->d, "plain is not valid for encryption parameters");
-        for (std::size_t j : js) need(pdiags[j]->level == l, "encrypted_ntt and plain_ntt parameter mismatch");
-    } else {
-        for (std::size_t j : js) check_ct(ctx, diags[j]);
-        for (std::size_t j : js) need(diags[j]->size == 2, "encrypted size must be 2");
-        for (std::size_t j : js) need(diags[j]->level == l, "encrypted1 and encrypted2 parameter mismatch");
-    }
-    auto dscale = [&](std::size_t j) { return pt ? pdiags[j]->scale : diags[j]->scale; };
     auto ddata = [&](std::size_t j) -> const u64 * { return pt ? pdiags[j]->d : diags[j]->d; };
-    // scale bookkeeping exactly as multiply[_plain]_inplace (bound) + add_inplace (are_close) would see it
-    std::vector<double> ps(p);
-    for (std::size_t i = 0; i < p; ++i) {
-        for (std::size_t k = 0; k < js.size(); ++k) {
-            const double sc = cols[i]->scale * dscale(js[k]);
-            need(scale_ok(c, sc, l), "scale out of bounds");
-            if (k == 0) ps[i] = sc;
-            else need(are_close(ps[i], sc), "scale mismatch");
-        }
-    }
-    if (finish && l < 2) throw std::invalid_argument("end of modulus switching chain reached");
     RotTrie trie;
     {
         std::vector<u32> seq;
@@ -878,8 +898,7 @@ void matvec_lanes(hec_context *ctx, const hec_ciphertext *const *diags, const he
         matvec_core(ctx, diags, pdiags, n, js, cols, p, rk, gk, finish, out);
         return;
     }
-    need(gk && gk->ctx == ctx, "galois_keys is not valid for encryption parameters");
-    check_ct(ctx, cols[0]);
+    matvec_check(ctx, diags, pdiags, n, js, cols, p, rk, gk, finish);  // whole batch, before any lane writes
     if (c.hoist) {  // the lazily built per-key tables, before the lanes only read them
         auto &gkm = const_cast<hec_galois_keys &>(*gk);
         for (auto &kv : gkm.keys) {
@@ -980,8 +999,13 @@ int hec_context_create(uint64_t N, const uint64_t *mod, uint64_t K, int device, 
         need(out != nullptr, "out is null");
         need(N >= 1024 && N <= 65536 && !(N & (N - 1)), "poly_modulus_degree must be a power of two in [2^10, 2^16]");
         need(K >= 2 && K - 1 <= HEC_MAXL, "coeff_modulus size is invalid");
+        // SEAL's context validation: every modulus at most SEAL_USER_MOD_BIT_COUNT_MAX = 60 bits, prime,
+        // = 1 mod 2N (NTT-friendly) and pairwise coprime.  The 60-bit bound is also what keeps the sharded
+        // exchange's plain int64 sum of up to 8 partial residues exact (shard.py exchange_partials).
         for (uint64_t i = 0; i < K; ++i)
-            need(isprime(mod[i]) && (mod[i] - 1) % (2 * N) == 0 && !(mod[i] >> 61), "coeff_modulus is invalid");
+            need(isprime(mod[i]) && (mod[i] - 1) % (2 * N) == 0 && !(mod[i] >> 60), "coeff_modulus is invalid");
+        for (uint64_t i = 0; i < K; ++i)
+            for (uint64_t j = 0; j < i; ++j) need(mod[i] != mod[j], "coeff_modulus is invalid");
         HEC_HIP(hipSetDevice(device));
         auto *ctx = new hec_context();
         Ctx &c = ctx->c;
@@ -991,7 +1015,6 @@ int hec_context_create(uint64_t N, const uint64_t *mod, uint64_t K, int device, 
         if (const char *f = std::getenv("HEC_FUSE_GALOIS")) c.fuse_galois = f[0] != '0';
         if (const char *f = std::getenv("HEC_FAN")) c.fan_out = f[0] != '0';
         if (const char *f = std::getenv("HEC_LANES")) c.lanes = std::max(1, std::atoi(f));
-        if (const char *f = std::getenv("HEC_NTT1")) c.ntt1 = std::atoi(f);
         if (const char *f = std::getenv("HEC_FANG"))
             std::sscanf(f, "%d,%d,%d", &c.fan_groups_moddown, &c.fan_groups_modup, &c.fan_groups_hoist);
         if (const char *f = std::getenv("HEC_HOIST")) c.hoist = f[0] != '0';

@@ -88,7 +88,6 @@ struct Ctx {
     int fan_groups_modup = 1;      // per launch x groups; the source's inverse pass is repeated per group)
     int fan_groups_hoist = 1;
     bool fan_out = true;           // HEC_FAN=0: separate INTT pass A (fan-out fuses it into the forward passes A)
-    int ntt1 = 0;                  // HEC_NTT1: single-pass (one workgroup per limb) N = 2^15 NTT kernels
     int lanes = 3;                 // HEC_LANES: concurrent batch lanes of a matvec (hec_engine.hip matvec_lanes)
     int lane_min_batch = 16;       // input vectors per lane at least
     bool fuse_galois = true;       // HEC_FUSE_GALOIS=0: materialise apply_galois before the key switch
@@ -179,9 +178,6 @@ void fill_uniform(Ctx &c, u64 *p, int npoly, int nl, int limb_prime0, int specia
 // CKKS encode of `count` slot vectors (hec_encode.hip): re/im device [count][nv] (im may be null), work
 // device doubles [count][2N], out [count][level][N] NTT form, maxabs[count] = max |coefficient| (bits
 // of a double)
-// single-pass forward NTT at N = 2^15 (hec_ntt1.hip); false when the shape is not supported
-bool ntt1_forward_strided(Ctx &c, const u64 *src, u64 ps_src, u64 *dst, u64 ps_dst, int nl, const int *pmap,
-                          int njobs, u32 elt);
 void encode_batch(Ctx &c, const double *re, const double *im, u64 nv, int count, double scale, int level, double *work,
                   u64 *out, u64 *maxabs);
 

@@ -456,8 +456,6 @@ void ntt_strided(Ctx &c, bool inverse, const u64 *src, u64 ps_src, u64 *dst, u64
                  int njobs, u32 elt, int stages)
 {
     if (nl > HEC_MAXL + 1) throw std::invalid_argument("too many limbs");
-    if (!inverse && stages == 3 && (c.ntt1 & 1) && ntt1_forward_strided(c, src, ps_src, dst, ps_dst, nl, pmap, njobs, elt))
-        return;
     const StridedIO first = strided(src, dst, ps_src, ps_dst, nl, c.logN, pmap, elt);
     const StridedIO second = strided(dst, dst, ps_dst, ps_dst, nl, c.logN, pmap);
     if (inverse) ntt_dispatch<true>(c, njobs, first, second, stages);

@@ -862,16 +862,17 @@ void rotate_vector_inplace(const Context &ctx, Ciphertext &a, int steps, const G
 }
 
 // =============================================================== he::linalg ==================
-std::vector<Ciphertext> matmul_diag_col(const Context &ctx, const std::vector<const Ciphertext *> &A,
-                                        const std::vector<const Ciphertext *> &X, const KSwitchKey &rk,
-                                        const GaloisKeys &gk, int nthreads, std::size_t j_begin,
-                                        std::size_t j_end, bool finish)
+std::vector<Ciphertext> matmul_diag_col_set(const Context &ctx, const std::vector<const Ciphertext *> &A,
+                                            const std::vector<std::size_t> &js,
+                                            const std::vector<const Ciphertext *> &X, const KSwitchKey &rk,
+                                            const GaloisKeys &gk, int nthreads, bool finish)
 {
-    const std::size_t n = A.size(), p = X.size();
-    j_end = std::min(j_end, n);
-    if (j_begin >= j_end) throw std::invalid_argument("empty diagonal range");
+    // A[k] is diagonal js[k]; out[i] = sum_k A[k] (*) rot(X[i], js[k])  (he_linalg.cpp:977-997 restricted
+    // to the diagonals js; a partition of [0, n) summed mod q gives the full loop's accumulator)
+    const std::size_t nj = js.size(), p = X.size();
+    if (nj == 0 || A.size() != nj) throw std::invalid_argument("empty diagonal range");
     nthreads = std::max(1, nthreads);
-    const std::size_t chunks = std::min<std::size_t>((std::size_t)nthreads, j_end - j_begin);
+    const std::size_t chunks = std::min<std::size_t>((std::size_t)nthreads, nj);
     std::vector<std::vector<Ciphertext>> part(p, std::vector<Ciphertext>(chunks));
     std::atomic<std::size_t> next{0};
     std::vector<std::string> errs(nthreads);
@@ -881,14 +882,13 @@ std::vector<Ciphertext> matmul_diag_col(const Context &ctx, const std::vector<co
                 const std::size_t w = next.fetch_add(1);
                 if (w >= p * chunks) break;
                 const std::size_t i = w / chunks, c = w % chunks;
-                const std::size_t span = j_end - j_begin;
-                const std::size_t jb = j_begin + span * c / chunks, je = j_begin + span * (c + 1) / chunks;
+                const std::size_t kb = nj * c / chunks, ke = nj * (c + 1) / chunks;
                 Ciphertext acc;
-                for (std::size_t j = jb; j < je; ++j) {  // he_linalg.cpp:977-997
+                for (std::size_t k = kb; k < ke; ++k) {  // he_linalg.cpp:977-997
                     Ciphertext t = *X[i];
-                    rotate_vector_inplace(ctx, t, (int)j, gk);
-                    multiply_inplace(ctx, t, *A[j]);
-                    if (j == jb) acc = std::move(t);
+                    rotate_vector_inplace(ctx, t, (int)js[k], gk);  // always from the original column (:988)
+                    multiply_inplace(ctx, t, *A[k]);
+                    if (k == kb) acc = std::move(t);
                     else add_inplace(ctx, acc, t);
                 }
                 part[i][c] = std::move(acc);
@@ -915,24 +915,53 @@ std::vector<Ciphertext> matmul_diag_col(const Context &ctx, const std::vector<co
     return out;
 }
 
+std::vector<Ciphertext> matmul_diag_col(const Context &ctx, const std::vector<const Ciphertext *> &A,
+                                        const std::vector<const Ciphertext *> &X, const KSwitchKey &rk,
+                                        const GaloisKeys &gk, int nthreads, std::size_t j_begin,
+                                        std::size_t j_end, bool finish)
+{
+    j_end = std::min(j_end, A.size());
+    if (j_begin >= j_end) throw std::invalid_argument("empty diagonal range");
+    std::vector<std::size_t> js;
+    std::vector<const Ciphertext *> a;
+    for (std::size_t j = j_begin; j < j_end; ++j) { js.push_back(j); a.push_back(A[j]); }
+    return matmul_diag_col_set(ctx, a, js, X, rk, gk, nthreads, finish);
+}
+
 std::vector<Ciphertext> matmul_col_colT(const Context &ctx, const std::vector<const Ciphertext *> &A,
                                         const std::vector<const Ciphertext *> &B, std::size_t p,
-                                        const KSwitchKey &rk, const GaloisKeys &gk)
+                                        const KSwitchKey &rk, const GaloisKeys &gk, int nthreads)
 {
+    // he_linalg.cpp:977-1002 with btype_is_col: out[i] = sum_j rot(B[j], i) (*) A[j]; outputs on threads
     const std::size_t n = A.size();
     if (B.size() != n) throw std::invalid_argument("dimension mismatch");
     std::vector<Ciphertext> out(p);
-    for (std::size_t i = 0; i < p; ++i) {
-        for (std::size_t j = 0; j < n; ++j) {
-            Ciphertext t = *B[j];
-            rotate_vector_inplace(ctx, t, (int)i, gk);
-            multiply_inplace(ctx, t, *A[j]);
-            if (j == 0) out[i] = std::move(t);
-            else add_inplace(ctx, out[i], t);
-        }
-        relinearize_inplace(ctx, out[i], rk);
-        rescale_to_next_inplace(ctx, out[i]);
+    std::atomic<std::size_t> next{0};
+    nthreads = std::max(1, nthreads);
+    std::vector<std::string> errs(nthreads);
+    auto worker = [&](int tid) {
+        try {
+            for (std::size_t i; (i = next.fetch_add(1)) < p;) {
+                for (std::size_t j = 0; j < n; ++j) {
+                    Ciphertext t = *B[j];
+                    rotate_vector_inplace(ctx, t, (int)i, gk);
+                    multiply_inplace(ctx, t, *A[j]);
+                    if (j == 0) out[i] = std::move(t);
+                    else add_inplace(ctx, out[i], t);
+                }
+                relinearize_inplace(ctx, out[i], rk);
+                rescale_to_next_inplace(ctx, out[i]);
+            }
+        } catch (const std::exception &e) { errs[tid] = e.what(); }
+    };
+    if (nthreads == 1) worker(0);
+    else {
+        std::vector<std::thread> th;
+        for (int t = 0; t < nthreads; ++t) th.emplace_back(worker, t);
+        for (auto &t : th) t.join();
     }
+    for (auto &e : errs)
+        if (!e.empty()) throw std::invalid_argument(e);
     return out;
 }
 

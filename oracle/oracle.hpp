@@ -220,6 +220,12 @@ std::vector<int> naf(int value);  // SEAL util::naf, least-significant term firs
 // BatchedMatrix::matmul (he_linalg.cpp:943-1006), diag(this) x col(other), SMART_RELIN = 1:
 //   out[i] = rescale(relin( sum_{j<n} rot(X[i], j) (*) A[j] ))
 // nthreads > 1 splits j over threads with size-3 partial sums (bit-identical: modular adds).
+// The same loop restricted to the diagonals js (A[k] is diagonal js[k]): the partials the sharded
+// engine entry hec_matmul_diag_col_partial_set computes.
+std::vector<Ciphertext> matmul_diag_col_set(const Context &ctx, const std::vector<const Ciphertext *> &A,
+                                            const std::vector<std::size_t> &js,
+                                            const std::vector<const Ciphertext *> &X, const KSwitchKey &rk,
+                                            const GaloisKeys &gk, int nthreads, bool finish);
 std::vector<Ciphertext> matmul_diag_col(const Context &ctx, const std::vector<const Ciphertext *> &A,
                                         const std::vector<const Ciphertext *> &X, const KSwitchKey &rk,
                                         const GaloisKeys &gk, int nthreads = 1, std::size_t j_begin = 0,
@@ -227,7 +233,7 @@ std::vector<Ciphertext> matmul_diag_col(const Context &ctx, const std::vector<co
 // BatchedMatrix::matmul, col(this) x col(other)^T:  out[i] = rescale(relin(sum_j rot(B[j], i) (*) A[j]))
 std::vector<Ciphertext> matmul_col_colT(const Context &ctx, const std::vector<const Ciphertext *> &A,
                                         const std::vector<const Ciphertext *> &B, std::size_t p,
-                                        const KSwitchKey &rk, const GaloisKeys &gk);
+                                        const KSwitchKey &rk, const GaloisKeys &gk, int nthreads = 1);
 // Matrix::matmul (he_linalg.cpp:202-236): column-major elementwise ciphertext matrices
 std::vector<Ciphertext> matrix_matmul(const Context &ctx, const std::vector<const Ciphertext *> &A,
                                       std::size_t a_rows, std::size_t a_cols, bool a_transposed,

@@ -1,6 +1,8 @@
 // ORACLE C API — test infrastructure only (see oracle.hpp).  Flat extern "C" entry points so
 // tests/ (ctypes) and bench.py's cpu_baseline leg can drive the CPU restatement.
+#include <atomic>
 #include <cstring>
+#include <thread>
 #include <string>
 
 #include "oracle.hpp"
@@ -154,6 +156,34 @@ int orc_encrypt(void *c, const u64 *sk, const u64 *pt, u64 level, double scale, 
         std::memcpy(out, ct.data.data(), ct.data.size() * sizeof(u64));
     });
 }
+// encode + encrypt `count` real slot vectors (row v of re: n values) on nthreads threads; ciphertext v uses
+// seed0 + v.  Test-input factory for full-size matrices (4096 encrypted diagonals at cfg3).
+int orc_encrypt_many(void *c, const u64 *sk, const double *re, u64 n, u64 count, double scale, u64 level, u64 seed0,
+                     int nthreads, u64 *out)
+{
+    return guard([&] {
+        auto &ctx = *static_cast<Context *>(c);
+        const SecretKey key = sk_view(ctx, sk);
+        const u64 words = 2 * level * ctx.N();
+        std::atomic<u64> next{0};
+        std::vector<std::string> errs(std::max(1, nthreads));
+        auto worker = [&](int tid) {
+            try {
+                for (u64 v; (v = next.fetch_add(1)) < count;) {
+                    std::vector<std::complex<double>> vals(n);
+                    for (u64 i = 0; i < n; ++i) vals[i] = {re[v * n + i], 0.0};
+                    auto ct = encrypt_symmetric(ctx, key, encode(ctx, vals, scale, level), seed0 + v);
+                    std::memcpy(out + v * words, ct.data.data(), words * sizeof(u64));
+                }
+            } catch (const std::exception &e) { errs[tid] = e.what(); }
+        };
+        std::vector<std::thread> th;
+        for (int t = 0; t < std::max(1, nthreads); ++t) th.emplace_back(worker, t);
+        for (auto &t : th) t.join();
+        for (auto &e : errs)
+            if (!e.empty()) throw std::invalid_argument(e);
+    });
+}
 int orc_decrypt(void *c, const u64 *sk, const OrcCt *ct, u64 *out)
 {
     return guard([&] {
@@ -278,13 +308,24 @@ int orc_matmul_diag_col(void *c, const OrcCt *A, u64 n, const OrcCt *X, u64 p, c
         for (u64 i = 0; i < p; ++i) out_ct(r[i], out + i);
     });
 }
+int orc_matmul_diag_col_set(void *c, const OrcCt *A, const u64 *js, u64 nj, const OrcCt *X, u64 p, const u64 *rk,
+                            const u32 *elts, const u64 *const *keys, u64 nkeys, OrcCt *out, int nthreads, int finish)
+{
+    return guard([&] {
+        auto &ctx = *static_cast<Context *>(c);
+        auto a = in_many(ctx, A, nj), x = in_many(ctx, X, p);
+        auto r = matmul_diag_col_set(ctx, ptrs(a), std::vector<std::size_t>(js, js + nj), ptrs(x), view(rk),
+                                     gkeys(elts, keys, nkeys), nthreads, finish != 0);
+        for (u64 i = 0; i < p; ++i) out_ct(r[i], out + i);
+    });
+}
 int orc_matmul_col_colT(void *c, const OrcCt *A, u64 n, const OrcCt *B, u64 p, const u64 *rk, const u32 *elts,
-                        const u64 *const *keys, u64 nkeys, OrcCt *out)
+                        const u64 *const *keys, u64 nkeys, OrcCt *out, int nthreads)
 {
     return guard([&] {
         auto &ctx = *static_cast<Context *>(c);
         auto a = in_many(ctx, A, n), b = in_many(ctx, B, n);
-        auto r = matmul_col_colT(ctx, ptrs(a), ptrs(b), p, view(rk), gkeys(elts, keys, nkeys));
+        auto r = matmul_col_colT(ctx, ptrs(a), ptrs(b), p, view(rk), gkeys(elts, keys, nkeys), nthreads);
         for (u64 i = 0; i < p; ++i) out_ct(r[i], out + i);
     });
 }

@@ -208,6 +208,15 @@ class Oracle:
                                  C.c_double(scale), C.c_uint64(seed), _p(out)))
         return Ct(out, float(scale))
 
+    def encrypt_many(self, sk, values, scale, level, seed0, nthreads=8):
+        """encode + encrypt each row of `values` (real slot vectors); row v uses seed0 + v (threaded)."""
+        v = np.ascontiguousarray(values, dtype=np.float64)
+        out = np.zeros((v.shape[0], 2, level, self.N), dtype=np.uint64)
+        _check(lib().orc_encrypt_many(self.h, _p(sk), v.ctypes.data_as(C.POINTER(C.c_double)), C.c_uint64(v.shape[1]),
+                                      C.c_uint64(v.shape[0]), C.c_double(scale), C.c_uint64(level), C.c_uint64(seed0),
+                                      C.c_int(nthreads), _p(out)))
+        return out
+
     def decrypt(self, sk, ct: Ct):
         out = np.zeros((ct.level, self.N), dtype=np.uint64)
         s = self._in(ct)
@@ -328,13 +337,24 @@ class Oracle:
                                          C.c_uint64(len(A) if j_end is None else j_end), C.c_int(int(finish))))
         return self._outs(outs, len(X))
 
-    def matmul_col_colT(self, A, B, p, rk, gk):
+    def matmul_diag_col_set(self, A, js, X, rk, gk, nthreads=1, finish=False):
+        """he_linalg.cpp:977-997 restricted to the diagonals js (A[k] is diagonal js[k])."""
+        a, ab = self._many(A)
+        x, xb = self._many(X)
+        jj = np.ascontiguousarray(np.array(js, dtype=np.uint64))
+        lvl = X[0].level
+        outs, ob = self._many([Ct(np.zeros((3, lvl, self.N), np.uint64), 1.0) for _ in X])
+        _check(lib().orc_matmul_diag_col_set(self.h, a, _p(jj), C.c_uint64(len(js)), x, C.c_uint64(len(X)), _p(rk),
+                                             *self._gk(gk), outs, C.c_int(nthreads), C.c_int(int(finish))))
+        return self._outs(outs, len(X))
+
+    def matmul_col_colT(self, A, B, p, rk, gk, nthreads=1):
         a, ab = self._many(A)
         b, bb = self._many(B)
         lvl = A[0].level
         outs, ob = self._many([Ct(np.zeros((3, lvl, self.N), np.uint64), 1.0) for _ in range(p)])
         _check(lib().orc_matmul_col_colT(self.h, a, C.c_uint64(len(A)), b, C.c_uint64(p), _p(rk),
-                                         *self._gk(gk), outs))
+                                         *self._gk(gk), outs, C.c_int(nthreads)))
         return self._outs(outs, p)
 
     def matrix_matmul(self, A, ar, ac, atr, B, br, bc, btr, rk):

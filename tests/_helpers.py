@@ -105,3 +105,64 @@ def diag_vectors(M, slots):
 def col_vector(x, slots):
     n = len(x)
     return np.array([x[r % n] for r in range(slots)])
+
+
+def rotation_seq(N, j):
+    """SEAL's key-switch sequence for rot(x, j) under the default Galois keys (rotate_internal: one key
+    for j = 2^i, else the NAF terms least significant first, +-N/2 skipped), as step amounts."""
+    if j & (j - 1) == 0:
+        return [j]
+    res, v, i = [], j, 0
+    while v:
+        z = (2 - (v & 3)) if v & 1 else 0
+        v = (v - z) >> 1
+        if z and abs(z << i) != N // 2:
+            res.append(z << i)
+        i += 1
+    return res
+
+
+def trie_subset(N, n, target=64, seed=0):
+    """A subset of the diagonals [0, n) whose rotation prefix trie exercises every shape of the full
+    one (the engine's RotTrie / walk_trie_hoisted): all children of the root (the largest hoisted node),
+    the depth-1 node with the most children (hoisted groups split at HOIST_GROUP below the root too),
+    the deepest NAF chains with a terminal at every depth along them, j = 0 (the no-rotation term),
+    then random diagonals up to `target`."""
+    seqs = {j: tuple(rotation_seq(N, j)) for j in range(1, n)}
+    pick = {0}
+    first = {}
+    for j, s in seqs.items():
+        first.setdefault(s[0], j)
+    pick |= set(first.values())
+    depth = max(len(s) for s in seqs.values())
+    deep = [j for j, s in seqs.items() if len(s) == depth]
+    for j in (deep[0], deep[len(deep) // 3], deep[2 * len(deep) // 3], deep[-1]):
+        pick.add(j)
+        s = seqs[j]
+        for k in range(1, len(s)):  # terminals along the chain: positive prefix sums whose sequence is the prefix
+            v = sum(s[:k])
+            if 0 < v < n and seqs[v] == s[:k]:
+                pick.add(v)
+    kids = {}
+    for j, s in seqs.items():
+        if len(s) >= 2:
+            kids.setdefault(s[:1], {}).setdefault(s[:2], j)
+    busiest = max(kids.values(), key=len)
+    pick |= set(busiest.values())
+    rng = np.random.default_rng(seed)
+    rest = [j for j in range(1, n) if j not in pick]
+    extra = max(0, target - len(pick))
+    pick |= set(int(x) for x in rng.choice(rest, extra, replace=False))
+    return sorted(pick)
+
+
+def subset_trie_shape(N, js):
+    """(children of the root, max children of any node, depth, key switches SEAL runs per vector)."""
+    kids = {(): set()}
+    for j in js:
+        s = tuple(rotation_seq(N, j)) if j else ()
+        for k in range(len(s)):
+            kids.setdefault(s[:k], set()).add(s[:k + 1])
+            kids.setdefault(s[:k + 1], set())
+    return (len(kids[()]), max(len(v) for v in kids.values()), max(len(k) for k in kids),
+            sum(len(rotation_seq(N, j)) for j in js if j))

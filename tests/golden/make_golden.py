@@ -9,7 +9,12 @@ cfg1 mirrors the reference demo `demo matrix_operations batched_matmul_ckks` wit
 scale 2^40, 64x64 data  mat1[c][r] = 2 + 64c + (r mod 64)  (:1079-1087), the same 64 column
 ciphertexts used as A's diagonals and as B's columns (:1129-1131), out = A.matmul(eval, rk, gk, B).
 
-Usage: python tests/golden/make_golden.py [--threads 8]
+cfg1_colcolT is the reference's compiled default, COL_OR_DIAG = 0 (:1123-1128): the same 64 column
+ciphertexts as a col-batched A, B = A^T (a transposed copy), out = A.matmul(eval, rk, gk, B), i.e. the
+col x col^T branch of he_linalg.cpp:977-1002: out[i] = rescale(relin(sum_j rot(A[j], i) (*) A[j])), the i-th
+diagonal of A.A^T.
+
+Usage: python tests/golden/make_golden.py [--threads 8] [--only cfg1_colcolT]
 """
 import argparse
 import hashlib
@@ -60,11 +65,40 @@ def cfg1_expected_plain(n, slots):
             for i in range(n)]
 
 
+def cfg1_colcolT_expected_plain(n):
+    """Plaintext value of out[i] slot r (r < n): sum_j col_j[(r+i) mod n] * col_j[r] = (A A^T)[r][(r+i) mod n]."""
+    col = lambda c, r: 2 + n * c + (r % n)  # noqa: E731
+    return [np.array([sum(col(j, r + i) * col(j, r) for j in range(n)) for r in range(n)], dtype=np.float64)
+            for i in range(n)]
+
+
+def make_colcolT(orc, threads):
+    o, m, sk, rk, gk, cts = cfg1_inputs(orc)
+    outs = o.matmul_col_colT(cts, cts, CFG1["n"], rk, gk, nthreads=threads)
+    exp = cfg1_colcolT_expected_plain(CFG1["n"])
+    for i in (0, 1, 33, 63):
+        d = o.decode(o.decrypt(sk, outs[i]), outs[i].scale).real[: CFG1["n"]]
+        err = np.max(np.abs(d - exp[i]) / np.abs(exp[i]))
+        assert err < 1e-6, (i, err)
+    fx = dict(CFG1)
+    fx.update(moduli=[int(x) for x in m], form="COL_OR_DIAG=0: col(A) x col(A)^T -> diag output",
+              input_sha256=[sha(c.data, c.scale) for c in cts],
+              output_sha256=[sha(c.data, c.scale) for c in outs],
+              output_level=outs[0].level, output_scale=outs[0].scale)
+    with open(os.path.join(HERE, "cfg1_colcolT.json"), "w") as f:
+        json.dump(fx, f, indent=1)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--threads", type=int, default=8)
+    ap.add_argument("--only", default=None)
     args = ap.parse_args()
     orc = load_oracle()
+    if args.only == "cfg1_colcolT":
+        make_colcolT(orc, args.threads)
+        return
+    make_colcolT(orc, args.threads)
     o, m, sk, rk, gk, cts = cfg1_inputs(orc)
     outs = o.matmul_diag_col(cts, cts, rk, gk, nthreads=args.threads)
     fx = dict(CFG1)

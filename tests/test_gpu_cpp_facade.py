@@ -70,6 +70,17 @@ def test_demo_batched_diag_matches_golden(demo, orc, tmp_path):
     assert [sha(d, sc) for d, sc in out] == fx["output_sha256"]
 
 
+def test_demo_batched_col_matches_golden(demo, orc, tmp_path):
+    """The reference's compiled default (COL_OR_DIAG = 0, matrix_operations.cpp:1123-1128) through the C++
+    drop-in: col-batched A, B = A^T, A.matmul(eval, rk, gk, B) -> the golden col x col^T hashes."""
+    sys.path.insert(0, GOLD)
+    from make_golden import cfg1_inputs, sha
+    fx = json.load(open(os.path.join(GOLD, "cfg1_colcolT.json")))
+    o, m, sk, rk, gk, cts = cfg1_inputs(orc)
+    out = run(demo, "batched_col", tmp_path, fx["N"], m, cts, rk, gk)
+    assert [sha(d, sc) for d, sc in out] == fx["output_sha256"]
+
+
 @pytest.fixture(scope="module")
 def small(orc):
     N = 1 << 11

@@ -99,6 +99,22 @@ def test_ntt_cfg2_golden(orc, hecdna):
     assert [sha(out[i]) for i in range(len(m))] == fx["forward_sha256"]
 
 
+def test_dyadic_multiply_cfg2(orc, hecdna):
+    """BASELINE cfg2 primitive: dyadic_product_coeffmod over u64[npolys][10][2^15] (the 10 data primes of
+    {60, 40 x 9, 60}) through hec_dyadic_multiply, and at a limb offset; equal to (a * b) mod q_i."""
+    N = 1 << 15
+    m = orc.Oracle.create_coeff_modulus(N, [60] + [40] * 9 + [60])
+    ctx = hecdna.Context(N, m)
+    rng = np.random.default_rng(15)
+    a = np.stack([np.stack([rng.integers(0, q, N, dtype=np.uint64) for q in m[:10]]) for _ in range(3)])
+    b = np.stack([np.stack([rng.integers(0, q, N, dtype=np.uint64) for q in m[:10]]) for _ in range(3)])
+    q = np.array(m[:10], dtype=object).reshape(1, 10, 1)
+    exp = (a.astype(object) * b.astype(object) % q).astype(np.uint64)
+    assert np.array_equal(ctx.dyadic_multiply(a, b), exp)
+    sub_a, sub_b = np.ascontiguousarray(a[:, 4:]), np.ascontiguousarray(b[:, 4:])
+    assert np.array_equal(ctx.dyadic_multiply(sub_a, sub_b, limb0=4), exp[:, 4:])
+
+
 # ------------------------------------------------------------------------------- ops -----
 def test_add_sub_negate(env11):
     e = env11
@@ -197,6 +213,21 @@ def test_matvec_cfg1_golden(orc, hecdna):
     out = ctx.matmul_diag_col(g, g, ctx.relin_key(rk), ctx.galois_keys(gk))
     hashes = [gsha(x.download(), x.scale) for x in out]
     assert hashes == fx["output_sha256"]
+
+
+def test_matmul_col_colT_cfg1_golden(orc, hecdna):
+    """The reference demo's compiled default, COL_OR_DIAG = 0 (matrix_operations.cpp:1123-1128): col-batched A
+    times B = A^T, i.e. out[i] = sum_j rot(A[j], i) (*) A[j] on the 64x64 cfg1 data; all 64 diagonal outputs
+    byte-identical to the golden hashes."""
+    import sys
+    sys.path.insert(0, GOLD)
+    from make_golden import cfg1_inputs, sha as gsha
+    fx = json.load(open(os.path.join(GOLD, "cfg1_colcolT.json")))
+    o, m, sk, rk, gk, cts = cfg1_inputs(orc)
+    ctx = hecdna.Context(fx["N"], m)
+    g = [ctx.ciphertext(c.data, c.scale) for c in cts]
+    out = ctx.matmul_col_colT(g, g, fx["n"], ctx.relin_key(rk), ctx.galois_keys(gk))
+    assert [gsha(x.download(), x.scale) for x in out] == fx["output_sha256"]
 
 
 def test_matvec_batched_equals_single_and_oracle(env11):
