@@ -22,6 +22,15 @@ pytestmark = pytest.mark.gpu
 THREADS = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)))
 
 
+@pytest.fixture(scope="module")
+def env15(orc, hecdna):
+    """BASELINE cfg3 parameters, N = 2^15, {60, 40 x 9, 60}, the 29 default Galois keys."""
+    from test_gpu_parity import Env
+    e = Env(orc, hecdna, 1 << 15, [60] + [40] * 9 + [60], seed=3131)
+    assert len(e.elts) == 29
+    return e
+
+
 def _place(e, js, cts, n):
     """n diagonal handles with the subset's ciphertexts at their indices (the rest are never read)."""
     g = [e.up(c) for c in cts]
