@@ -54,10 +54,12 @@ def algorithmic_bytes_per_matvec(N, l, n, B, ks):
 
 def pmc_traffic(kernel, B, logn, level, n):
     """HBM bytes per launch of the roofline kernel from the committed rocprofv3 PMC passes
-    (profiles/r01_pmc_<kernel>_B<B>.json, written by tools/pmc_summary.py: FETCH_SIZE and WRITE_SIZE in
+    (profiles/r02_pmc_<kernel>_B<B>.json, else r01_; written by tools/pmc_summary.py: FETCH_SIZE and WRITE_SIZE in
     separate passes, gfx950 FETCH x2 correction for 16-B/lane reads) when they were taken on this
     configuration; else None."""
-    path = os.path.join(ROOT, "profiles", f"r01_pmc_{kernel}_B{B}.json")
+    path = os.path.join(ROOT, "profiles", f"r02_pmc_{kernel}_B{B}.json")
+    if not os.path.exists(path):
+        path = os.path.join(ROOT, "profiles", f"r01_pmc_{kernel}_B{B}.json")
     if not os.path.exists(path):
         return None
     p = json.load(open(path))
@@ -66,9 +68,35 @@ def pmc_traffic(kernel, B, logn, level, n):
     return p["traffic_bytes_per_dispatch"]
 
 
+def cpu_info():
+    model = "unknown"
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                model = ln.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    share = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    # the GPU pool gives one GPU job a CPU share of OMP_NUM_THREADS cores (16) on a larger host: use all of
+    # that share; os.cpu_count() is the whole host
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    threads = min(share, omp) if omp > 0 else share
+    return model, os.cpu_count(), share, threads
+
+
 def cpu_baseline(N, moduli, n, sample_diags, threads):
-    """The oracle (C++ restatement of the reference's SEAL path, `port`) timed on this host on a bounded
-    sample: diagonals j in [0, sample_diags) of one matvec, extrapolated by key-switch count."""
+    """The oracle (the C++ restatement of the reference's SEAL path, kind "port"), built here with
+    -march=native, timed on this host:
+      all cores: ONE FULL matvec (all n diagonals, SEAL's per-rotation key switches, relinearize + rescale)
+                 on `threads` threads (parallel over diagonal ranges, bit-identical partial sums);
+      1 core:    the first `sample_diags` diagonals, extrapolated by key-switch count (labelled as such:
+                 a full 1-core cfg3 matvec takes ~15 minutes)."""
+    import subprocess
+    import tempfile
+    build = tempfile.mkdtemp(prefix="orc_native_")
+    subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "native", f"OUT={build}"])
+    os.environ["HEC_ORACLE_LIB"] = os.path.join(build, "liboracle_native.so")
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle_py as orc
     o = orc.Oracle(N, moduli)
@@ -86,18 +114,14 @@ def cpu_baseline(N, moduli, n, sample_diags, threads):
         return k
     elts = o.default_galois_elts()
     gk = {e: rnd_key() for e in elts}
-    A = [rnd_ct() for _ in range(sample_diags)]
+    rk = rnd_key()
+    A = [rnd_ct() for _ in range(8)]   # n diagonals cycle over 8 distinct ciphertexts (data-oblivious timing)
     X = [rnd_ct()]
     from _helpers import ks_count
     ks_sample = ks_count(N, sample_diags)
-    res = {}
-    for th in (1, threads):
-        t0 = time.perf_counter()
-        # finish=False: the sample times rotations + tensors; rk is unused (any key array passes)
-        o.matmul_diag_col(A, X, gk[elts[0]], gk, nthreads=th, j_begin=0, j_end=sample_diags, finish=False)
-        dt = time.perf_counter() - t0
-        res[th] = dt * ks_total(N, n) / ks_sample  # seconds per full matvec
-    return res, ks_sample
+    full = o.bench_matvec(A, n, X, rk, gk, nthreads=threads)
+    one = o.bench_matvec(A, n, X, rk, gk, nthreads=1, j_end=sample_diags, finish=False)
+    return {"full_s": full, "one_core_s": one * ks_total(N, n) / ks_sample, "ks_sample": ks_sample}
 
 
 def main():
@@ -216,6 +240,7 @@ def main():
     breakdown = {}
     classes = ("ks_intt", "ks_modup", "ks_mac", "ks_modup_a", "ks_bmac", "ks_modup_h", "ks_hmac", "ks_moddown",
                "galois", "tensor", "relin", "rescale")
+    prof_classes, prof_ex = [], {}
     if not args.no_profile:
         ctx.profile(2)
         step()
@@ -224,49 +249,57 @@ def main():
             ms, cnt = ctx.profile_read(cls)
             if cnt:
                 breakdown[cls] = {"ms": round(ms, 3), "launch_groups": cnt}
+        prof_classes = ctx.profile_classes()
+        prof_ex = {c: ctx.profile_read_ex(c) for c in prof_classes}
         ctx.profile(0)
 
-    # roofline of the dominant single-kernel phase: its algorithmic bytes (compulsory reads + writes,
-    # SURVEY §8(d) units: limb = N*8 B, B targets, level l, K = l+1 key moduli) / its measured time.
-    #   ks_hmac = k_hmacm, the hoisted key MAC of a group of sibling rotations: per launch
-    #     the node's digits E (B l^2 limbs) + its c1 (B l), and per child the key (2 l K), the sign-mask
-    #     NTTs W (K) and the ACC output (2 B K); summed over the phase's launches and children
-    #   ks_bmac = k_bmac, fused mod-up pass B + key MAC of one non-hoisted rotation
-    K = L + 1
-    limb = N * 8
-    Bt = args.batch
-    from _helpers import rotation_trie_stats
-    _, _, h_children, _ = rotation_trie_stats(N, args.n)
-    phases = {}
-    if "ks_hmac" in breakdown:
-        nl = breakdown["ks_hmac"]["launch_groups"]
-        phases["ks_hmac"] = ("k_hmacm", nl * Bt * (L * L + L) + h_children * (2 * L * K + K + 2 * Bt * K))
-    if "ks_bmac" in breakdown:
-        nl = breakdown["ks_bmac"]["launch_groups"]
-        phases["ks_bmac"] = ("k_bmac", nl * (Bt * L * L + Bt * L + 2 * L * K + 2 * Bt * K))
+    # per-kernel table and roofline.  Every kernel launch of the profile step sits in a "k:<kernel>/<role>"
+    # scope that carries its algorithmic bytes (compulsory reads + writes of that kernel given the engine's
+    # decomposition, SURVEY 8(d) units: limb = N*8 B, B targets, level l, K = l+1 key moduli):
+    # achieved GB/s = bytes / event-timed ms.  The roofline line reports the kernel with the most GPU time.
+    kernels = {}
     roof = None
-    if phases:
-        dom = max(phases, key=lambda c: breakdown[c]["ms"])
-        kern, limbs = phases[dom]
-        bm = breakdown[dom]
-        per = bm["ms"] / bm["launch_groups"]
-        algo = limbs * limb / bm["launch_groups"]
-        ach = algo / (per * 1e-3) / 1e9
-        roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(ach / HBM_PEAK_GBS, 4),
-                "traffic": pmc_traffic(kern, args.batch, args.logn, L, args.n),
-                "kernel": kern, "avg_ms": round(per, 4), "algorithmic_bytes_per_launch": int(algo),
-                "launches_per_step": bm["launch_groups"]}
+    if not args.no_profile:
+        for cls in prof_classes:
+            if not cls.startswith("k:"):
+                continue
+            ms, scopes, nbytes, kl = prof_ex[cls]
+            kern, _, role = cls[2:].partition("/")
+            k = kernels.setdefault(kern, {"ms": 0.0, "launches": 0, "bytes": 0.0, "roles": {}})
+            k["ms"] += ms
+            k["launches"] += kl
+            k["bytes"] += nbytes
+            k["roles"][role or kern] = {"ms": round(ms, 3), "launches": kl,
+                                        "GBps": round(nbytes / (ms * 1e-3) / 1e9, 1) if ms else None}
+        for kern, k in kernels.items():
+            k["GBps"] = round(k["bytes"] / (k["ms"] * 1e-3) / 1e9, 1) if k["ms"] else None
+            k["frac"] = round(k["GBps"] / HBM_PEAK_GBS, 4) if k["GBps"] else None
+            k["ms"] = round(k["ms"], 3)
+            k["bytes_per_launch"] = int(k["bytes"] / max(1, k["launches"]))
+            del k["bytes"]
+        if kernels:
+            kern = max(kernels, key=lambda x: kernels[x]["ms"])
+            k = kernels[kern]
+            per = k["ms"] / k["launches"]
+            roof = {"bound": "hbm", "achieved": k["GBps"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": k["frac"], "traffic": pmc_traffic(kern, args.batch, args.logn, L, args.n),
+                    "kernel": kern, "avg_ms": round(per, 4), "algorithmic_bytes_per_launch": k["bytes_per_launch"],
+                    "launches_per_step": k["launches"],
+                    "share_of_step_gpu_time": round(k["ms"] / sum(v["ms"] for v in kernels.values()), 3)}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not ctpt:
-        threads = min(16, os.cpu_count() or 1)
-        res, ks_s = cpu_baseline(N, moduli, args.n, args.cpu_sample_diags, threads)
-        cpu = {"value": round(1.0 / res[1], 6), "unit": "matvec/s", "cores": 1, "kind": "port",
-               "sample": f"oracle (C++ SEAL-semantics port) diagonals j<{args.cpu_sample_diags} of one "
-                         f"N=2^{args.logn} L={L} matvec ({ks_s} key switches), extrapolated to the "
-                         f"{ks} key switches of the n={args.n} matvec",
-               "all_cores": {"value": round(1.0 / res[threads], 6), "cores": threads}}
+        model, host_cpus, share, threads = cpu_info()
+        res = cpu_baseline(N, moduli, args.n, args.cpu_sample_diags, threads)
+        cpu = {"value": round(1.0 / res["full_s"], 6), "unit": "matvec/s", "cores": threads, "kind": "port",
+               "sample": f"one full n={args.n} N=2^{args.logn} L={L} diag x col matvec ({ks} key switches, SEAL's "
+                         f"per-rotation schedule, relinearize + rescale) by the oracle (C++ SEAL-semantics port, "
+                         f"-march=native) on {threads} threads",
+               "cpu_model": model, "host_cpus": host_cpus, "cpus_available": share,
+               "full_matvec_s": round(res["full_s"], 2),
+               "one_core": {"value": round(1.0 / res["one_core_s"], 6), "cores": 1, "extrapolated": True,
+                            "sample": f"diagonals j<{args.cpu_sample_diags} ({res['ks_sample']} key switches) "
+                                      f"on 1 thread, scaled to {ks} key switches"}}
 
     algo_mv = algorithmic_bytes_per_matvec(N, L, args.n, args.batch, ks)
     if rank == 0:
@@ -284,8 +317,12 @@ def main():
                        "parallelism": (f"sharded{world}: diagonals split by rotation-trie subtrees, one RCCL "
                                        f"reduce-scatter of size-3 partials" if sharded else
                                        f"replicated matrix+keys, dp{world} over input vectors"),
-                       "batch_global": args.batch * (1 if sharded else world)},
+                       "batch_global": args.batch * (1 if sharded else world),
+                       "precomputed_untimed": "per-Galois-key tables of the hoisted MAC (sign-mask NTTs W and "
+                                              "key sums KW, galois_negw / galois_kw) are built once per key "
+                                              "and level before the timed steps, like the keys themselves"},
             "roofline": roof,
+            "kernels_one_step": kernels,
             "cpu_baseline": cpu,
             "whole_step_algorithmic_GBps": round(algo_mv * total / dt / 1e9, 2),
             "breakdown_ms_one_step": breakdown,

@@ -114,6 +114,8 @@ def lib():
             "hec_time_ntt_forward": [vp, vp, C.c_uint64, C.c_uint64, C.c_int, C.POINTER(C.c_double)],
             "hec_profile_enable": [vp, C.c_int],
             "hec_profile_read": [vp, C.c_char_p, C.POINTER(C.c_double), u64p],
+            "hec_profile_read_ex": [vp, C.c_char_p, C.POINTER(C.c_double), u64p, C.POINTER(C.c_double), u64p],
+            "hec_profile_classes": [vp, C.c_char_p, C.c_uint64],
             "hec_create_coeff_modulus": [C.c_uint64, C.POINTER(C.c_int), C.c_uint64, u64p],
         }
         for name, args in sig.items():
@@ -126,6 +128,7 @@ def lib():
         L.hec_default_galois_elts.restype = C.c_uint64
         L.hec_galois_keys_has.argtypes = [vp, C.c_uint32]
         L.hec_galois_keys_has.restype = C.c_int
+        L.hec_profile_classes.restype = C.c_uint64
         _lib = L
     return _lib
 
@@ -366,6 +369,18 @@ class Context:
         n = C.c_uint64()
         _check(lib().hec_profile_read(self.h, cls.encode(), C.byref(ms), C.byref(n)))
         return ms.value, n.value
+
+    def profile_read_ex(self, cls):
+        """(ms, scopes, algorithmic bytes, kernel launches) of one profile class."""
+        ms, n, b, kl = C.c_double(), C.c_uint64(), C.c_double(), C.c_uint64()
+        _check(lib().hec_profile_read_ex(self.h, cls.encode(), C.byref(ms), C.byref(n), C.byref(b), C.byref(kl)))
+        return ms.value, n.value, b.value, kl.value
+
+    def profile_classes(self):
+        need = lib().hec_profile_classes(self.h, None, 0)
+        buf = C.create_string_buffer(int(need))
+        lib().hec_profile_classes(self.h, buf, need)
+        return [x for x in buf.value.decode().split("\n") if x]
 
 
 class DeviceBuffer:

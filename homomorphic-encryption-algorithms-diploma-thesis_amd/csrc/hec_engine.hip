@@ -257,6 +257,8 @@ struct Scratch {
 struct ProfScope {
     Ctx &c;
     const char *name;
+    double bytes = 0;
+    int kl = 1;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     hipEvent_t pool_event()
     {
@@ -267,7 +269,8 @@ struct ProfScope {
         }
         return c.ev_pool[c.ev_used++];
     }
-    ProfScope(Ctx &cc, const char *n) : c(cc), name(n)
+    ProfScope(Ctx &cc, const char *n, double limbs = 0, int launches = 1)
+        : c(cc), name(n), bytes(limbs * 8.0 * (double)cc.N), kl(launches)
     {
         if (!c.prof_mode) return;
         if (c.prof_mode == 2) {
@@ -284,7 +287,7 @@ struct ProfScope {
         if (!c.prof_mode || !e0) return;
         (void)hipEventRecord(e1, c.stream);
         if (c.prof_mode == 2) {
-            c.prof_pend.push_back({name, e0, e1});
+            c.prof_pend.push_back({name, e0, e1, bytes, kl});
             return;
         }
         (void)hipEventSynchronize(e1);
@@ -293,6 +296,8 @@ struct ProfScope {
         auto &r = c.prof_tab[name];
         r.ms += ms;
         r.n += 1;
+        r.bytes += bytes;
+        r.kl += kl;
         (void)hipEventDestroy(e0);
         (void)hipEventDestroy(e1);
     }
@@ -307,6 +312,8 @@ void prof_resolve(Ctx &c)
         auto &r = c.prof_tab[p.name];
         r.ms += ms;
         r.n += 1;
+        r.bytes += p.bytes;
+        r.kl += p.kl;
     }
     c.prof_pend.clear();
     c.ev_used = 0;
@@ -326,10 +333,19 @@ void moddown(Ctx &c, u64 *ACC, u64 *Z, PolyArr IN, int in_nk, PolyArr OUT, int B
     const bool fan = c.fan_out;
     ProfScope ps(c, "ks_moddown");
     const int pP[1] = {(int)c.K - 1};
-    ntt_strided(c, true, ACC + l * N, (l + 1) * N, ACC + l * N, (l + 1) * N, 1, pP, 2 * B, 1, fan ? 1 : 3);
-    if (fan) fan_divide_round(c, ACC + l * N, 2 * (l + 1) * N, (l + 1) * N, Z, B, 2, l, (int)c.K - 1);
-    divide_round(c, ACC + l * N, 2 * (l + 1) * N, (l + 1) * N, PolyArr{ACC, 2 * (l + 1) * N, (l + 1) * N}, IN, in_nk,
-                 OUT, B, 2, l, (int)c.K - 1, c.p_inv.data(), c.p_inv_q.data(), Z, elt, fan ? 2 : 3);
+    {  // P limbs of both key polys: read + write 2B limbs per pass
+        ProfScope k(c, fan ? "k:k_ntt/moddown_intt" : "k:k_ntt/moddown_intt2", 4.0 * B, fan ? 1 : 2);
+        ntt_strided(c, true, ACC + l * N, (l + 1) * N, ACC + l * N, (l + 1) * N, 1, pP, 2 * B, 1, fan ? 1 : 3);
+    }
+    if (fan) {  // 2B P limbs -> 2B l rounding limbs (pass-A domain)
+        ProfScope k(c, "k:k_fan/moddown", 2.0 * B * (l + 1));
+        fan_divide_round(c, ACC + l * N, 2 * (l + 1) * N, (l + 1) * N, Z, B, 2, l, (int)c.K - 1);
+    }
+    {  // Z (2Bl), ACC data limbs (2Bl), IN (in_nk B l), OUT (2Bl)
+        ProfScope k(c, fan ? "k:k_ntt/divround_b" : "k:k_ntt/divround2", (6.0 + in_nk) * B * l, fan ? 1 : 2);
+        divide_round(c, ACC + l * N, 2 * (l + 1) * N, (l + 1) * N, PolyArr{ACC, 2 * (l + 1) * N, (l + 1) * N}, IN,
+                     in_nk, OUT, B, 2, l, (int)c.K - 1, c.p_inv.data(), c.p_inv_q.data(), Z, elt, fan ? 2 : 3);
+    }
 }
 
 // The mod-downs of ng sibling rotations of one node at once: ACC[q] = ACC + q B 2 (l+1) N (contiguous), IN the
@@ -344,12 +360,20 @@ void moddown_group(Ctx &c, u64 *ACC, u64 *Z, PolyArr IN, const PolyArr *OUT, con
     }
     ProfScope ps(c, "ks_moddown");
     const int pP[1] = {(int)c.K - 1};
-    ntt_strided(c, true, ACC + l * N, (l + 1) * N, ACC + l * N, (l + 1) * N, 1, pP, 2 * B * ng, 1, 1);
-    fan_divide_round(c, ACC + l * N, 2 * (l + 1) * N, (l + 1) * N, Z, B * ng, 2, l, (int)c.K - 1);
-    for (int q = 0; q < ng; ++q)
+    {
+        ProfScope k(c, "k:k_ntt/moddown_intt", 4.0 * B * ng);
+        ntt_strided(c, true, ACC + l * N, (l + 1) * N, ACC + l * N, (l + 1) * N, 1, pP, 2 * B * ng, 1, 1);
+    }
+    {
+        ProfScope k(c, "k:k_fan/moddown", 2.0 * B * ng * (l + 1));
+        fan_divide_round(c, ACC + l * N, 2 * (l + 1) * N, (l + 1) * N, Z, B * ng, 2, l, (int)c.K - 1);
+    }
+    for (int q = 0; q < ng; ++q) {
+        ProfScope k(c, "k:k_ntt/divround_b", 7.0 * B * l);
         divide_round(c, ACC + q * sacc + l * N, 2 * (l + 1) * N, (l + 1) * N,
                      PolyArr{ACC + q * sacc, 2 * (l + 1) * N, (l + 1) * N}, IN, 1, OUT[q], B, 2, l, (int)c.K - 1,
                      c.p_inv.data(), c.p_inv_q.data(), Z + q * sz, elts[q], 2);
+    }
 }
 
 // T (the target polys) and IN (added to the output) are read through the Galois permutation of elt
@@ -364,18 +388,23 @@ void keyswitch(Ctx &c, Scratch &s, PolyArr T, const u64 *key, PolyArr IN, int in
     int pmap[HEC_MAXL + 1];
     for (int i = 0; i <= HEC_MAXL; ++i) pmap[i] = i;
     const bool fan = c.fan_out && c.fused_modup_mac;
+    const double K = l + 1;
     {
         ProfScope ps(c, "ks_intt");  // with fan-out only its first pass; the fan kernel finishes it
+        ProfScope k(c, fan ? "k:k_ntt/intt_b" : "k:k_ntt/intt2", 2.0 * B * l, fan ? 1 : 2);
         ntt_strided(c, true, T.p, T.sb, D, l * N, l, pmap, B * l, elt, fan ? 1 : 3);
     }
     if (c.fused_modup_mac) {  // mod-up pass A, then pass B fused with the key MAC (no E round trip)
         {
             ProfScope ps(c, "ks_modup_a");
+            ProfScope k(c, fan ? "k:k_fan/modup" : "k:k_ntt/modup_a", (double)B * l * (l + 1), 1);
             if (fan) fan_modup(c, D, E, B, l);
             else ks_modup_mac(c, D, E, T, key, ACC, B, l, 1, elt);
         }
-        {
+        {  // digits E (B l^2) + the I == J targets (B l) + key (2 l K) -> ACC (2 B K)
             ProfScope ps(c, "ks_bmac");
+            ProfScope k(c, "k:k_bmac", (double)B * l * l + (double)B * l + 2.0 * l * K + 2.0 * B * K,
+                        c.split_classes ? 2 : 1);
             ks_modup_mac(c, D, E, T, key, ACC, B, l, 2, elt);
         }
     } else {
@@ -422,11 +451,23 @@ void hoist_node(Ctx &c, PolyArr X, int B, int l, const Hoist &h)
     for (int i = 0; i <= HEC_MAXL; ++i) pmap[i] = i;
     {
         ProfScope ps(c, "ks_intt");
-        ntt_strided(c, true, X.p + X.sk, X.sb, h.D, l * N, l, pmap, B * l);
+        {
+            ProfScope k(c, "k:k_ntt/intt_b", 2.0 * B * l);
+            ntt_strided(c, true, X.p + X.sk, X.sb, h.D, l * N, l, pmap, B * l, 1, 1);
+        }
+        {
+            ProfScope k(c, "k:k_ntt/intt_a", 2.0 * B * l);
+            ntt_strided(c, true, h.D, l * N, h.D, l * N, l, pmap, B * l, 1, 2);
+        }
+        ProfScope k(c, "k:k_zscan", (double)B * l);
         zero_scan(c, h.D, B * l, h.zl);
     }
     ProfScope ps(c, "ks_modup_h");
-    fan_modup(c, h.D, h.E, B, l, true);  // pass A of every NTT_I(D_J mod q_I), from the canonical D
+    {
+        ProfScope k(c, "k:k_fan/hoist", (double)B * l * (l + 1));
+        fan_modup(c, h.D, h.E, B, l, true);  // pass A of every NTT_I(D_J mod q_I), from the canonical D
+    }
+    ProfScope k(c, "k:k_ntt/modup_h_b", 2.0 * B * l * l);
     ks_modup(c, h.D, h.E, B, l, 2);      // pass B, canonical NTT-form digits
 }
 // one child of a hoisted node: OUT = key switch of apply_galois(X, elt) (X: the node's ciphertexts)
@@ -649,9 +690,11 @@ void walk_trie_hoisted(Ctx &c, Scratch &s, const RotTrie &t, int node, PolyArr s
                                  galois_kw(ctx, gk, e, l)};
         }
         for (int q0 = 0; q0 < ng; q0 += (int)grp) {  // one profile scope per launch (bench.py's roofline)
+            const int nk = std::min((int)grp, ng - q0);
+            const double K = l + 1;  // digits E (B l^2) + c1 (B l); per child key (2 l K), W (K), KW (2 K), ACC (2 B K)
             ProfScope ps(c, "ks_hmac");
-            hoisted_mac_multi(c, PolyArr{src.p + src.sk, src.sb, 0}, h.E, h.zl, kids + q0,
-                              std::min((int)grp, ng - q0), B, l);
+            ProfScope k(c, "k:k_hmacm", (double)B * (l * l + l) + nk * (2.0 * l * K + 3.0 * K + 2.0 * B * K));
+            hoisted_mac_multi(c, PolyArr{src.p + src.sk, src.sb, 0}, h.E, h.zl, kids + q0, nk, B, l);
         }
         if ((int)bufs.b[depth + 1].size() < ng) {  // too few rotation buffers to hold the group at once
             for (int q = 0; q < ng; ++q) {
@@ -779,6 +822,9 @@ void matvec_core(hec_context *ctx, const hec_ciphertext *const *diags, const hec
     auto flush = [&] {
         if (tb.T == 0) return;
         ProfScope pr(c, "tensor");
+        // T rotated inputs (2 B l each) + T diagonals (2 l, or l plaintext) + ACC read (unless first) + write
+        const double accl = (pt ? 2.0 : 3.0) * p * l;
+        ProfScope k(c, "k:k_tensor_multi", tb.T * (2.0 * p * l + (pt ? 1.0 : 2.0) * l) + (first ? 1 : 2) * accl);
         tensor_multi(c, tb, S2, l * N, l * N, Aa, (int)p, (int)l, first, pt);
         first = false;
         tb.T = 0;
@@ -2117,6 +2163,39 @@ int hec_profile_enable(hec_context *ctx, int mode)
         c.prof_mode = mode;
         if (mode) c.prof_tab.clear();
     });
+}
+int hec_profile_read_ex(hec_context *ctx, const char *cls, double *total_ms, uint64_t *scopes, double *alg_bytes,
+                        uint64_t *kernel_launches)
+{
+    return guard([&] {
+        need(ctx && cls, "null");
+        set_device(ctx);
+        prof_resolve(ctx->c);
+        auto it = ctx->c.prof_tab.find(cls);
+        const bool has = it != ctx->c.prof_tab.end();
+        if (total_ms) *total_ms = has ? it->second.ms : 0;
+        if (scopes) *scopes = has ? it->second.n : 0;
+        if (alg_bytes) *alg_bytes = has ? it->second.bytes : 0;
+        if (kernel_launches) *kernel_launches = has ? it->second.kl : 0;
+    });
+}
+uint64_t hec_profile_classes(hec_context *ctx, char *buf, uint64_t cap)
+{
+    if (!ctx) return 0;
+    std::string all;
+    try {
+        set_device(ctx);
+        prof_resolve(ctx->c);
+    } catch (...) {
+        return 0;
+    }
+    for (const auto &kv : ctx->c.prof_tab) all += kv.first + "\n";
+    if (buf && cap) {
+        const std::size_t n = std::min<std::size_t>(all.size(), cap - 1);
+        std::memcpy(buf, all.data(), n);
+        buf[n] = 0;
+    }
+    return all.size() + 1;
 }
 int hec_profile_read(hec_context *ctx, const char *cls, double *total_ms, uint64_t *launches)
 {

@@ -94,9 +94,11 @@ struct Ctx {
     bool fused_modup_mac = true;  // HEC_FUSED_MODUP_MAC=0: separate mod-up pass B and key MAC kernels
     // profiling (ProfScope in hec_engine.hip)
     int prof_mode = 0;  // 0 off, 1 synchronous per scope, 2 asynchronous event pairs
-    struct ProfRec { double ms = 0; uint64_t n = 0; };
+    // a scope's algorithmic bytes (compulsory reads + writes of its kernels) and kernel launches, so
+    // per-kernel scopes ("k:<kernel>/<role>") give each kernel's achieved GB/s (bench.py roofline)
+    struct ProfRec { double ms = 0; uint64_t n = 0; double bytes = 0; uint64_t kl = 0; };
     std::map<std::string, ProfRec> prof_tab;
-    struct ProfPend { const char *name; hipEvent_t e0, e1; };
+    struct ProfPend { const char *name; hipEvent_t e0, e1; double bytes; int kl; };
     std::vector<ProfPend> prof_pend;
     std::vector<hipEvent_t> ev_pool;
     std::size_t ev_used = 0;

@@ -195,6 +195,14 @@ int hec_time_ntt_forward(hec_context *ctx, uint64_t *dev_data, uint64_t nlimbs, 
  * phase counts per class. */
 int hec_profile_enable(hec_context *ctx, int mode);
 int hec_profile_read(hec_context *ctx, const char *kernel_class, double *total_ms, uint64_t *launches);
+/* The same plus the class's algorithmic bytes (compulsory reads + writes of its kernels, summed over its
+ * scopes) and kernel launches.  Classes named "k:<kernel>/<role>" wrap single kernels (k_fan, k_ntt, k_bmac,
+ * k_hmacm, k_tensor_multi, k_zscan) inside the phases, so bytes / ms is that kernel's achieved GB/s. */
+int hec_profile_read_ex(hec_context *ctx, const char *kernel_class, double *total_ms, uint64_t *scopes,
+                        double *alg_bytes, uint64_t *kernel_launches);
+/* Newline-separated names of every class recorded since hec_profile_enable; returns the bytes needed
+ * (including the terminating NUL), writes at most cap bytes into buf when buf != NULL. */
+uint64_t hec_profile_classes(hec_context *ctx, char *buf, uint64_t cap);
 
 #ifdef __cplusplus
 }

@@ -1,6 +1,7 @@
 // ORACLE C API — test infrastructure only (see oracle.hpp).  Flat extern "C" entry points so
 // tests/ (ctypes) and bench.py's cpu_baseline leg can drive the CPU restatement.
 #include <atomic>
+#include <chrono>
 #include <cstring>
 #include <thread>
 #include <string>
@@ -317,6 +318,25 @@ int orc_matmul_diag_col_set(void *c, const OrcCt *A, const u64 *js, u64 nj, cons
         auto r = matmul_diag_col_set(ctx, ptrs(a), std::vector<std::size_t>(js, js + nj), ptrs(x), view(rk),
                                      gkeys(elts, keys, nkeys), nthreads, finish != 0);
         for (u64 i = 0; i < p; ++i) out_ct(r[i], out + i);
+    });
+}
+// CPU baseline (bench.py cpu_baseline leg): one full diag x col matvec (he_linalg.cpp:943-1006, relinearize +
+// rescale) of n diagonals over X, timed with steady_clock around the call as the reference's Timer does
+// (tic_toc.h:20-28).  The n diagonals cycle over the nA distinct ones given (every step is data-oblivious, so
+// the time equals that of n distinct ciphertexts without n copies in memory).  j range [j_begin, j_end).
+int orc_bench_matvec(void *c, const OrcCt *A, u64 nA, u64 n, const OrcCt *X, u64 p, const u64 *rk, const u32 *elts,
+                     const u64 *const *keys, u64 nkeys, int nthreads, u64 j_begin, u64 j_end, int finish,
+                     double *seconds)
+{
+    return guard([&] {
+        auto &ctx = *static_cast<Context *>(c);
+        auto a = in_many(ctx, A, nA), x = in_many(ctx, X, p);
+        std::vector<const Ciphertext *> diag(n);
+        for (u64 j = 0; j < n; ++j) diag[j] = &a[j % nA];
+        const auto gk = gkeys(elts, keys, nkeys);
+        const auto t0 = std::chrono::steady_clock::now();
+        auto r = matmul_diag_col(ctx, diag, ptrs(x), view(rk), gk, nthreads, j_begin, j_end, finish != 0);
+        *seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     });
 }
 int orc_matmul_col_colT(void *c, const OrcCt *A, u64 n, const OrcCt *B, u64 p, const u64 *rk, const u32 *elts,

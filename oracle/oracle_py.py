@@ -15,7 +15,8 @@ from dataclasses import dataclass
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_LIB_PATH = os.path.join(_HERE, "_build", "liboracle.so")
+# HEC_ORACLE_LIB: another build of the same sources (bench.py's cpu_baseline uses a -march=native build)
+_LIB_PATH = os.environ.get("HEC_ORACLE_LIB") or os.path.join(_HERE, "_build", "liboracle.so")
 _lib = None
 
 u64p = C.POINTER(C.c_uint64)
@@ -347,6 +348,17 @@ class Oracle:
         _check(lib().orc_matmul_diag_col_set(self.h, a, _p(jj), C.c_uint64(len(js)), x, C.c_uint64(len(X)), _p(rk),
                                              *self._gk(gk), outs, C.c_int(nthreads), C.c_int(int(finish))))
         return self._outs(outs, len(X))
+
+    def bench_matvec(self, A, n, X, rk, gk, nthreads=1, j_begin=0, j_end=None, finish=True):
+        """Seconds for one diag x col matvec of n diagonals (cycling over the distinct A) over X (C++ timer)."""
+        a, ab = self._many(A)
+        x, xb = self._many(X)
+        secs = C.c_double()
+        _check(lib().orc_bench_matvec(self.h, a, C.c_uint64(len(A)), C.c_uint64(n), x, C.c_uint64(len(X)), _p(rk),
+                                      *self._gk(gk), C.c_int(nthreads), C.c_uint64(j_begin),
+                                      C.c_uint64(n if j_end is None else j_end), C.c_int(int(finish)),
+                                      C.byref(secs)))
+        return secs.value
 
     def matmul_col_colT(self, A, B, p, rk, gk, nthreads=1):
         a, ab = self._many(A)
