@@ -609,12 +609,132 @@ __global__ void __launch_bounds__(NSEG *(1 << LOGP) / 16)
     }
 }
 
+// ------------------------------------------------------------------ register-direct fan-out (k_fan2)
+// The stages of one round on 16 register-resident elements: thread ts of a P = 2^LOGP point column holds the
+// elements ntt_round_g gives it for stages [S0, S1): v[gi 2^D + a] <-> x = xb(ts G + gi) | (a << (LOGP - S1)).
+// Round 0 (stages 0..3) owns x = ts + k TPS ("stride set"), round 1 (stages 4..LOGP-1) x = 16 ts + k ("block
+// set"), k = 0..15, TPS = P / 16.
+template <int LOGP, int S0, int S1, bool INV, bool FP, class TwG>
+__device__ __forceinline__ void ntt_round_r(u64 *v, int ts, const TwG &twg, const DevPrime &pr)
+{
+    constexpr int D = S1 - S0, G = 1 << (4 - D), NQ = 1 << D;
+    static_assert(D >= 1 && D <= 4, "round covers 1..4 stages");
+    const u64 q = pr.q, two_q = 2 * q;
+#pragma unroll
+    for (int gi = 0; gi < G; ++gi) {
+        const int g = ts * G + gi;
+        const int hi = g >> (LOGP - S1);
+#pragma unroll
+        for (int k = 0; k < D; ++k) {
+            const int st = INV ? D - 1 - k : k;
+            const int bit = 1 << (D - 1 - st);
+#pragma unroll
+            for (int a = 0; a < NQ; ++a) {
+                if (a & bit) continue;
+                const int m = a >> (D - st);
+                u64 &X = v[gi * NQ + a], &Y = v[gi * NQ + (a | bit)];
+                if constexpr (FP) {
+                    double x = __longlong_as_double((long long)X), y = __longlong_as_double((long long)Y);
+                    const double w = twg.f(S0 + st, (hi << st) | m);
+                    if constexpr (!INV) ct_bfly_fp(x, y, w, pr.qd, pr.qinv);
+                    else gs_bfly_fp(x, y, w, pr.qd, pr.qinv);
+                    X = (u64)__double_as_longlong(x);
+                    Y = (u64)__double_as_longlong(y);
+                } else {
+                    const ulonglong2 w = twg.w(S0 + st, (hi << st) | m);
+                    if constexpr (!INV) ct_bfly(X, Y, w.x, w.y, q, two_q);
+                    else gs_bfly(X, Y, w.x, w.y, q, two_q);
+                }
+            }
+        }
+    }
+}
+
+// k_fan with the NTT rounds on registers: the source is loaded straight into the thread's element set and
+// the target tiles are stored straight from it, so each transform (the INTT and every target's forward
+// pass) exchanges through LDS once instead of three times, with one barrier per exchange (two LDS tiles
+// alternate between consecutive exchanges).  Same inputs, outputs and intermediate formats as k_fan.
+template <int LOGP, int NSEG, class FAN>
+__global__ void __launch_bounds__(NSEG *(1 << LOGP) / 16)
+    k_fan2(const FAN fan, TwTables inv, TwTables fwd, const DevPrime *__restrict__ primes, int logN)
+{
+    constexpr int P = 1 << LOGP, TPS = P / 16, LD = NSEG + 1, TILE = P * LD;
+    __shared__ u64 lds[2 * TILE];
+    const int seg0 = blockIdx.x * NSEG, lc = logN - LOGP;
+    const int ts = threadIdx.x / NSEG, sg = threadIdx.x % NSEG;
+    auto gstride = [&](int k) { return ((u64)(ts + k * TPS) << lc) + seg0 + sg; };
+    auto gblock = [&](int k) { return ((u64)(16 * ts + k) << lc) + seg0 + sg; };
+    auto lstride = [&](int k) { return (ts + k * TPS) * LD + sg; };
+    auto lblock = [&](int k) { return (16 * ts + k) * LD + sg; };
+    auto twidx = [](int s, int i) -> u64 { return (1ull << s) + (u64)i; };
+    const auto src = fan.src(blockIdx.y);
+    const DevPrime ps = primes[src.prime];
+    int buf = 0;
+    u64 d[16];  // canonical coefficient-form values of the source, stride set
+    if constexpr (FAN::kDirect) {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) d[k] = src.in[gstride(k)];
+    } else {
+        u64 v[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) v[k] = src.in[gblock(k)];
+        const GlobalTw<decltype(twidx)> tg{twidx, inv.a + ((u64)src.prime << logN), inv.fa + ((u64)src.prime << logN)};
+        if (ps.fp) ntt_round_r<LOGP, 4, LOGP, true, true>(v, ts, tg, ps);
+        else ntt_round_r<LOGP, 4, LOGP, true, false>(v, ts, tg, ps);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) lds[lblock(k)] = v[k];
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < 16; ++k) v[k] = lds[lstride(k)];
+        buf = 1;
+        if (ps.fp) {
+            ntt_round_r<LOGP, 0, 4, true, true>(v, ts, tg, ps);
+#pragma unroll
+            for (int k = 0; k < 16; ++k)
+                d[k] = fp_canon(fp_mulmod(__longlong_as_double((long long)v[k]), ps.ninv_d, ps.qd, ps.qinv), ps.qd, ps.qinv);
+        } else {
+            ntt_round_r<LOGP, 0, 4, true, false>(v, ts, tg, ps);
+#pragma unroll
+            for (int k = 0; k < 16; ++k) d[k] = shoup(v[k], ps.ninv, ps.ninv_q, ps.q);
+        }
+    }
+    const int nt = fan.ntargets(), t0 = blockIdx.z * nt / gridDim.z, t1 = (blockIdx.z + 1) * nt / gridDim.z;
+    for (int t = t0; t < t1; ++t) {
+        const auto tgt = fan.tgt(blockIdx.y, t);
+        if (!tgt.valid) continue;
+        const DevPrime pt = primes[tgt.prime];
+        const GlobalTw<decltype(twidx)> tw{twidx, fwd.a + ((u64)tgt.prime << logN), fwd.fa + ((u64)tgt.prime << logN)};
+        u64 *tile = lds + buf * TILE;
+        buf ^= 1;
+        u64 v[16];
+        if (pt.fp) {
+#pragma unroll
+            for (int k = 0; k < 16; ++k) v[k] = (u64)__double_as_longlong(u2d(fan.xf(tgt, d[k])));
+            ntt_round_r<LOGP, 0, 4, false, true>(v, ts, tw, pt);
+        } else {
+#pragma unroll
+            for (int k = 0; k < 16; ++k) v[k] = fan.xf(tgt, d[k]);
+            ntt_round_r<LOGP, 0, 4, false, false>(v, ts, tw, pt);
+        }
+#pragma unroll
+        for (int k = 0; k < 16; ++k) tile[lstride(k)] = v[k];
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < 16; ++k) v[k] = tile[lblock(k)];
+        if (pt.fp) ntt_round_r<LOGP, 4, LOGP, false, true>(v, ts, tw, pt);
+        else ntt_round_r<LOGP, 4, LOGP, false, false>(v, ts, tw, pt);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) tgt.out[gblock(k)] = v[k];
+    }
+}
+
 template <int LOGR, int LOGC, int NA, class FAN>
 static void run_fan(Ctx &c, int njobs, const FAN &fan, int groups)
 {
     constexpr int R = 1 << LOGR, C = 1 << LOGC;
     const TwTables fwd{c.tw, c.twb, c.twf, c.twbf}, inv{c.itw, c.itwb, c.itwf, c.itwbf};
-    k_fan<LOGR, NA><<<dim3(C / NA, njobs, groups), NA * R / 16, 0, c.stream>>>(fan, inv, fwd, c.primes, c.logN);
+    if (c.fan2) k_fan2<LOGR, NA><<<dim3(C / NA, njobs, groups), NA * R / 16, 0, c.stream>>>(fan, inv, fwd, c.primes, c.logN);
+    else k_fan<LOGR, NA><<<dim3(C / NA, njobs, groups), NA * R / 16, 0, c.stream>>>(fan, inv, fwd, c.primes, c.logN);
     HEC_HIP(hipGetLastError());
 }
 template <class FAN>
