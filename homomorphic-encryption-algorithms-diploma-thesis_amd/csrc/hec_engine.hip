@@ -1061,6 +1061,7 @@ int hec_context_create(uint64_t N, const uint64_t *mod, uint64_t K, int device, 
         if (const char *f = std::getenv("HEC_FUSE_GALOIS")) c.fuse_galois = f[0] != '0';
         if (const char *f = std::getenv("HEC_FAN")) c.fan_out = f[0] != '0';
         if (const char *f = std::getenv("HEC_FAN2")) c.fan2 = f[0] != '0';
+        if (const char *f = std::getenv("HEC_TENSOR_BG")) c.tensor_bg = std::atoi(f);
         if (const char *f = std::getenv("HEC_LANES")) c.lanes = std::max(1, std::atoi(f));
         if (const char *f = std::getenv("HEC_FANG"))
             std::sscanf(f, "%d,%d,%d", &c.fan_groups_moddown, &c.fan_groups_modup, &c.fan_groups_hoist);

@@ -80,6 +80,7 @@ struct Ctx {
                                    // integer launches on one stream (1) or on two streams (2)
     int tensor_defer_max = 12;     // HEC_TENSOR_DEFER: terminals per deferred tensor batch (1 = immediate)
     int tensor_defer_bufs = 8;     // HEC_TENSOR_BUFS: rotation buffers per trie depth
+    int tensor_bg = 1;             // HEC_TENSOR_BG=0: k_tensor_multi (one thread per coefficient, whole batch)
     bool hoist = true;             // HEC_HOIST=0: no hoisted mod-up in the rotation trie walk
     int hoist_min_children = 2;
     int hmac_cfg = 3;              // HEC_HMAC: 0 one hoisted MAC per child; siblings fused: 1 (4 x 1 batch),

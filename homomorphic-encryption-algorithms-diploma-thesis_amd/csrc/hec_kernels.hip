@@ -501,15 +501,22 @@ struct FanModUpT {  // source (b, J) = D[b][J] (inverse pass-B domain) -> E[b][I
     int l, logN, kP;
     const DevPrime *primes;
     struct Src { const u64 *in; int prime; };
-    struct Tgt { bool valid; int prime; u64 *out; u64 q, r1; };
+    // red: how digit J (canonical, < q_J) reduces mod q_I: 0 nothing (q_J <= q_I: the 40-bit digits at the
+    // 60-bit targets), 1 one conditional subtraction (q_J <= 2 q_I: 40-bit digit, 40-bit target), 2 Barrett
+    struct Tgt { bool valid; int prime; u64 *out; u64 q, r1; int red; };
     __device__ int ntargets() const { return l + 1; }
     __device__ Src src(int job) const { return Src{D + ((u64)job << logN), job % l}; }
     __device__ Tgt tgt(int job, int I) const
     {
         const int b = job / l, J = job % l, p = I == l ? kP : I;
-        return Tgt{I != J, p, E + (((u64)((b * (l + 1) + I) * l + J)) << logN), primes[p].q, primes[p].r1};
+        const u64 qI = primes[p].q, qJ = primes[J].q;
+        return Tgt{I != J, p, E + (((u64)((b * (l + 1) + I) * l + J)) << logN), qI, primes[p].r1,
+                   qJ <= qI ? 0 : (qJ <= 2 * qI ? 1 : 2)};
     }
-    __device__ u64 xf(const Tgt &t, u64 d) const { return barrett64(d, t.q, t.r1); }
+    __device__ u64 xf(const Tgt &t, u64 d) const
+    {
+        return t.red == 0 ? d : t.red == 1 ? csub(d, t.q) : barrett64(d, t.q, t.r1);
+    }
 };
 using FanModUp = FanModUpT<false>;
 struct FanDivRound {  // source (b, k) = last limb (inverse pass-B domain) -> Z[b][k][i] for i < nl
@@ -1735,11 +1742,104 @@ __global__ void __launch_bounds__(256)
     }
 }
 
+// k_tensor_multi with the batch split over the grid: a thread owns one coefficient of BG batch entries
+// (blockIdx.y picks the group), loads each diagonal word once for its BG entries and keeps BG sets of
+// accumulators, so a wave has BG rotated-input loads in flight per diagonal and the diagonals are re-read
+// B / BG times (from L2) instead of B times.  Products are reduced as SEAL reduces them; sums are exact
+// (FP64: |sum| < 12 x 0.53 q; 60-bit primes: 128-bit sums of < 2^120 products) and canonicalised once.
+template <bool PT, int BG>
+__global__ void __launch_bounds__(256)
+    k_tensor_multi2(TensorBatch tb, u64 r_sb, u64 r_sk, u64 a_sk, PolyArr ACC, int B, int logN, u64 total, int assign,
+                    const DevPrime *__restrict__ primes)
+{
+    const u64 idx = (u64)blockIdx.x * 256 + threadIdx.x;
+    if (idx >= total) return;
+    const int b0 = blockIdx.y * BG;
+    const int nb = min(BG, B - b0);
+    const DevPrime pr = primes[idx >> logN];
+    u64 d0[BG], d1[BG], d2[BG];
+    if (pr.fp) {
+        double s0[BG], s1[BG], s2[BG];
+#pragma unroll
+        for (int g = 0; g < BG; ++g) s0[g] = s1[g] = s2[g] = 0;
+        for (int t = 0; t < tb.T; ++t) {
+            const double a0 = u2d(tb.a[t][idx]);
+            const double a1 = PT ? 0.0 : u2d(tb.a[t][a_sk + idx]);
+            const u64 *r = tb.r[t] + (u64)b0 * r_sb;
+#pragma unroll
+            for (int g = 0; g < BG; ++g) {
+                if (g >= nb) break;
+                const double r0 = u2d(r[g * r_sb + idx]), r1 = u2d(r[g * r_sb + r_sk + idx]);
+                s0[g] += fp_mulmod(r0, a0, pr.qd, pr.qinv);
+                if constexpr (PT) {
+                    s1[g] += fp_mulmod(r1, a0, pr.qd, pr.qinv);
+                } else {
+                    s1[g] += fp_mulmod(r0, a1, pr.qd, pr.qinv) + fp_mulmod(r1, a0, pr.qd, pr.qinv);
+                    s2[g] += fp_mulmod(r1, a1, pr.qd, pr.qinv);
+                }
+            }
+        }
+#pragma unroll
+        for (int g = 0; g < BG; ++g) {
+            d0[g] = fp_canon(s0[g], pr.qd, pr.qinv);
+            d1[g] = fp_canon(s1[g], pr.qd, pr.qinv);
+            d2[g] = PT ? 0 : fp_canon(s2[g], pr.qd, pr.qinv);
+        }
+    } else {
+#pragma unroll
+        for (int g = 0; g < BG; ++g) d0[g] = d1[g] = d2[g] = 0;
+        for (int t = 0; t < tb.T; ++t) {
+            const u64 a0 = tb.a[t][idx];
+            const u64 a1 = PT ? 0 : tb.a[t][a_sk + idx];
+            const u64 *r = tb.r[t] + (u64)b0 * r_sb;
+#pragma unroll
+            for (int g = 0; g < BG; ++g) {
+                if (g >= nb) break;
+                const u64 r0 = r[g * r_sb + idx], r1 = r[g * r_sb + r_sk + idx];
+                d0[g] = addmod(d0[g], mulmod(r0, a0, pr), pr.q);
+                if constexpr (PT) {
+                    d1[g] = addmod(d1[g], mulmod(r1, a0, pr), pr.q);
+                } else {
+                    U128 m{r0 * a1, mulhi64(r0, a1)};
+                    mac128(m, r1, a0);
+                    d1[g] = addmod(d1[g], barrett128(m.lo, m.hi, pr.q, pr.r0, pr.r1), pr.q);
+                    d2[g] = addmod(d2[g], mulmod(r1, a1, pr), pr.q);
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int g = 0; g < BG; ++g) {
+        if (g >= nb) break;
+        u64 *o = ACC.p + (u64)(b0 + g) * ACC.sb;
+        if (assign) {
+            o[idx] = d0[g]; o[ACC.sk + idx] = d1[g];
+            if constexpr (!PT) o[2 * ACC.sk + idx] = d2[g];
+        } else {
+            o[idx] = addmod(o[idx], d0[g], pr.q);
+            o[ACC.sk + idx] = addmod(o[ACC.sk + idx], d1[g], pr.q);
+            if constexpr (!PT) o[2 * ACC.sk + idx] = addmod(o[2 * ACC.sk + idx], d2[g], pr.q);
+        }
+    }
+}
+
 void tensor_multi(Ctx &c, const TensorBatch &tb, u64 r_sb, u64 r_sk, u64 a_sk, PolyArr ACC, int B, int l, bool assign,
                   bool plain)
 {
     const u64 total = (u64)l * c.N;
     const unsigned grid = (unsigned)((total + 255) / 256);
+    if (c.tensor_bg > 0) {
+        constexpr int BG = 4;
+        const dim3 g2(grid, (unsigned)((B + BG - 1) / BG));
+        if (plain)
+            k_tensor_multi2<true, BG><<<g2, 256, 0, c.stream>>>(tb, r_sb, r_sk, a_sk, ACC, B, c.logN, total, assign ? 1 : 0,
+                                                               c.primes);
+        else
+            k_tensor_multi2<false, BG><<<g2, 256, 0, c.stream>>>(tb, r_sb, r_sk, a_sk, ACC, B, c.logN, total,
+                                                                assign ? 1 : 0, c.primes);
+        HEC_HIP(hipGetLastError());
+        return;
+    }
     if (plain)
         k_tensor_multi<true><<<grid, 256, 0, c.stream>>>(tb, r_sb, r_sk, a_sk, ACC, B, c.logN, total, assign ? 1 : 0,
                                                           c.primes);
