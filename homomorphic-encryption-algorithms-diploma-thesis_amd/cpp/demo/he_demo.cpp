@@ -106,7 +106,7 @@ void write_output(const char *path, const std::vector<const Ciphertext *> &cts)
 int main(int argc, char **argv)
 {
     if (argc != 4) {
-        std::cout << "usage: he_demo <batched_diag|batched_col|ops|matrix|encode> <in.bin> <out.bin>\n";
+        std::cout << "usage: he_demo <batched_diag|batched_col|ops|matrix|encode|sum_elems:<dim>> <in.bin> <out.bin>\n";
         return 1;
     }
     const std::string mode = argv[1];
@@ -159,6 +159,17 @@ int main(int argc, char **argv)
         Ciphertext t = eval % cts[0] - cts[1];
         t -= eval;                                // negate
         keep.push_back(t);
+    } else if (mode.rfind("sum_elems:", 0) == 0) {
+        // matrix_operations.cpp:797-799 (BatchedVector bvec(op.size(), op_ct); bvec.sum_elems_inplace(eval, gk)) and
+        // the least-squares reductions (:919-928) through BatchedMatrix::sum_bvec_elems: every input ciphertext
+        // as a batched vector of dimension <dim>; output 0 = bvec 0 summed out of place, then the matrix's bvecs
+        const std::size_t dim = std::stoul(mode.substr(10));
+        std::vector<BatchedVector> bvecs;
+        for (auto &c : cts) bvecs.emplace_back(dim, c);
+        keep.push_back(bvecs[0].sum_elems(eval, gk).get_bvec());
+        BatchedMatrix m(BatchedMatrix::BatchingType::col, std::move(bvecs));
+        BatchedMatrix s = m.sum_bvec_elems(eval, gk);
+        for (const auto &b : s.get_bvecs()) keep.push_back(b.get_bvec());
     } else if (mode == "matrix") {
         // Matrix::matmul on 2x2 element-wise ciphertext matrices (column-major elems)
         Matrix A(2, 2, std::vector<Ciphertext>(cts.begin(), cts.begin() + 4));

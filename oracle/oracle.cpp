@@ -862,6 +862,39 @@ void rotate_vector_inplace(const Context &ctx, Ciphertext &a, int steps, const G
 }
 
 // =============================================================== he::linalg ==================
+// BatchedVector::sum_elems_inplace (he_linalg.cpp:667-713): every slot r receives the sum of the dim slots
+// r, r+1, ..., r+dim-1, built over the binary expansion of dim with rotate-and-add steps (power-of-two
+// windows), in the reference's order of rotations and additions.
+void sum_elems_inplace(const Context &ctx, Ciphertext &v, std::size_t dim, const GaloisKeys &gk)
+{
+    Ciphertext rest = v;   // the slots not yet folded in, rotated past what has been summed so far
+    Ciphertext part, t;
+    int win = 1;
+    bool started = false;  // v already holds a partial sum (odd dim: the first slot on its own)
+    if (dim & 1) {
+        started = true;
+        rotate_vector_inplace(ctx, rest, win, gk);
+    }
+    for (std::size_t bits = dim >> 1; bits; bits >>= 1) {
+        win <<= 1;
+        if (!(bits & 1)) continue;
+        int step = win >> 1;
+        t = rest;
+        rotate_vector_inplace(ctx, t, step, gk);
+        Ciphertext &w = started ? part : v;   // a window of win slots: rest + rot(rest, win/2) + ...
+        w = rest;
+        add_inplace(ctx, w, t);
+        for (step >>= 1; step; step >>= 1) {
+            t = w;
+            rotate_vector_inplace(ctx, t, step, gk);
+            add_inplace(ctx, w, t);
+        }
+        if (started) add_inplace(ctx, v, part);
+        started = true;
+        if (bits != 1) rotate_vector_inplace(ctx, rest, win, gk);
+    }
+}
+
 std::vector<Ciphertext> matmul_diag_col_set(const Context &ctx, const std::vector<const Ciphertext *> &A,
                                             const std::vector<std::size_t> &js,
                                             const std::vector<const Ciphertext *> &X, const KSwitchKey &rk,

@@ -220,6 +220,8 @@ std::vector<int> naf(int value);  // SEAL util::naf, least-significant term firs
 // BatchedMatrix::matmul (he_linalg.cpp:943-1006), diag(this) x col(other), SMART_RELIN = 1:
 //   out[i] = rescale(relin( sum_{j<n} rot(X[i], j) (*) A[j] ))
 // nthreads > 1 splits j over threads with size-3 partial sums (bit-identical: modular adds).
+// BatchedVector::sum_elems_inplace (he_linalg.cpp:667-713): log-step rotate-and-add over dim slots
+void sum_elems_inplace(const Context &ctx, Ciphertext &v, std::size_t dim, const GaloisKeys &gk);
 // The same loop restricted to the diagonals js (A[k] is diagonal js[k]): the partials the sharded
 // engine entry hec_matmul_diag_col_partial_set computes.
 std::vector<Ciphertext> matmul_diag_col_set(const Context &ctx, const std::vector<const Ciphertext *> &A,

@@ -283,6 +283,16 @@ int orc_rotate(void *c, OrcCt *a, int steps, const u32 *elts, const u64 *const *
     });
 }
 
+int orc_sum_elems(void *c, OrcCt *a, u64 dim, const u32 *elts, const u64 *const *keys, u64 nkeys)
+{
+    return guard([&] {
+        auto &ctx = *static_cast<Context *>(c);
+        Ciphertext x = in_ct(ctx, a);
+        sum_elems_inplace(ctx, x, dim, gkeys(elts, keys, nkeys));
+        out_ct(x, a);
+    });
+}
+
 static std::vector<Ciphertext> in_many(const Context &ctx, const OrcCt *v, u64 n)
 {
     std::vector<Ciphertext> r;

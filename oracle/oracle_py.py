@@ -308,6 +308,12 @@ class Oracle:
         _check(lib().orc_rotate(self.h, C.byref(s), C.c_int(steps), *self._gk(gk)))
         return self._out(s)
 
+    def sum_elems(self, a, dim, gk):
+        """BatchedVector::sum_elems_inplace (he_linalg.cpp:667-713)."""
+        s = self._in(a)
+        _check(lib().orc_sum_elems(self.h, C.byref(s), C.c_uint64(dim), *self._gk(gk)))
+        return self._out(s)
+
     # ------------------------------------------------------------------ linalg ----------------
     def _many(self, cts, cap=3):
         arr = (OrcCt * len(cts))()

@@ -145,3 +145,25 @@ def test_demo_matrix_matmul(demo, small, tmp_path):
     assert len(out) == 4
     for g, e in zip(out, exp):
         same(g, e)
+
+
+@pytest.mark.parametrize("dim", [10, 5, 6, 1])
+def test_demo_sum_elems(demo, small, tmp_path, dim):
+    """BatchedVector::sum_elems[_inplace] and BatchedMatrix::sum_bvec_elems (he_linalg.cpp:667-713, 922-938)
+    through the C++ drop-in on the GPU, bit-exact against the oracle's restatement; dim = 10 on the reference
+    demo's own vector {-11, 8, 8, 7, -10, 80, 4, 2, 3, 1} (matrix_operations.cpp:780-799)."""
+    N, m, o, rk, gk, cts = small
+    if dim == 10:
+        sk = o.secret_key(21)
+        op = np.array([-11, 8, 8, 7, -10, 80, 4, 2, 3, 1], dtype=float)
+        cts = [o.encrypt(sk, o.encode(op, 2.0**40, 3), 2.0**40, 77)] + list(cts[:2])
+    else:
+        cts = list(cts[:3])
+    out = run(demo, f"sum_elems:{dim}", tmp_path, N, m, cts, rk, gk)
+    exp = [o.sum_elems(cts[0], dim, gk)] + [o.sum_elems(c, dim, gk) for c in cts]
+    assert len(out) == len(exp)
+    for g, e in zip(out, exp):
+        same(g, e)
+    if dim == 10:
+        d = o.decode(o.decrypt(sk, exp[0]), exp[0].scale).real
+        assert abs(d[0] - 92.0) < 1e-5

@@ -85,3 +85,24 @@ def test_col_colT_and_matrix_matmul_functional(env):
         for j in range(2):
             exp = sum(Mx[i + 2 * k] * My[k + 2 * j] for k in range(2))
             assert np.max(np.abs(dec(o, sk, R[i + 2 * j]) - exp)) < 1e-4
+
+
+def test_sum_elems_functional(orc):
+    """BatchedVector::sum_elems_inplace restated (he_linalg.cpp:667-713): slot r of the result holds
+    sum_{k<dim} x[r + k], for odd and even dims; the reference demo's vector sums to 92 in slot 0
+    (matrix_operations.cpp:780-799)."""
+    N = 1 << 11
+    m = orc.Oracle.create_coeff_modulus(N, [50, 36, 36, 50])
+    o = orc.Oracle(N, m)
+    sk = o.secret_key(1)
+    gk = o.galois_keys(sk, o.default_galois_elts(), 3)
+    op = np.array([-11, 8, 8, 7, -10, 80, 4, 2, 3, 1], dtype=float)
+    r = o.sum_elems(o.encrypt(sk, o.encode(op, 2.0**40, 3), 2.0**40, 5), 10, gk)
+    assert abs(o.decode(o.decrypt(sk, r), r.scale).real[0] - 92.0) < 1e-5
+    slots = N // 2
+    for dim in (1, 2, 3, 6, 7, 13):
+        x = np.random.default_rng(dim).uniform(-1, 1, slots)
+        r = o.sum_elems(o.encrypt(sk, o.encode(x, 2.0**40, 3), 2.0**40, 7), dim, gk)
+        d = o.decode(o.decrypt(sk, r), r.scale).real
+        exp = np.array([x[(np.arange(dim) + j) % slots].sum() for j in range(slots)])
+        assert np.max(np.abs(d - exp)) < 1e-5
