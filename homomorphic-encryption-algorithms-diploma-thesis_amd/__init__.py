@@ -116,6 +116,12 @@ def lib():
             "hec_profile_read": [vp, C.c_char_p, C.POINTER(C.c_double), u64p],
             "hec_profile_read_ex": [vp, C.c_char_p, C.POINTER(C.c_double), u64p, C.POINTER(C.c_double), u64p],
             "hec_profile_classes": [vp, C.c_char_p, C.c_uint64],
+            "hec_plan_diagonal_shards": [C.c_uint64, C.c_uint64, C.c_int, C.POINTER(C.c_uint32), C.c_uint64,
+                                         C.POINTER(C.c_int32)],
+            "hec_comm_unique_id": [vp],
+            "hec_comm_init": [vp, C.c_int, C.c_int, vp],
+            "hec_context_comm": [vp, C.POINTER(C.c_int), C.POINTER(C.c_int)],
+            "hec_matmul_diag_col_sharded": [vp, vp, C.c_uint64, vp, C.c_uint64, vp, vp, vp],
             "hec_create_coeff_modulus": [C.c_uint64, C.POINTER(C.c_int), C.c_uint64, u64p],
         }
         for name, args in sig.items():
@@ -153,6 +159,23 @@ def exported_symbols():
     import re
     txt = open(HEADER_PATH).read()
     return sorted(set(re.findall(r"\b(hec_[a-z0-9_]+)\s*\(", txt)))
+
+
+def plan_diagonal_shards(N, n, world, key_elts):
+    """hec_plan_diagonal_shards (host only): per rank the sorted diagonals it owns."""
+    keys = (C.c_uint32 * max(1, len(key_elts)))(*key_elts)
+    out = (C.c_int32 * n)()
+    _check(lib().hec_plan_diagonal_shards(N, n, world, keys, len(key_elts), out))
+    plan = [[] for _ in range(world)]
+    for j in range(n):
+        plan[out[j]].append(j)
+    return plan
+
+
+def comm_unique_id() -> bytes:
+    buf = C.create_string_buffer(128)
+    _check(lib().hec_comm_unique_id(buf))
+    return buf.raw
 
 
 def create_coeff_modulus(N, bits):
@@ -292,6 +315,17 @@ class Context:
         out = out or [Ciphertext(self) for _ in cols]
         _check(lib().hec_matmul_diag_col(self.h, self._arr(diags), len(diags), self._arr(cols), len(cols), rk.h,
                                          gk.h, self._arr(out)))
+        return out
+
+    def comm_init(self, rank, world, unique_id: bytes | None = None):
+        buf = C.create_string_buffer(unique_id, 128) if unique_id is not None else None
+        _check(lib().hec_comm_init(self.h, rank, world, buf))
+
+    def matmul_diag_col_sharded(self, diags, cols, rk, gk, out=None):
+        """hec_matmul_diag_col_sharded: every rank calls it; returns all p outputs on every rank."""
+        out = out or [Ciphertext(self) for _ in cols]
+        _check(lib().hec_matmul_diag_col_sharded(self.h, self._arr(diags), len(diags), self._arr(cols), len(cols),
+                                                 rk.h, gk.h, self._arr(out)))
         return out
 
     def matmul_diagpt_col(self, pdiags, cols, gk, out=None):

@@ -126,14 +126,16 @@ int main(int argc, char **argv)
 
     std::vector<const Ciphertext *> outs;
     std::vector<Ciphertext> keep;
-    if (mode == "batched_diag" || mode == "batched_col") {
+    if (mode == "batched_diag_sharded")  // the same demo with the context on a (one-rank) RCCL communicator
+        ctx.comm_init(0, 1, hecdna::Context::comm_unique_id());
+    if (mode == "batched_diag" || mode == "batched_col" || mode == "batched_diag_sharded") {
         // matrix_operations.cpp:1112-1141 — the same code the reference runs over seal:: types
         const std::size_t dim = cts.size();
         std::vector<BatchedVector> mat1_cols_bvec;
         mat1_cols_bvec.reserve(dim);
         for (std::size_t i = 0; i < dim; ++i) mat1_cols_bvec.emplace_back(dim, cts[i]);
         std::vector<BatchedVector> res;
-        if (mode == "batched_diag") {
+        if (mode != "batched_col") {
             BatchedMatrix mat1_bmat(BatchedMatrix::BatchingType::diag, mat1_cols_bvec);
             BatchedMatrix mat2_bmat(BatchedMatrix::BatchingType::col, std::move(mat1_cols_bvec));
             BatchedMatrix mat3_bmat = mat1_bmat.matmul(eval, rk, gk, mat2_bmat);

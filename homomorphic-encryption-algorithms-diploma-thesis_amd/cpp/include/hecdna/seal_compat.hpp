@@ -71,6 +71,19 @@ public:
         return v;
     }
     void set_stream(void *hip_stream) const { check(hec_context_set_stream(h_.get(), hip_stream)); }
+    // multi-GPU (one process per GPU): after comm_init, BatchedMatrix::matmul diag x col shards its diagonals
+    // over the ranks (hec_matmul_diag_col_sharded); every rank gets every output
+    static std::vector<char> comm_unique_id()
+    {
+        std::vector<char> id(128);
+        check(hec_comm_unique_id(id.data()));
+        return id;
+    }
+    void comm_init(int rank, int world, const std::vector<char> &unique_id) const
+    {
+        check(hec_comm_init(h_.get(), rank, world, unique_id.empty() ? nullptr : unique_id.data()));
+    }
+    bool has_comm() const { return hec_context_comm(h_.get(), nullptr, nullptr) == 1; }
     void synchronize() const { check(hec_context_synchronize(h_.get())); }
 
 private:

@@ -425,8 +425,12 @@ namespace he::linalg
                                               po.data()));
         } else {    // diag x col -> col batched result (the matvec)
             assert(!other.transposed);
-            hecdna::check(hec_matmul_diag_col(eval.context().get(), pa.data(), n, pb.data(), p, rk.get(), gk.get(),
-                                              po.data()));
+            if (eval.context().has_comm())  // sharded over the ranks of the context's communicator
+                hecdna::check(hec_matmul_diag_col_sharded(eval.context().get(), pa.data(), n, pb.data(), p, rk.get(),
+                                                          gk.get(), po.data()));
+            else
+                hecdna::check(hec_matmul_diag_col(eval.context().get(), pa.data(), n, pb.data(), p, rk.get(),
+                                                  gk.get(), po.data()));
         }
         vector<BatchedVector> res;
         res.reserve(p);

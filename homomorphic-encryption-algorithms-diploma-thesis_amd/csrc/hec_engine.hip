@@ -21,9 +21,14 @@
 #include <cstring>
 #include <exception>
 #include <limits>
+#include <mutex>
+#include <set>
 #include <thread>
 
 #include "hec_internal.h"
+
+#include <dlfcn.h>
+#include <rccl/rccl.h>
 #include "hecdna.h"
 
 using namespace hec;
@@ -35,6 +40,9 @@ struct hec_context {
     // batch lanes (matvec_lanes): contexts sharing this one's device tables, each with its own HIP
     // stream, workspace and zero flag, built on first use
     std::vector<hec_context *> lanes;
+    // multi-GPU (hec_comm_init): this process's rank in a world of one process per GPU, RCCL communicator
+    int rank = 0, world = 1;
+    void *comm = nullptr;  // ncclComm_t
 };
 struct hec_ciphertext {
     hec_context *ctx = nullptr;
@@ -984,6 +992,124 @@ void matvec_lanes(hec_context *ctx, const hec_ciphertext *const *diags, const he
     for (auto &e : err)
         if (e) std::rethrow_exception(e);
 }
+
+// ---------------------------------------------------------------- multi-GPU planner and RCCL
+// The diagonal planner: SEAL's key-switch sequence of every rotation j < n (rotate_internal over the key
+// set), the diagonals ordered depth-first over the rotation prefix trie (lexicographic order of the
+// sequences keeps every subtree contiguous), then cut into `world` chunks with the smallest key-switch
+// budget per chunk that fits (binary search).  A cut inside a subtree only repeats the path above it, so
+// the ranks together spend about the 1-GPU trie's key switches.  Same rule as shard.plan_diagonal_shards.
+void plan_elts(std::size_t N, int step, const std::set<u32> &keys, std::vector<u32> &out)
+{
+    if (step == 0) return;
+    const u64 m = 2 * N;
+    const u64 s = step < 0 ? (u64)((long)N / 2 + step) : (u64)step;
+    u64 e = 1;
+    for (u64 k = 0; k < s; ++k) e = e * 3 % m;
+    if (keys.count((u32)e)) { out.push_back((u32)e); return; }
+    for (int t : naf(step))
+        if ((std::size_t)std::abs(t) != N / 2) plan_elts(N, t, keys, out);
+}
+std::vector<std::vector<std::size_t>> plan_shards(std::size_t N, std::size_t n, int world, const std::set<u32> &keys)
+{
+    need(world >= 1 && (std::size_t)world <= n, "need 1 <= world <= n");
+    std::vector<std::vector<u32>> seq(n);
+    for (std::size_t j = 0; j < n; ++j) plan_elts(N, (int)j, keys, seq[j]);
+    std::vector<std::size_t> order(n);
+    for (std::size_t j = 0; j < n; ++j) order[j] = j;
+    std::stable_sort(order.begin(), order.end(), [&](std::size_t a, std::size_t b) { return seq[a] < seq[b]; });
+    auto prefixes = [&](std::size_t j) {
+        std::vector<std::vector<u32>> pre;
+        for (std::size_t k = 1; k <= seq[j].size(); ++k) pre.emplace_back(seq[j].begin(), seq[j].begin() + k);
+        return pre;
+    };
+    std::set<std::vector<u32>> all;
+    for (std::size_t j = 0; j < n; ++j)
+        for (auto &x : prefixes(j)) all.insert(x);
+    const std::size_t total = all.size();
+    auto chunk = [&](std::size_t budget, std::size_t limit, std::vector<std::vector<std::size_t>> &out) {
+        out.clear();
+        std::vector<std::size_t> cur;
+        std::set<std::vector<u32>> seen;
+        std::size_t cost = 0;
+        for (std::size_t j : order) {
+            const auto pre = prefixes(j);
+            std::size_t add = 0;
+            for (auto &x : pre) add += seen.count(x) ? 0 : 1;
+            if (!cur.empty() && cost + add > budget) {
+                out.push_back(cur);
+                if (out.size() >= limit) return false;
+                cur.clear();
+                seen.clear();
+                cost = 0;
+                add = pre.size();
+            }
+            cur.push_back(j);
+            for (auto &x : pre) seen.insert(x);
+            cost += add;
+        }
+        out.push_back(cur);
+        return true;
+    };
+    std::size_t lo = std::max<std::size_t>(1, total / (std::size_t)world), hi = total + 1;
+    std::vector<std::vector<std::size_t>> best, tmp;
+    while (lo <= hi) {
+        const std::size_t mid = (lo + hi) / 2;
+        if (chunk(mid, (std::size_t)world, tmp)) {
+            best = tmp;
+            hi = mid - 1;
+        } else {
+            lo = mid + 1;
+        }
+    }
+    while ((int)best.size() < world) {  // split the largest chunks until every rank has one
+        std::size_t k = 0;
+        for (std::size_t i = 1; i < best.size(); ++i)
+            if (best[i].size() > best[k].size()) k = i;
+        std::vector<std::size_t> c = best[k];
+        best.erase(best.begin() + (long)k);
+        best.insert(best.begin() + (long)k, std::vector<std::size_t>(c.begin() + (long)(c.size() / 2), c.end()));
+        best.insert(best.begin() + (long)k, std::vector<std::size_t>(c.begin(), c.begin() + (long)(c.size() / 2)));
+    }
+    for (auto &c : best) std::sort(c.begin(), c.end());
+    return best;
+}
+
+// RCCL, loaded on first use (the engine itself does not link it): the functions of rccl.h we call
+struct Rccl {
+    decltype(&ncclGetUniqueId) get_unique_id = nullptr;
+    decltype(&ncclCommInitRank) init_rank = nullptr;
+    decltype(&ncclCommDestroy) destroy = nullptr;
+    decltype(&ncclAllReduce) all_reduce = nullptr;
+    decltype(&ncclGetErrorString) error_string = nullptr;
+};
+const Rccl &rccl()
+{
+    static Rccl r;
+    static bool tried = false;
+    static std::mutex mu;
+    std::lock_guard<std::mutex> lock(mu);
+    if (!tried) {
+        tried = true;
+        void *h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (h) {
+            r.get_unique_id = (decltype(r.get_unique_id))dlsym(h, "ncclGetUniqueId");
+            r.init_rank = (decltype(r.init_rank))dlsym(h, "ncclCommInitRank");
+            r.destroy = (decltype(r.destroy))dlsym(h, "ncclCommDestroy");
+            r.all_reduce = (decltype(r.all_reduce))dlsym(h, "ncclAllReduce");
+            r.error_string = (decltype(r.error_string))dlsym(h, "ncclGetErrorString");
+        }
+    }
+    if (!r.get_unique_id || !r.init_rank || !r.all_reduce || !r.destroy)
+        throw std::logic_error("RCCL (librccl.so.1) is not available");
+    return r;
+}
+void nccl_check(ncclResult_t e, const char *what)
+{
+    if (e != ncclSuccess)
+        throw std::logic_error(std::string(what) + ": " + (rccl().error_string ? rccl().error_string(e) : "RCCL error"));
+}
 }  // namespace
 
 // =============================================================================== workspace ==
@@ -1207,6 +1333,7 @@ int hec_context_destroy(hec_context *ctx)
         (void)hipSetDevice(c.device);
         for (hec_context *l : ctx->lanes) free_lane(l);
         (void)hipStreamSynchronize(c.stream);
+        if (ctx->comm) (void)rccl().destroy((ncclComm_t)ctx->comm);
         c.ws.release();
         (void)hipFree(c.primes);
         (void)hipFree(c.imap);
@@ -1947,6 +2074,104 @@ int hec_matmul_finish(hec_context *ctx, hec_ciphertext *const *acc, uint64_t p, 
             d2d(c, out[i]->d, O + i * So, So);
             out[i]->size = 2; out[i]->level = l - 1; out[i]->scale = sc[i];
         }
+    });
+}
+
+// ------------------------------------------------------------------ multi-GPU
+
+int hec_plan_diagonal_shards(uint64_t N, uint64_t n, int world, const uint32_t *key_elts, uint64_t nkeys,
+                             int32_t *rank_of_diag)
+{
+    return guard([&] {
+        need(rank_of_diag && (key_elts || nkeys == 0), "null argument");
+        need(N >= 1024 && N <= 65536 && !(N & (N - 1)), "poly_modulus_degree must be a power of two in [2^10, 2^16]");
+        std::set<u32> keys(key_elts, key_elts + nkeys);
+        const auto plan = plan_shards(N, n, world, keys);
+        for (std::size_t r = 0; r < plan.size(); ++r)
+            for (std::size_t j : plan[r]) rank_of_diag[j] = (int32_t)r;
+    });
+}
+
+int hec_comm_unique_id(void *unique_id)
+{
+    return guard([&] {
+        need(unique_id != nullptr, "null argument");
+        ncclUniqueId id;
+        nccl_check(rccl().get_unique_id(&id), "ncclGetUniqueId");
+        std::memcpy(unique_id, &id, sizeof(id));
+    });
+}
+
+int hec_comm_init(hec_context *ctx, int rank, int world, const void *unique_id)
+{
+    return guard([&] {
+        set_device(ctx);
+        need(world >= 1 && rank >= 0 && rank < world, "invalid rank / world");
+        need(ctx->comm == nullptr, "communicator already initialised");
+        if (world > 1 || unique_id) {  // world 1 with an id: a one-rank communicator (exercises the RCCL path)
+            need(unique_id != nullptr, "null argument");
+            ncclUniqueId id;
+            std::memcpy(&id, unique_id, sizeof(id));
+            ncclComm_t comm = nullptr;
+            nccl_check(rccl().init_rank(&comm, world, id, rank), "ncclCommInitRank");
+            ctx->comm = comm;
+        }
+        ctx->rank = rank;
+        ctx->world = world;
+    });
+}
+
+int hec_context_comm(const hec_context *ctx, int *rank, int *world)
+{
+    if (!ctx) return HEC_EINVAL;
+    if (rank) *rank = ctx->rank;
+    if (world) *world = ctx->world;
+    return ctx->comm ? 1 : 0;
+}
+
+int hec_matmul_diag_col_sharded(hec_context *ctx, const hec_ciphertext *const *diags, uint64_t n,
+                                const hec_ciphertext *const *cols, uint64_t p, const hec_kswitch_key *rk,
+                                const hec_galois_keys *gk, hec_ciphertext *const *out)
+{
+    return guard([&] {
+        set_device(ctx);
+        need(diags && cols && out && n >= 1 && p >= 1, "empty matrix operand");
+        need(gk && gk->ctx == ctx, "galois_keys is not valid for encryption parameters");
+        need(ctx->world == 1 || ctx->comm, "hec_comm_init has not been called");
+        Ctx &c = ctx->c;
+        std::vector<std::size_t> all(n);
+        for (uint64_t j = 0; j < n; ++j) all[j] = j;
+        matvec_check(ctx, diags, nullptr, n, all, cols, p, rk, gk, true);  // SEAL's errors, same on every rank
+        std::set<u32> keys;
+        for (const auto &kv : gk->keys) keys.insert(kv.first);
+        const auto plan = plan_shards(c.N, n, ctx->world, keys);
+        const std::vector<std::size_t> &mine = plan[ctx->rank];
+        const std::size_t l = cols[0]->level, S3 = 3 * l * c.N;
+        // this rank's size-3 partials over its trie subtrees of diagonals
+        std::vector<hec_ciphertext> acc(p);
+        std::vector<hec_ciphertext *> accp(p);
+        for (uint64_t i = 0; i < p; ++i) { acc[i].ctx = ctx; accp[i] = &acc[i]; }
+        struct Free {
+            std::vector<hec_ciphertext> &a;
+            ~Free() { for (auto &x : a) if (x.d) (void)hipFree(x.d); }
+        } free_acc{acc};
+        matvec_lanes(ctx, diags, nullptr, n, mine, cols, p, nullptr, gk, false, accp.data());
+        if (ctx->comm) {
+            // the one exchange: a plain u64 sum of the world's canonical residues (< world 2^60 < 2^64), then
+            // reduce mod q; every rank then holds the full accumulators (he_linalg.cpp:977-997 summed)
+            u64 *buf = nullptr;
+            HEC_HIP(hipMallocAsync((void **)&buf, p * S3 * sizeof(u64), c.stream));
+            for (uint64_t i = 0; i < p; ++i) d2d(c, buf + i * S3, acc[i].d, S3);
+            nccl_check(rccl().all_reduce(buf, buf, p * S3, ncclUint64, ncclSum, (ncclComm_t)ctx->comm, c.stream),
+                       "ncclAllReduce");
+            ew_reduce(c, buf, (int)(3 * p), (int)l);
+            for (uint64_t i = 0; i < p; ++i) d2d(c, acc[i].d, buf + i * S3, S3);
+            HEC_HIP(hipFreeAsync(buf, c.stream));
+        }
+        // lazy relinearize + rescale (he_linalg.cpp:999-1002) of every output on every rank: p key switches
+        // against the ~n/world rotations each rank ran, and no second collective
+        const int rc = hec_matmul_finish(ctx, accp.data(), p, rk, out);
+        if (rc != HEC_OK) throw std::logic_error(hec_last_error());
     });
 }
 

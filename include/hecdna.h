@@ -170,6 +170,31 @@ int hec_matrix_matmul(hec_context *ctx, const hec_ciphertext *const *A, uint64_t
                       int a_transposed, const hec_ciphertext *const *B, uint64_t b_rows, uint64_t b_cols,
                       int b_transposed, const hec_kswitch_key *rk, hec_ciphertext *const *out);
 
+/* ---------------------------------------------------------------- multi-GPU (SURVEY 8(b),(e)) */
+/* One process per GPU.  The reference is single-threaded (no collective anywhere); the sharded matvec splits
+ * the diagonal loop of BatchedMatrix::matmul (he_linalg.cpp:977-997) over the ranks and exchanges the size-3
+ * partial sums once over RCCL (xGMI), so a C++ caller of the he_linalg.h drop-in shards through this ABI alone.
+ *
+ * Planner (host only, no GPU): rank_of_diag[j] = the rank that owns diagonal j < n: whole subtrees of the
+ * rotation prefix trie (SEAL's key-switch sequences over the key set key_elts), balanced by key switches. */
+int hec_plan_diagonal_shards(uint64_t poly_modulus_degree, uint64_t n, int world, const uint32_t *key_elts,
+                             uint64_t nkeys, int32_t *rank_of_diag);
+/* ncclGetUniqueId: 128 bytes that rank 0 creates and every rank passes to hec_comm_init (RCCL is loaded on
+ * first use from librccl.so.1; HEC_ELOGIC when it is absent). */
+int hec_comm_unique_id(void *unique_id);
+/* ncclCommInitRank on the context's device; world == 1 needs no id.  The communicator lives until
+ * hec_context_destroy. */
+int hec_comm_init(hec_context *ctx, int rank, int world, const void *unique_id);
+/* 1 when the context has a communicator (then *rank, *world are set), 0 when not, HEC_EINVAL on NULL */
+int hec_context_comm(const hec_context *ctx, int *rank, int *world);
+/* BatchedMatrix::matmul diag x col over the world (every rank calls it with the same arguments): rank r
+ * computes the partial sums over its planned diagonals (only those diags[j] are read, others may be any
+ * handle), one RCCL all-reduce (u64 sum, exact for world <= 8 and 60-bit primes) + reduction mod q, then every
+ * rank relinearizes and rescales all p outputs: out[i] is bit-identical to hec_matmul_diag_col on one GPU. */
+int hec_matmul_diag_col_sharded(hec_context *ctx, const hec_ciphertext *const *diags, uint64_t n,
+                                const hec_ciphertext *const *cols, uint64_t p, const hec_kswitch_key *rk,
+                                const hec_galois_keys *gk, hec_ciphertext *const *out);
+
 /* ---------------------------------------------------------------- primitives (cfg2) ------- */
 /* In-place batched negacyclic NTT over device data u64[npolys][nlimbs][N]; limb j uses prime
  * limb0 + j (SEAL ntt_negacyclic_harvey / inverse_ntt_negacyclic_harvey, canonical in/out). */

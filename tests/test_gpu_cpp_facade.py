@@ -81,6 +81,17 @@ def test_demo_batched_col_matches_golden(demo, orc, tmp_path):
     assert [sha(d, sc) for d, sc in out] == fx["output_sha256"]
 
 
+def test_demo_batched_diag_sharded_rccl(demo, orc, tmp_path):
+    """The he_linalg.h drop-in with its context on an RCCL communicator (one rank): BatchedMatrix::matmul takes
+    the sharded C-ABI path (hec_matmul_diag_col_sharded) and still reproduces the cfg1 golden hashes."""
+    sys.path.insert(0, GOLD)
+    from make_golden import cfg1_inputs, sha
+    fx = json.load(open(os.path.join(GOLD, "cfg1_matvec.json")))
+    o, m, sk, rk, gk, cts = cfg1_inputs(orc)
+    out = run(demo, "batched_diag_sharded", tmp_path, fx["N"], m, cts, rk, gk)
+    assert [sha(d, sc) for d, sc in out] == fx["output_sha256"]
+
+
 @pytest.fixture(scope="module")
 def small(orc):
     N = 1 << 11

@@ -69,3 +69,26 @@ def test_partial_set_rejects_bad_indices(env, hecdna):
         e.ctx.matmul_diag_col_partial_set(gA, [0, 4], gX, e.gk)
     with pytest.raises(hecdna.InvalidArgument):
         e.ctx.matmul_diag_col_partial_set(gA, [], gX, e.gk)
+
+
+def test_cabi_sharded_matvec_one_rank_rccl(env, hecdna):
+    """hec_comm_init with a real one-rank RCCL communicator + hec_matmul_diag_col_sharded (planner, partials,
+    ncclAllReduce of the u64 words, reduction mod q, finish on every rank) equals hec_matmul_diag_col bit for
+    bit; without a communicator the call runs the world-1 path."""
+    e = env
+    n, p = 20, 3
+    gA = [e.up(e.enc(seed=700 + j)) for j in range(n)]
+    gX = [e.up(e.enc(seed=800 + i)) for i in range(p)]
+    ref = e.ctx.matmul_diag_col(gA, gX, e.rk, e.gk)
+    ctx = hecdna.Context(e.N, e.m)
+    rk, gk = ctx.relin_key(e.rk_h), ctx.galois_keys(e.gk_h)
+    A = [ctx.ciphertext(a.download(), a.scale) for a in gA]
+    X = [ctx.ciphertext(x.download(), x.scale) for x in gX]
+    plain = ctx.matmul_diag_col_sharded(A, X, rk, gk)            # no communicator: world 1
+    ctx.comm_init(0, 1, hecdna.comm_unique_id())
+    got = ctx.matmul_diag_col_sharded(A, X, rk, gk)
+    for g, q, r in zip(got, plain, ref):
+        assert np.array_equal(g.download(), r.download()) and g.scale == r.scale
+        assert np.array_equal(q.download(), r.download())
+    with pytest.raises(hecdna.InvalidArgument, match="already"):
+        ctx.comm_init(0, 1, hecdna.comm_unique_id())

@@ -136,3 +136,13 @@ def test_gloo_world2_exchange_bit_exact(shard, p):
     assert all(r[1] == "ok" for r in res), res
     owned = sorted(i for r in res for i in r[2])
     assert owned == list(range(p))
+
+
+@pytest.mark.parametrize("N,n,world", [(1 << 15, 4096, 2), (1 << 15, 4096, 8), (1 << 13, 64, 3), (1 << 16, 1024, 4),
+                                       (1 << 11, 10, 8)])
+def test_cpp_planner_equals_python(hecdna, N, n, world):
+    """hec_plan_diagonal_shards (the C-ABI planner a C++ caller of the he_linalg.h drop-in uses) makes the same
+    trie-subtree partition as shard.plan_diagonal_shards."""
+    import hecdna.shard as shard
+    keys = shard.default_galois_elts(N)
+    assert hecdna.plan_diagonal_shards(N, n, world, keys) == shard.plan_diagonal_shards(N, n, world, set(keys))
