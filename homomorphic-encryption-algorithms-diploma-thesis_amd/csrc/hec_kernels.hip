@@ -517,6 +517,27 @@ struct FanModUpT {  // source (b, J) = D[b][J] (inverse pass-B domain) -> E[b][I
     {
         return t.red == 0 ? d : t.red == 1 ? csub(d, t.q) : barrett64(d, t.q, t.r1);
     }
+    // the 16 values of a thread as the target's NTT input (k_fan2; the class branch is block-uniform).  FP64
+    // targets take any congruent integer-valued double with |x| < 2 q_I (their forward butterflies stay below
+    // 10 q_I over all stages and every output is canonicalised): a digit with q_J <= 2 q_I needs no
+    // reduction at all, only the conversion
+    __device__ void xf16(const Tgt &t, bool fp, const u64 *d, u64 *v) const
+    {
+        if (t.red == 2) {
+#pragma unroll
+            for (int k = 0; k < 16; ++k) v[k] = barrett64(d[k], t.q, t.r1);
+        } else if (t.red == 1 && !fp) {
+#pragma unroll
+            for (int k = 0; k < 16; ++k) v[k] = csub(d[k], t.q);
+        } else {
+#pragma unroll
+            for (int k = 0; k < 16; ++k) v[k] = d[k];
+        }
+        if (fp) {
+#pragma unroll
+            for (int k = 0; k < 16; ++k) v[k] = (u64)__double_as_longlong(u2d(v[k]));
+        }
+    }
 };
 using FanModUp = FanModUpT<false>;
 struct FanDivRound {  // source (b, k) = last limb (inverse pass-B domain) -> Z[b][k][i] for i < nl
@@ -528,6 +549,7 @@ struct FanDivRound {  // source (b, k) = last limb (inverse pass-B domain) -> Z[
     u64 last, half;
     const DevPrime *primes;
     u64 fix[HEC_MAXL];
+    u64 two32[HEC_MAXL], hmod[HEC_MAXL];  // 2^32 mod q_i and half mod q_i (FP64 targets)
     struct Src { const u64 *in; int prime; };
     struct Tgt { bool valid; int prime; u64 *out; u64 q, r1, fix; };
     __device__ int ntargets() const { return nl; }
@@ -541,6 +563,26 @@ struct FanDivRound {  // source (b, k) = last limb (inverse pass-B domain) -> Z[
         u64 v = d + half;
         v = v >= last ? v - last : v;
         return barrett64(v, t.q, t.r1) + t.fix;
+    }
+    // FP64 targets (q_i < 2^42): v = (y + h) mod last < 2^61 split as vh 2^32 + vl; vh (2^32 mod q_i) by the
+    // exact FP64 product (|r| <= 0.53 q_i), plus vl < 2^32 and -(h mod q_i): an integer-valued double congruent
+    // to v - h, |.| < 1.6 q_i (the forward FP64 NTT's input bound is 2 q_i; outputs are canonicalised later)
+    __device__ void xf16(const Tgt &t, bool fp, const u64 *d, u64 *v) const
+    {
+        if (!fp) {
+#pragma unroll
+            for (int k = 0; k < 16; ++k) v[k] = xf(t, d[k]);
+            return;
+        }
+        const DevPrime &pr = primes[t.prime];
+        const double c32 = u2d(two32[t.prime]), hneg = -u2d(hmod[t.prime]);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            u64 y = d[k] + half;
+            y = y >= last ? y - last : y;
+            const double r = fp_mulmod(u2d(y >> 32), c32, pr.qd, pr.qinv) + u2d(y & 0xffffffffull) + hneg;
+            v[k] = (u64)__double_as_longlong(r);
+        }
     }
 };
 
@@ -715,12 +757,10 @@ __global__ void __launch_bounds__(NSEG *(1 << LOGP) / 16)
         buf ^= 1;
         u64 v[16];
         if (pt.fp) {
-#pragma unroll
-            for (int k = 0; k < 16; ++k) v[k] = (u64)__double_as_longlong(u2d(fan.xf(tgt, d[k])));
+            fan.xf16(tgt, true, d, v);
             ntt_round_r<LOGP, 0, 4, false, true>(v, ts, tw, pt);
         } else {
-#pragma unroll
-            for (int k = 0; k < 16; ++k) v[k] = fan.xf(tgt, d[k]);
+            fan.xf16(tgt, false, d, v);
             ntt_round_r<LOGP, 0, 4, false, false>(v, ts, tw, pt);
         }
 #pragma unroll
@@ -1206,7 +1246,11 @@ void fan_divide_round(Ctx &c, const u64 *Y, u64 ysb, u64 ysk, u64 *Z, int B, int
     FanDivRound f{};
     f.Y = Y; f.ysb = ysb; f.ysk = ysk; f.Z = Z; f.nk = nk; f.nl = nl; f.logN = c.logN; f.last_idx = last_idx;
     f.last = c.q[last_idx]; f.half = f.last >> 1; f.primes = c.primes;
-    for (int i = 0; i < nl; ++i) f.fix[i] = c.q[i] - (f.half % c.q[i]);
+    for (int i = 0; i < nl; ++i) {
+        f.fix[i] = c.q[i] - (f.half % c.q[i]);
+        f.two32[i] = (u64)(((unsigned __int128)1 << 32) % c.q[i]);
+        f.hmod[i] = f.half % c.q[i];
+    }
     fan_dispatch(c, B * nk, f, std::min(c.fan_groups_moddown, nl));
 }
 
