@@ -1186,7 +1186,7 @@ int hec_context_create(uint64_t N, const uint64_t *mod, uint64_t K, int device, 
         if (const char *f = std::getenv("HEC_BMAC_KEYS")) c.bmac_keys = f[0] - '0';
         if (const char *f = std::getenv("HEC_FUSE_GALOIS")) c.fuse_galois = f[0] != '0';
         if (const char *f = std::getenv("HEC_FAN")) c.fan_out = f[0] != '0';
-        if (const char *f = std::getenv("HEC_FAN2")) c.fan2 = f[0] != '0';
+        if (const char *f = std::getenv("HEC_FAN2")) c.fan2 = std::atoi(f);
         if (const char *f = std::getenv("HEC_TENSOR_BG")) c.tensor_bg = std::atoi(f);
         if (const char *f = std::getenv("HEC_LANES")) c.lanes = std::max(1, std::atoi(f));
         if (const char *f = std::getenv("HEC_FANG"))

@@ -549,7 +549,6 @@ struct FanDivRound {  // source (b, k) = last limb (inverse pass-B domain) -> Z[
     u64 last, half;
     const DevPrime *primes;
     u64 fix[HEC_MAXL];
-    u64 two32[HEC_MAXL], hmod[HEC_MAXL];  // 2^32 mod q_i and half mod q_i (FP64 targets)
     struct Src { const u64 *in; int prime; };
     struct Tgt { bool valid; int prime; u64 *out; u64 q, r1, fix; };
     __device__ int ntargets() const { return nl; }
@@ -564,24 +563,15 @@ struct FanDivRound {  // source (b, k) = last limb (inverse pass-B domain) -> Z[
         v = v >= last ? v - last : v;
         return barrett64(v, t.q, t.r1) + t.fix;
     }
-    // FP64 targets (q_i < 2^42): v = (y + h) mod last < 2^61 split as vh 2^32 + vl; vh (2^32 mod q_i) by the
-    // exact FP64 product (|r| <= 0.53 q_i), plus vl < 2^32 and -(h mod q_i): an integer-valued double congruent
-    // to v - h, |.| < 1.6 q_i (the forward FP64 NTT's input bound is 2 q_i; outputs are canonicalised later)
+    // (an FP64 split reduction here, (y >> 32) (2^32 mod q_i) by the exact FP64 product plus the low word,
+    // measured slower: 276 VGPRs, one wave per SIMD, mod-down fan-out 1,396 vs 1,045 ms per step)
     __device__ void xf16(const Tgt &t, bool fp, const u64 *d, u64 *v) const
     {
-        if (!fp) {
 #pragma unroll
-            for (int k = 0; k < 16; ++k) v[k] = xf(t, d[k]);
-            return;
-        }
-        const DevPrime &pr = primes[t.prime];
-        const double c32 = u2d(two32[t.prime]), hneg = -u2d(hmod[t.prime]);
+        for (int k = 0; k < 16; ++k) v[k] = xf(t, d[k]);
+        if (fp) {
 #pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            u64 y = d[k] + half;
-            y = y >= last ? y - last : y;
-            const double r = fp_mulmod(u2d(y >> 32), c32, pr.qd, pr.qinv) + u2d(y & 0xffffffffull) + hneg;
-            v[k] = (u64)__double_as_longlong(r);
+            for (int k = 0; k < 16; ++k) v[k] = (u64)__double_as_longlong(u2d(v[k]));
         }
     }
 };
@@ -703,12 +693,14 @@ __device__ __forceinline__ void ntt_round_r(u64 *v, int ts, const TwG &twg, cons
 // the target tiles are stored straight from it, so each transform (the INTT and every target's forward
 // pass) exchanges through LDS once instead of three times, with one barrier per exchange (two LDS tiles
 // alternate between consecutive exchanges).  Same inputs, outputs and intermediate formats as k_fan.
-template <int LOGP, int NSEG, class FAN>
-__global__ void __launch_bounds__(NSEG *(1 << LOGP) / 16)
+// DB: two alternating LDS tiles and one barrier per exchange (2 blocks per CU at N = 2^15); DB = false: one
+// tile, a second barrier per target, and MINW waves per SIMD requested from the register allocator.
+template <int LOGP, int NSEG, class FAN, bool DB = true, int MINW = 1>
+__global__ void __launch_bounds__(NSEG *(1 << LOGP) / 16, MINW)
     k_fan2(const FAN fan, TwTables inv, TwTables fwd, const DevPrime *__restrict__ primes, int logN)
 {
     constexpr int P = 1 << LOGP, TPS = P / 16, LD = NSEG + 1, TILE = P * LD;
-    __shared__ u64 lds[2 * TILE];
+    __shared__ u64 lds[(DB ? 2 : 1) * TILE];
     const int seg0 = blockIdx.x * NSEG, lc = logN - LOGP;
     const int ts = threadIdx.x / NSEG, sg = threadIdx.x % NSEG;
     auto gstride = [&](int k) { return ((u64)(ts + k * TPS) << lc) + seg0 + sg; };
@@ -753,8 +745,9 @@ __global__ void __launch_bounds__(NSEG *(1 << LOGP) / 16)
         if (!tgt.valid) continue;
         const DevPrime pt = primes[tgt.prime];
         const GlobalTw<decltype(twidx)> tw{twidx, fwd.a + ((u64)tgt.prime << logN), fwd.fa + ((u64)tgt.prime << logN)};
-        u64 *tile = lds + buf * TILE;
+        u64 *tile = lds + (DB ? buf * TILE : 0);
         buf ^= 1;
+        if (!DB) __syncthreads();  // the previous exchange's reads are done
         u64 v[16];
         if (pt.fp) {
             fan.xf16(tgt, true, d, v);
@@ -780,7 +773,10 @@ static void run_fan(Ctx &c, int njobs, const FAN &fan, int groups)
 {
     constexpr int R = 1 << LOGR, C = 1 << LOGC;
     const TwTables fwd{c.tw, c.twb, c.twf, c.twbf}, inv{c.itw, c.itwb, c.itwf, c.itwbf};
-    if (c.fan2) k_fan2<LOGR, NA><<<dim3(C / NA, njobs, groups), NA * R / 16, 0, c.stream>>>(fan, inv, fwd, c.primes, c.logN);
+    if (c.fan2 == 2)
+        k_fan2<LOGR, NA, FAN, false, 3><<<dim3(C / NA, njobs, groups), NA * R / 16, 0, c.stream>>>(fan, inv, fwd, c.primes,
+                                                                                                  c.logN);
+    else if (c.fan2) k_fan2<LOGR, NA><<<dim3(C / NA, njobs, groups), NA * R / 16, 0, c.stream>>>(fan, inv, fwd, c.primes, c.logN);
     else k_fan<LOGR, NA><<<dim3(C / NA, njobs, groups), NA * R / 16, 0, c.stream>>>(fan, inv, fwd, c.primes, c.logN);
     HEC_HIP(hipGetLastError());
 }
@@ -1248,8 +1244,6 @@ void fan_divide_round(Ctx &c, const u64 *Y, u64 ysb, u64 ysk, u64 *Z, int B, int
     f.last = c.q[last_idx]; f.half = f.last >> 1; f.primes = c.primes;
     for (int i = 0; i < nl; ++i) {
         f.fix[i] = c.q[i] - (f.half % c.q[i]);
-        f.two32[i] = (u64)(((unsigned __int128)1 << 32) % c.q[i]);
-        f.hmod[i] = f.half % c.q[i];
     }
     fan_dispatch(c, B * nk, f, std::min(c.fan_groups_moddown, nl));
 }
