@@ -123,6 +123,21 @@ def lib():
             "hec_context_comm": [vp, C.POINTER(C.c_int), C.POINTER(C.c_int)],
             "hec_matmul_diag_col_sharded": [vp, vp, C.c_uint64, vp, C.c_uint64, vp, vp, vp],
             "hec_create_coeff_modulus": [C.c_uint64, C.POINTER(C.c_int), C.c_uint64, u64p],
+            "hec_seal_blake2b": [vp, C.c_uint64, C.c_uint64, vp],
+            "hec_seal_parms_id": [C.c_uint64, u64p, C.c_uint64, u64p],
+            "hec_seal_ciphertext_load": [vp, C.c_uint64, u64p, u64p, u64p, C.POINTER(C.c_double), u64p, u64p,
+                                         C.c_uint64, u64p],
+            "hec_seal_ciphertext_save": [u64p, C.c_uint64, C.c_uint64, C.c_uint64, C.c_double, u64p, C.c_int, vp,
+                                         C.c_uint64, u64p],
+            "hec_seal_parms_load": [vp, C.c_uint64, u64p, u64p, C.c_uint64, u64p, u64p],
+            "hec_seal_parms_save": [C.c_uint64, u64p, C.c_uint64, C.c_int, vp, C.c_uint64, u64p],
+            "hec_seal_kswitch_keys_load": [vp, C.c_uint64, C.c_uint64, u64p, u64p, C.c_uint64, u64p, u64p],
+            "hec_seal_kswitch_keys_save": [C.c_uint64, u64p, C.c_uint64, C.POINTER(u64p), u64p, C.c_uint64, C.c_int,
+                                           vp, C.c_uint64, u64p],
+            "hec_ciphertext_load_seal": [vp, vp, C.c_uint64, u64p],
+            "hec_ciphertext_save_seal": [vp, C.c_int, vp, C.c_uint64, u64p],
+            "hec_kswitch_key_load_seal": [vp, vp, C.c_uint64, C.POINTER(vp), u64p],
+            "hec_galois_keys_load_seal": [vp, vp, C.c_uint64, u64p],
         }
         for name, args in sig.items():
             fn = getattr(L, name)
@@ -135,6 +150,7 @@ def lib():
         L.hec_galois_keys_has.argtypes = [vp, C.c_uint32]
         L.hec_galois_keys_has.restype = C.c_int
         L.hec_profile_classes.restype = C.c_uint64
+        L.hec_seal_last_error.restype = C.c_char_p
         _lib = L
     return _lib
 
@@ -176,6 +192,97 @@ def comm_unique_id() -> bytes:
     buf = C.create_string_buffer(128)
     _check(lib().hec_comm_unique_id(buf))
     return buf.raw
+
+
+# ------------------------------------------------------------------ SEAL wire format (host side)
+COMPR_NONE, COMPR_ZLIB, COMPR_ZSTD = 0, 1, 2
+
+
+def _seal_check(rc):
+    if rc != 0:
+        msg = lib().hec_seal_last_error().decode()
+        raise (InvalidArgument if rc == 1 else LogicError)(rc, msg)
+
+
+def _bytes_in(b: bytes):
+    return C.c_char_p(b), len(b)
+
+
+def _sized_out(fn):
+    """Call fn(out, cap, written) twice: size query, then into a buffer of that size."""
+    n = C.c_uint64()
+    _seal_check(fn(None, 0, C.byref(n)))
+    buf = C.create_string_buffer(n.value)
+    _seal_check(fn(buf, n.value, C.byref(n)))
+    return buf.raw[: n.value]
+
+
+def seal_blake2b(data: bytes, outlen=64) -> bytes:
+    out = C.create_string_buffer(outlen)
+    _seal_check(lib().hec_seal_blake2b(C.c_char_p(data), len(data), outlen, out))
+    return out.raw
+
+
+def seal_parms_id(N, moduli):
+    m = np.ascontiguousarray(np.array(moduli, dtype=np.uint64))
+    out = np.zeros(4, dtype=np.uint64)
+    _seal_check(lib().hec_seal_parms_id(N, _p(m), len(m), _p(out)))
+    return out
+
+
+def seal_ciphertext_save(data: np.ndarray, scale: float, moduli, compr=COMPR_ZSTD) -> bytes:
+    """Ciphertext::save of u64[size][level][N] (parms_id of its level from moduli)."""
+    d = np.ascontiguousarray(data, dtype=np.uint64)
+    m = np.ascontiguousarray(np.array(moduli, dtype=np.uint64))
+    size, level, N = d.shape
+    return _sized_out(lambda o, c, w: lib().hec_seal_ciphertext_save(_p(d), size, level, N, scale, _p(m), compr, o, c, w))
+
+
+def seal_ciphertext_load(b: bytes):
+    """-> (data u64[size][level][N], scale, parms_id, bytes consumed)"""
+    size, level, N, used = C.c_uint64(), C.c_uint64(), C.c_uint64(), C.c_uint64()
+    scale = C.c_double()
+    pid = np.zeros(4, dtype=np.uint64)
+    src, n = _bytes_in(b)
+    _seal_check(lib().hec_seal_ciphertext_load(src, n, C.byref(size), C.byref(level), C.byref(N), C.byref(scale),
+                                               _p(pid), None, 0, C.byref(used)))
+    d = np.zeros((size.value, level.value, N.value), dtype=np.uint64)
+    _seal_check(lib().hec_seal_ciphertext_load(src, n, None, None, None, None, None, _p(d), d.size, None))
+    return d, scale.value, pid, used.value
+
+
+def seal_parms_save(N, moduli, compr=COMPR_NONE) -> bytes:
+    m = np.ascontiguousarray(np.array(moduli, dtype=np.uint64))
+    return _sized_out(lambda o, c, w: lib().hec_seal_parms_save(N, _p(m), len(m), compr, o, c, w))
+
+
+def seal_parms_load(b: bytes):
+    """EncryptionParameters::load -> (N, moduli, bytes consumed)"""
+    N, k, used = C.c_uint64(), C.c_uint64(), C.c_uint64()
+    src, n = _bytes_in(b)
+    out = np.zeros(64, dtype=np.uint64)
+    _seal_check(lib().hec_seal_parms_load(src, n, C.byref(N), _p(out), 64, C.byref(k), C.byref(used)))
+    return N.value, [int(x) for x in out[: k.value]], used.value
+
+
+def seal_kswitch_keys_save(N, moduli, key_lists, compr=COMPR_NONE) -> bytes:
+    """KSwitchKeys::save: key_lists[i] = u64[L][2][K][N] or None (an empty list)."""
+    m = np.ascontiguousarray(np.array(moduli, dtype=np.uint64))
+    keep = [None if k is None else np.ascontiguousarray(k, dtype=np.uint64) for k in key_lists]
+    ptrs = (u64p * max(1, len(keep)))(*[(_p(k) if k is not None else u64p()) for k in keep])
+    digits = np.array([0 if k is None else k.shape[0] for k in keep] or [0], dtype=np.uint64)
+    return _sized_out(lambda o, c, w: lib().hec_seal_kswitch_keys_save(N, _p(m), len(m), ptrs, _p(digits), len(keep),
+                                                                     compr, o, c, w))
+
+
+def seal_kswitch_keys_load(b: bytes, index):
+    """key list `index` as u64 words (u64[L][2][K][N] flattened), and the object's list count"""
+    lists, words, used = C.c_uint64(), C.c_uint64(), C.c_uint64()
+    src, n = _bytes_in(b)
+    _seal_check(lib().hec_seal_kswitch_keys_load(src, n, index, C.byref(lists), None, 0, C.byref(words), C.byref(used)))
+    out = np.zeros(words.value, dtype=np.uint64)
+    _seal_check(lib().hec_seal_kswitch_keys_load(src, n, index, None, _p(out), out.size, None, None))
+    return out, lists.value, used.value
 
 
 def create_coeff_modulus(N, bits):
@@ -495,6 +602,20 @@ class Ciphertext:
         _check(lib().hec_ciphertext_copy(c.h, self.h))
         return c
 
+    def load_seal(self, b: bytes):
+        """Ciphertext::load(context, in, size) from SEAL's wire format; returns the bytes read."""
+        used = C.c_uint64()
+        _check(lib().hec_ciphertext_load_seal(self.h, C.c_char_p(b), len(b), C.byref(used)))
+        return used.value
+
+    def save_seal(self, compr=COMPR_ZSTD) -> bytes:
+        """Ciphertext::save(stream, compr_mode) in SEAL's wire format."""
+        n = C.c_uint64()
+        _check(lib().hec_ciphertext_save_seal(self.h, compr, None, 0, C.byref(n)))
+        buf = C.create_string_buffer(n.value)
+        _check(lib().hec_ciphertext_save_seal(self.h, compr, buf, n.value, C.byref(n)))
+        return buf.raw[: n.value]
+
 
 class Plaintext:
     def __init__(self, ctx: Context, data, scale):
@@ -531,10 +652,14 @@ class Plaintext:
 
 
 class KSwitchKey:
-    def __init__(self, ctx: Context, data=None, seed=None):
+    def __init__(self, ctx: Context, data=None, seed=None, seal_bytes: bytes | None = None):
         self.ctx = ctx
         h = C.c_void_p()
-        if data is not None:
+        if seal_bytes is not None:  # RelinKeys::load(context, in, size)
+            used = C.c_uint64()
+            _check(lib().hec_kswitch_key_load_seal(ctx.h, C.c_char_p(seal_bytes), len(seal_bytes), C.byref(h),
+                                                   C.byref(used)))
+        elif data is not None:
             a = np.ascontiguousarray(data, dtype=np.uint64)
             _check(lib().hec_kswitch_key_upload(ctx.h, _p(a), C.byref(h)))
         else:
@@ -566,6 +691,12 @@ class GaloisKeys:
 
     def has(self, elt):
         return bool(lib().hec_galois_keys_has(self.h, int(elt)))
+
+    def load_seal(self, b: bytes):
+        """GaloisKeys::load(context, in, size): every key list of a SEAL-serialized GaloisKeys."""
+        used = C.c_uint64()
+        _check(lib().hec_galois_keys_load_seal(self.h, C.c_char_p(b), len(b), C.byref(used)))
+        return used.value
 
     def __del__(self):
         try:

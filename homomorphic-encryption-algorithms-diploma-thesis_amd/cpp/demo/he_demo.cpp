@@ -9,6 +9,8 @@
 //          batched_col    (COL_OR_DIAG = 0: A col-batched x A^T)
 //          ops            (operator expressions: ((eval%gk%c0) << 5) * c1, relin, rescale, + c2 ...)
 //          matrix         (Matrix 2x2 elementwise-ciphertext matmul, he_linalg.cpp:202-236)
+//          server         (server.cpp:99-152 on SEAL-serialized parms, relin key and two ciphertexts; the
+//                          result written with Ciphertext::save)
 //          encode         (the demo's plaintexts: CKKSEncoder::encode of mat1's columns, the data of
 //                          matrix_operations.cpp:1079-1087 at dim = #ciphertexts in the input, scale 2^40,
 //                          matrix_operations.cpp:1106-1108; written as size-1 entries)
@@ -18,6 +20,7 @@
 #include <cstring>
 #include <fstream>
 #include <iostream>
+#include <iterator>
 #include <map>
 #include <string>
 #include <vector>
@@ -110,6 +113,33 @@ int main(int argc, char **argv)
         return 1;
     }
     const std::string mode = argv[1];
+    if (mode == "server") {
+        // src/demos/server.cpp:99-152 (server_demo's receive / compute / send) over the SEAL wire format: the input
+        // file is the client's network buffer (EncryptionParameters, RelinKeys, two Ciphertexts, as client.cpp
+        // writes them); the output file is res_ct.save(onet_strm), SEAL's default zstd compression
+        std::ifstream f(argv[2], std::ios::binary);
+        std::vector<char> raw((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+        const auto *inet_buf = reinterpret_cast<const hecdna::seal_byte *>(raw.data());
+        const std::streamoff inet_buf_sz = (std::streamoff)raw.size();
+        hecdna::EncryptionParameters parms;
+        std::streamoff inet_buf_curpos = 0;
+        inet_buf_curpos += parms.load(inet_buf + inet_buf_curpos, inet_buf_sz - inet_buf_curpos);
+        hecdna::Context sctx(parms);
+        hecdna::RelinKeys srk;
+        inet_buf_curpos += srk.load(sctx, inet_buf + inet_buf_curpos, inet_buf_sz - inet_buf_curpos);
+        Ciphertext op1_ct, op2_ct;
+        inet_buf_curpos += op1_ct.load(sctx, inet_buf + inet_buf_curpos, inet_buf_sz - inet_buf_curpos);
+        inet_buf_curpos += op2_ct.load(sctx, inet_buf + inet_buf_curpos, inet_buf_sz - inet_buf_curpos);
+        hecdna::Evaluator seval(sctx);
+        Ciphertext res_ct;
+        res_ct = seval % op1_ct * op2_ct;
+        res_ct &= seval % srk;  // relin
+        res_ct ^= seval;        // rescale
+        std::ofstream onet_strm(argv[3], std::ios::binary);
+        const std::streamoff n = res_ct.save(onet_strm);
+        std::cout << "he_demo server: read " << inet_buf_curpos << " bytes, wrote " << n << " bytes\n";
+        return 0;
+    }
     const Input in = read_input(argv[2]);
 
     hecdna::Context ctx(in.N, in.moduli);  // SEALContext ctx(parms)

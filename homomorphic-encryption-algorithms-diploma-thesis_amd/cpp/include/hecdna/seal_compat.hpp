@@ -18,7 +18,9 @@
 #include <complex>
 #include <cstddef>
 #include <cstdint>
+#include <ios>
 #include <memory>
+#include <ostream>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -45,8 +47,55 @@ struct CoeffModulus {
     }
 };
 
+// seal::compr_mode_type and the byte type of SEAL's buffer load/save overloads
+enum class compr_mode_type : std::uint8_t { none = HEC_COMPR_NONE, zlib = HEC_COMPR_ZLIB, zstd = HEC_COMPR_ZSTD };
+using seal_byte = std::byte;
+
+inline void seal_check(int rc)
+{
+    if (rc == HEC_EINVAL) throw std::invalid_argument(hec_seal_last_error());
+    if (rc != HEC_OK) throw std::logic_error(hec_seal_last_error());
+}
+
+// seal::EncryptionParameters (CKKS): the SEAL wire format load/save (server.cpp:110-112, client.cpp:82)
+class EncryptionParameters {
+public:
+    EncryptionParameters() = default;
+    EncryptionParameters(std::size_t poly_modulus_degree, std::vector<std::uint64_t> coeff_modulus)
+        : n_(poly_modulus_degree), q_(std::move(coeff_modulus)) {}
+    std::size_t poly_modulus_degree() const { return n_; }
+    const std::vector<std::uint64_t> &coeff_modulus() const { return q_; }
+    void set_poly_modulus_degree(std::size_t n) { n_ = n; }
+    void set_coeff_modulus(std::vector<std::uint64_t> q) { q_ = std::move(q); }
+    std::streamoff load(const seal_byte *in, std::size_t size)
+    {
+        std::uint64_t n = 0, k = 0, used = 0;
+        seal_check(hec_seal_parms_load(in, size, &n, nullptr, 0, &k, &used));
+        q_.resize(k);
+        seal_check(hec_seal_parms_load(in, size, &n, q_.data(), k, &k, &used));
+        n_ = n;
+        return (std::streamoff)used;
+    }
+    std::streamoff save(std::ostream &out, compr_mode_type mode = compr_mode_type::zstd) const
+    {
+        std::uint64_t w = 0;
+        seal_check(hec_seal_parms_save(n_, q_.data(), q_.size(), (int)mode, nullptr, 0, &w));
+        std::vector<char> b(w);
+        seal_check(hec_seal_parms_save(n_, q_.data(), q_.size(), (int)mode, b.data(), w, &w));
+        out.write(b.data(), (std::streamsize)w);
+        return (std::streamoff)w;
+    }
+
+private:
+    std::size_t n_ = 0;
+    std::vector<std::uint64_t> q_;
+};
+
 class Context {
 public:
+    // SEALContext ctx(parms) (server.cpp:112)
+    explicit Context(const EncryptionParameters &parms, int device = 0)
+        : Context(parms.poly_modulus_degree(), parms.coeff_modulus(), device) {}
     Context(std::size_t poly_modulus_degree, const std::vector<std::uint64_t> &coeff_modulus, int device = 0)
     {
         hec_context *c = nullptr;
@@ -139,6 +188,25 @@ public:
     std::size_t level() const { return info().level; }
     double scale() const { return info().scale; }
     const Context &context() const { return *ctx_; }
+    // SEAL wire format: Ciphertext::load(context, in, size) (server.cpp:120-121) returns the bytes read;
+    // save(stream, compr_mode) (server.cpp:140-141; SEAL's default compression is zstd)
+    std::streamoff load(const Context &ctx, const seal_byte *in, std::size_t size)
+    {
+        if (ctx_ != &ctx) { reset(); ctx_ = &ctx; }
+        ensure();
+        std::uint64_t used = 0;
+        check(hec_ciphertext_load_seal(h_, in, size, &used));
+        return (std::streamoff)used;
+    }
+    std::streamoff save(std::ostream &out, compr_mode_type mode = compr_mode_type::zstd) const
+    {
+        std::uint64_t w = 0;
+        check(hec_ciphertext_save_seal(h_, (int)mode, nullptr, 0, &w));
+        std::vector<char> b(w);
+        check(hec_ciphertext_save_seal(h_, (int)mode, b.data(), w, &w));
+        out.write(b.data(), (std::streamsize)w);
+        return (std::streamoff)w;
+    }
     hec_ciphertext *get() const { return h_; }
     // bind a default-constructed ciphertext to a context (used by out-of-place operations)
     void bind(const Context &ctx)
@@ -270,6 +338,15 @@ public:
         h_.reset(k, [](hec_kswitch_key *x) { hec_kswitch_key_destroy(x); });
     }
     hec_kswitch_key *get() const { return h_.get(); }
+    // RelinKeys::load(context, in, size) (server.cpp:116)
+    std::streamoff load(const Context &ctx, const seal_byte *in, std::size_t size)
+    {
+        hec_kswitch_key *k = nullptr;
+        std::uint64_t used = 0;
+        check(hec_kswitch_key_load_seal(ctx.get(), in, size, &k, &used));
+        h_.reset(k, [](hec_kswitch_key *x) { hec_kswitch_key_destroy(x); });
+        return (std::streamoff)used;
+    }
 
 private:
     std::shared_ptr<hec_kswitch_key> h_;
@@ -286,6 +363,14 @@ public:
     }
     void add(std::uint32_t galois_elt, const std::uint64_t *data) { check(hec_galois_keys_add(h_.get(), galois_elt, data)); }
     bool has_key(std::uint32_t galois_elt) const { return hec_galois_keys_has(h_.get(), galois_elt) != 0; }
+    // GaloisKeys::load(context, in, size): every key list present in the buffer
+    std::streamoff load(const Context &ctx, const seal_byte *in, std::size_t size)
+    {
+        if (!h_) *this = GaloisKeys(ctx);
+        std::uint64_t used = 0;
+        check(hec_galois_keys_load_seal(h_.get(), in, size, &used));
+        return (std::streamoff)used;
+    }
     hec_galois_keys *get() const { return h_.get(); }
 
 private:

@@ -1790,6 +1790,89 @@ int hec_galois_keys_destroy(hec_galois_keys *gk)
 }
 
 // ------------------------------------------------------------------ evaluator -------------
+// ---------------------------------------------------------------- SEAL wire format on device objects
+namespace {
+void seal_rc(int rc)
+{
+    if (rc == HEC_EINVAL) throw std::invalid_argument(hec_seal_last_error());
+    if (rc != HEC_OK) throw std::logic_error(hec_seal_last_error());
+}
+}  // namespace
+
+int hec_ciphertext_load_seal(hec_ciphertext *ct, const void *bytes, uint64_t nbytes, uint64_t *consumed)
+{
+    return guard([&] {
+        need(ct && bytes, "null argument");
+        Ctx &c = ct->ctx->c;
+        uint64_t size = 0, level = 0, N = 0, pid[4], used = 0;
+        double scale = 0;
+        seal_rc(hec_seal_ciphertext_load(bytes, nbytes, &size, &level, &N, &scale, pid, nullptr, 0, &used));
+        // Ciphertext::load(context, ...): the data must be valid for the context (is_valid_for)
+        need(N == c.N && level >= 1 && level <= c.L && size >= 2, "ciphertext data is invalid");
+        uint64_t want[4];
+        seal_rc(hec_seal_parms_id(c.N, c.q.data(), level, want));
+        need(std::memcmp(want, pid, 32) == 0, "ciphertext data is invalid");
+        std::vector<u64> host(size * level * N);
+        seal_rc(hec_seal_ciphertext_load(bytes, nbytes, nullptr, nullptr, nullptr, nullptr, nullptr, host.data(),
+                                         host.size(), nullptr));
+        const int rc = hec_ciphertext_upload(ct, host.data(), size, level, scale);
+        if (rc != HEC_OK) throw std::logic_error(hec_last_error());
+        if (consumed) *consumed = used;
+    });
+}
+
+int hec_ciphertext_save_seal(const hec_ciphertext *ct, int compr_mode, void *out, uint64_t cap, uint64_t *written)
+{
+    return guard([&] {
+        need(ct && ct->d, "null argument");
+        const Ctx &c = ct->ctx->c;
+        std::vector<u64> host(ct->size * ct->level * c.N);
+        const int rc = hec_ciphertext_download(ct, host.data());
+        if (rc != HEC_OK) throw std::logic_error(hec_last_error());
+        seal_rc(hec_seal_ciphertext_save(host.data(), ct->size, ct->level, c.N, ct->scale, c.q.data(), compr_mode, out,
+                                         cap, written));
+    });
+}
+
+int hec_kswitch_key_load_seal(hec_context *ctx, const void *bytes, uint64_t nbytes, hec_kswitch_key **out,
+                              uint64_t *consumed)
+{
+    return guard([&] {
+        need(ctx && bytes && out, "null argument");
+        const Ctx &c = ctx->c;
+        uint64_t words = 0, used = 0, lists = 0;
+        seal_rc(hec_seal_kswitch_keys_load(bytes, nbytes, 0, &lists, nullptr, 0, &words, &used));
+        need(lists >= 1 && words == c.L * 2 * c.K * c.N, "relin_keys is not valid for encryption parameters");
+        std::vector<u64> host(words);
+        seal_rc(hec_seal_kswitch_keys_load(bytes, nbytes, 0, nullptr, host.data(), words, nullptr, nullptr));
+        const int rc = hec_kswitch_key_upload(ctx, host.data(), out);
+        if (rc != HEC_OK) throw std::logic_error(hec_last_error());
+        if (consumed) *consumed = used;
+    });
+}
+
+int hec_galois_keys_load_seal(hec_galois_keys *gk, const void *bytes, uint64_t nbytes, uint64_t *consumed)
+{
+    return guard([&] {
+        need(gk && bytes, "null argument");
+        const Ctx &c = gk->ctx->c;
+        uint64_t lists = 0, used = 0;
+        seal_rc(hec_seal_kswitch_keys_load(bytes, nbytes, UINT64_MAX, &lists, nullptr, 0, nullptr, &used));
+        std::vector<u64> host;
+        for (uint64_t i = 0; i < lists; ++i) {  // GaloisKeys::get_index(elt) = (elt - 1) / 2
+            uint64_t words = 0;
+            seal_rc(hec_seal_kswitch_keys_load(bytes, nbytes, i, nullptr, nullptr, 0, &words, nullptr));
+            if (!words) continue;
+            need(words == c.L * 2 * c.K * c.N, "galois_keys is not valid for encryption parameters");
+            host.resize(words);
+            seal_rc(hec_seal_kswitch_keys_load(bytes, nbytes, i, nullptr, host.data(), words, nullptr, nullptr));
+            const int rc = hec_galois_keys_add(gk, (uint32_t)(2 * i + 1), host.data());
+            if (rc != HEC_OK) throw std::logic_error(hec_last_error());
+        }
+        if (consumed) *consumed = used;
+    });
+}
+
 int hec_negate_inplace(hec_context *ctx, hec_ciphertext *a)
 {
     return guard([&] {

@@ -195,6 +195,49 @@ int hec_matmul_diag_col_sharded(hec_context *ctx, const hec_ciphertext *const *d
                                 const hec_ciphertext *const *cols, uint64_t p, const hec_kswitch_key *rk,
                                 const hec_galois_keys *gk, hec_ciphertext *const *out);
 
+/* ---------------------------------------------------------------- SEAL wire format */
+/* seal::Serialization::Save / Load byte layouts of the objects the reference's socket layer exchanges
+ * (src/demos/client.cpp:113-115,238-240 saves, src/demos/server.cpp:110-122,140-152 loads): SEALHeader (16 B:
+ * magic 0xA15E, header size, version 4.1, compr_mode, size) + members, compr_mode HEC_COMPR_NONE / ZLIB / ZSTD
+ * (zlib, zstd loaded on first use).  Host-only functions return HEC_EINVAL with SEAL's wording for malformed
+ * input ("loaded SEALHeader is invalid", ...); hec_seal_last_error() holds the message.  Seeded ciphertexts
+ * (encrypt_symmetric().save(), client.cpp:113-114) must be expanded by the caller's SEAL (HEC_EINVAL). */
+#define HEC_COMPR_NONE 0
+#define HEC_COMPR_ZLIB 1
+#define HEC_COMPR_ZSTD 2
+const char *hec_seal_last_error(void);
+/* BLAKE2b (util::HashFunction behind parms_id), outlen <= 64 bytes */
+int hec_seal_blake2b(const void *in, uint64_t nbytes, uint64_t outlen, void *out);
+/* EncryptionParameters::parms_id() of CKKS {N, coeff_modulus[0..count)} (a ciphertext at level l: its l primes) */
+int hec_seal_parms_id(uint64_t poly_modulus_degree, const uint64_t *coeff_modulus, uint64_t count, uint64_t out[4]);
+/* Ciphertext::load / save on host buffers: data u64[size][level][N]; *consumed / *written = object bytes
+ * (out == NULL: size query) */
+int hec_seal_ciphertext_load(const void *bytes, uint64_t nbytes, uint64_t *size, uint64_t *level,
+                             uint64_t *poly_modulus_degree, double *scale, uint64_t parms_id[4], uint64_t *data,
+                             uint64_t data_words, uint64_t *consumed);
+int hec_seal_ciphertext_save(const uint64_t *data, uint64_t size, uint64_t level, uint64_t poly_modulus_degree,
+                             double scale, const uint64_t *coeff_modulus, int compr_mode, void *out, uint64_t cap,
+                             uint64_t *written);
+/* EncryptionParameters::load / save (CKKS) */
+int hec_seal_parms_load(const void *bytes, uint64_t nbytes, uint64_t *poly_modulus_degree, uint64_t *coeff_modulus,
+                        uint64_t cap, uint64_t *count, uint64_t *consumed);
+int hec_seal_parms_save(uint64_t poly_modulus_degree, const uint64_t *coeff_modulus, uint64_t count, int compr_mode,
+                        void *out, uint64_t cap, uint64_t *written);
+/* KSwitchKeys (RelinKeys, GaloisKeys) load of key list `index` (RelinKeys 0, GaloisKeys (galois_elt - 1) / 2)
+ * in the engine's key layout u64[L][2][K][N]; *lists = the object's list count, *words = that list's words */
+int hec_seal_kswitch_keys_load(const void *bytes, uint64_t nbytes, uint64_t index, uint64_t *lists, uint64_t *out,
+                               uint64_t cap_words, uint64_t *words, uint64_t *consumed);
+int hec_seal_kswitch_keys_save(uint64_t poly_modulus_degree, const uint64_t *coeff_modulus, uint64_t K,
+                               const uint64_t *const *keys, const uint64_t *digits, uint64_t nlists, int compr_mode,
+                               void *out, uint64_t cap, uint64_t *written);
+/* device objects: Ciphertext::load(context, ...) (checks N and the parms_id of its level against the context)
+ * and Ciphertext::save(stream, compr_mode); RelinKeys::load; GaloisKeys::load (every non-empty key list) */
+int hec_ciphertext_load_seal(hec_ciphertext *ct, const void *bytes, uint64_t nbytes, uint64_t *consumed);
+int hec_ciphertext_save_seal(const hec_ciphertext *ct, int compr_mode, void *out, uint64_t cap, uint64_t *written);
+int hec_kswitch_key_load_seal(hec_context *ctx, const void *bytes, uint64_t nbytes, hec_kswitch_key **out,
+                              uint64_t *consumed);
+int hec_galois_keys_load_seal(hec_galois_keys *gk, const void *bytes, uint64_t nbytes, uint64_t *consumed);
+
 /* ---------------------------------------------------------------- primitives (cfg2) ------- */
 /* In-place batched negacyclic NTT over device data u64[npolys][nlimbs][N]; limb j uses prime
  * limb0 + j (SEAL ntt_negacyclic_harvey / inverse_ntt_negacyclic_harvey, canonical in/out). */

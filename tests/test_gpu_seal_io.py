@@ -1,0 +1,76 @@
+"""SEAL wire format on device objects: Ciphertext::load(context, ...) / save, RelinKeys::load,
+GaloisKeys::load through the C ABI, and the reference server's receive → compute → send flow
+(src/demos/server.cpp:99-152) run by the C++ drop-in on SEAL-serialized inputs, bit-exact against the oracle.
+The input bytes come from the independent Python restatement of the layout (tests/seal_format.py); parity of
+the format against SEAL itself is unpinned (no SEAL-written bytes exist under /root/reference)."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import seal_format as sf
+from test_gpu_parity import Env
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "homomorphic-encryption-algorithms-diploma-thesis_amd")
+
+
+@pytest.fixture(scope="module")
+def env(orc, hecdna):
+    return Env(orc, hecdna, 1 << 11, [50, 36, 36, 50], seed=41)
+
+
+def test_ciphertext_load_save_on_device(env, hecdna):
+    e = env
+    ct = e.enc(seed=1)
+    for b in (sf.ciphertext(ct.data, ct.scale, e.m), sf.ciphertext(ct.data, ct.scale, e.m, compr=1)):
+        g = hecdna.Ciphertext(e.ctx)
+        assert g.load_seal(b + b"tail") == len(b)
+        e.same(g, ct)
+    g = e.up(ct)
+    assert g.save_seal(hecdna.COMPR_NONE) == sf.ciphertext(ct.data, ct.scale, e.m)
+    h = hecdna.Ciphertext(e.ctx)
+    h.load_seal(g.save_seal())                                   # zstd round trip
+    e.same(h, ct)
+    low = e.ctx.rescale_to_next(e.up(ct))                        # a lower level: the parms_id of its 2 primes
+    assert low.save_seal(hecdna.COMPR_NONE)[16:48] == sf.parms_id(e.N, e.m[:2]).tobytes()
+    wrong = sf.ciphertext(ct.data, ct.scale, e.m, pid=sf.parms_id(e.N, e.m[:2]))
+    with pytest.raises(hecdna.InvalidArgument, match="ciphertext data is invalid"):
+        hecdna.Ciphertext(e.ctx).load_seal(wrong)
+
+
+def test_keys_load_on_device(env, hecdna):
+    e = env
+    rk = hecdna.KSwitchKey(e.ctx, seal_bytes=sf.kswitch_keys(e.N, e.m, [e.rk_h]))
+    a = e.rand_ct(3, 3, 2.0**60)
+    e.same(e.ctx.relinearize(e.up(a), rk), e.o.relinearize(a, e.rk_h))
+    elts = sorted(e.gk_h)
+    lists = [None] * ((max(elts) - 1) // 2 + 1)
+    for elt in elts:
+        lists[(elt - 1) // 2] = e.gk_h[elt]
+    gk = hecdna.GaloisKeys(e.ctx)
+    gk.load_seal(sf.kswitch_keys(e.N, e.m, lists))
+    assert all(gk.has(elt) for elt in elts)
+    b = e.rand_ct(2, 3)
+    e.same(e.ctx.rotate_vector(e.up(b), 7, gk), e.o.rotate(b, 7, e.gk_h))
+
+
+def test_server_flow_on_seal_bytes(env, hecdna, tmp_path):
+    """he_demo server = server.cpp:99-152 with hecdna:: types: EncryptionParameters / RelinKeys / 2 Ciphertexts loaded
+    from the client's buffer, res = relin(op1 * op2) rescaled, saved with Ciphertext::save (zstd)."""
+    e = env
+    op1, op2 = e.enc(seed=11), e.enc(seed=12)
+    buf = (sf.parms(e.N, e.m) + sf.kswitch_keys(e.N, e.m, [e.rk_h]) + sf.ciphertext(op1.data, op1.scale, e.m)
+           + hecdna.seal_ciphertext_save(op2.data, op2.scale, e.m))   # the second operand zstd-compressed
+    inp, outp = tmp_path / "client.bin", tmp_path / "server.bin"
+    inp.write_bytes(buf)
+    subprocess.check_call(["make", "-s", "-C", PKG, "bin/he_demo"])
+    subprocess.check_call([os.path.join(PKG, "bin", "he_demo"), "server", str(inp), str(outp)])
+    res = outp.read_bytes()
+    assert res[5] == hecdna.COMPR_ZSTD
+    data, scale, pid, used = hecdna.seal_ciphertext_load(res)
+    exp = e.o.rescale(e.o.relinearize(e.o.multiply(op1, op2), e.rk_h))
+    assert used == len(res) and np.array_equal(data, exp.data) and scale == exp.scale
+    assert np.array_equal(pid, sf.parms_id(e.N, e.m[:exp.level]))
