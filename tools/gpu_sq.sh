@@ -1,7 +1,7 @@
 #!/bin/bash
 # SQ counters (one pass, 8 slots) for the dominant kernels on a small bench run
 set -o pipefail
-OUT=$GRAFT_REPO_ROOT/gpurun_out/sq
+OUT=$GRAFT_REPO_ROOT/gpurun_out/${1:-sq}
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
 export HEC_LANES=1  # one lane: per-kernel counters of whole-batch launches
