@@ -9,6 +9,7 @@
 //          batched_col    (COL_OR_DIAG = 0: A col-batched x A^T)
 //          ops            (operator expressions: ((eval%gk%c0) << 5) * c1, relin, rescale, + c2 ...)
 //          matrix         (Matrix 2x2 elementwise-ciphertext matmul, he_linalg.cpp:202-236)
+//          matrix_family  (left_matmul_with_transp, matmul_square, matmul_pow, he_linalg.cpp:241-349)
 //          server         (server.cpp:99-152 on SEAL-serialized parms, relin key and two ciphertexts; the
 //                          result written with Ciphertext::save)
 //          encode         (the demo's plaintexts: CKKSEncoder::encode of mat1's columns, the data of
@@ -202,6 +203,21 @@ int main(int argc, char **argv)
         BatchedMatrix m(BatchedMatrix::BatchingType::col, std::move(bvecs));
         BatchedMatrix s = m.sum_bvec_elems(eval, gk);
         for (const auto &b : s.get_bvecs()) keep.push_back(b.get_bvec());
+    } else if (mode == "matrix_family") {
+        // Matrix::left_matmul_with_transp, matmul_square, matmul_pow (he_linalg.cpp:241-349) on the first four
+        // ciphertexts as a 2x2 column-major matrix, then matmul_pow(3), which needs operands of two levels
+        // (A and A^2): SEAL throws there, and so must the drop-in (the last output is a marker)
+        Matrix A(2, 2, std::vector<Ciphertext>(cts.begin(), cts.begin() + 4));
+        for (const auto &m : {A.left_matmul_with_transp(eval, rk), A.matmul_square(eval, rk), A.matmul_pow(eval, rk, 2),
+                              A.matmul_pow(eval, rk, 4)})
+            for (const auto &c : m.get_elems()) keep.push_back(c);
+        bool threw = false;
+        try {
+            (void)A.matmul_pow(eval, rk, 3);
+        } catch (const std::invalid_argument &e) {
+            threw = std::string(e.what()).find("mismatch") != std::string::npos;
+        }
+        keep.push_back(threw ? cts[0] : cts[1]);
     } else if (mode == "matrix") {
         // Matrix::matmul on 2x2 element-wise ciphertext matrices (column-major elems)
         Matrix A(2, 2, std::vector<Ciphertext>(cts.begin(), cts.begin() + 4));

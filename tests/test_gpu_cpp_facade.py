@@ -178,3 +178,27 @@ def test_demo_sum_elems(demo, small, tmp_path, dim):
     if dim == 10:
         d = o.decode(o.decrypt(sk, exp[0]), exp[0].scale).real
         assert abs(d[0] - 92.0) < 1e-5
+
+
+def test_demo_matrix_family(demo, orc, tmp_path):
+    """Matrix::left_matmul_with_transp (A^T A), matmul_square (A A) and matmul_pow (square-and-multiply,
+    he_linalg.cpp:241-349) through the C++ drop-in, bit-exact against the oracle's Matrix::matmul on the same
+    operands; matmul_pow(3) multiplies A by A^2 across two levels, which SEAL rejects ("parameter mismatch"),
+    and so does the drop-in."""
+    N = 1 << 11
+    m = orc.Oracle.create_coeff_modulus(N, [50, 36, 36, 50])
+    o = orc.Oracle(N, m)
+    sk = o.secret_key(61)
+    rk = o.relin_key(sk, 62)
+    rng = np.random.default_rng(63)
+    scale = 2.0**30
+    A = [o.encrypt(sk, o.encode(rng.uniform(-1, 1, N // 2), scale, 3), scale, 70 + i) for i in range(4)]
+    out = run(demo, "matrix_family", tmp_path, N, m, A, rk, {})
+    AtA = o.matrix_matmul(A, 2, 2, True, A, 2, 2, False, rk)
+    A2 = o.matrix_matmul(A, 2, 2, False, A, 2, 2, False, rk)
+    A4 = o.matrix_matmul(A2, 2, 2, False, A2, 2, 2, False, rk)
+    exp = AtA + A2 + A2 + A4
+    assert len(out) == 17
+    for g, e in zip(out[:16], exp):
+        same(g, e)
+    same(out[16], A[0])  # the matmul_pow(3) level-mismatch error was raised
