@@ -907,7 +907,7 @@ void matvec_core(hec_context *ctx, const hec_ciphertext *const *diags, const hec
 // cycles), so the batch of a matvec is split into up to c.lanes sub-batches of at least
 // c.lane_min_batch vectors that run the same trie walk concurrently, each from its own host thread on its
 // own HIP stream and workspace.  Outputs are independent per input vector, so the bits are unchanged.
-hec_context *make_lane(hec_context *parent)
+hec_context *make_lane(hec_context *parent, int index)
 {
     auto *l = new hec_context();
     Ctx &c = l->c;
@@ -921,7 +921,19 @@ hec_context *make_lane(hec_context *parent)
     c.stream = c.side = nullptr;
     c.ev_fork = c.ev_join = nullptr;
     c.zflag = nullptr;
-    HEC_HIP(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
+    if (c.lane_cumask != 0 && c.lanes > 1) {  // the lane's own share of the CUs
+        hipDeviceProp_t prop;
+        HEC_HIP(hipGetDeviceProperties(&prop, c.device));
+        const int ncu = prop.multiProcessorCount, n = c.lanes, i = index % n;
+        std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+        for (int cu = 0; cu < ncu; ++cu) {
+            const bool mine = c.lane_cumask == 1 ? cu % n == i : (cu % 32) * n / 32 == i;
+            if (mine) mask[cu / 32] |= 1u << (cu % 32);
+        }
+        HEC_HIP(hipExtStreamCreateWithCUMask(&c.stream, (uint32_t)mask.size(), mask.data()));
+    } else {
+        HEC_HIP(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
+    }
     c.own_stream = true;
     HEC_HIP(hipStreamCreateWithFlags(&c.side, hipStreamNonBlocking));
     HEC_HIP(hipEventCreateWithFlags(&c.ev_fork, hipEventDisableTiming));
@@ -960,7 +972,7 @@ void matvec_lanes(hec_context *ctx, const hec_ciphertext *const *diags, const he
             galois_kw(ctx, gkm, kv.first, (int)cols[0]->level);
         }
     }
-    while ((int)ctx->lanes.size() < nl) ctx->lanes.push_back(make_lane(ctx));
+    while ((int)ctx->lanes.size() < nl) ctx->lanes.push_back(make_lane(ctx, (int)ctx->lanes.size()));
     hipEvent_t start;
     HEC_HIP(hipEventCreateWithFlags(&start, hipEventDisableTiming));
     HEC_HIP(hipEventRecord(start, c.stream));  // the inputs were produced on the context's stream
@@ -1187,8 +1199,10 @@ int hec_context_create(uint64_t N, const uint64_t *mod, uint64_t K, int device, 
         if (const char *f = std::getenv("HEC_FUSE_GALOIS")) c.fuse_galois = f[0] != '0';
         if (const char *f = std::getenv("HEC_FAN")) c.fan_out = f[0] != '0';
         if (const char *f = std::getenv("HEC_FAN2")) c.fan2 = std::atoi(f);
+        if (const char *f = std::getenv("HEC_FANSPLIT")) c.fan_split = std::atoi(f);
         if (const char *f = std::getenv("HEC_TENSOR_BG")) c.tensor_bg = std::atoi(f);
         if (const char *f = std::getenv("HEC_LANES")) c.lanes = std::max(1, std::atoi(f));
+        if (const char *f = std::getenv("HEC_LANE_CUMASK")) c.lane_cumask = std::atoi(f);
         if (const char *f = std::getenv("HEC_FANG"))
             std::sscanf(f, "%d,%d,%d", &c.fan_groups_moddown, &c.fan_groups_modup, &c.fan_groups_hoist);
         if (const char *f = std::getenv("HEC_HOIST")) c.hoist = f[0] != '0';

@@ -88,10 +88,15 @@ struct Ctx {
     int fan_groups_moddown = 1;    // HEC_FANG="moddown,modup,hoist": target groups per k_fan source (blocks
     int fan_groups_modup = 1;      // per launch x groups; the source's inverse pass is repeated per group)
     int fan_groups_hoist = 1;
+    int fan_split = 1;             // HEC_FANSPLIT=0: Barrett (not the FP64 split) for the mod-down rounding limbs
+                                   // at FP64 targets (FanDivRound::xf16)
     int fan2 = 1;                  // HEC_FAN2=0: the LDS-round k_fan instead of the register-direct k_fan2
     bool fan_out = true;           // HEC_FAN=0: separate INTT pass A (fan-out fuses it into the forward passes A)
     int lanes = 3;                 // HEC_LANES: concurrent batch lanes of a matvec (hec_engine.hip matvec_lanes)
     int lane_min_batch = 16;       // input vectors per lane at least
+    int lane_cumask = 0;           // HEC_LANE_CUMASK: 0 lanes share every CU; 1 lane i of n owns the CUs with
+                                   // index % n == i; 2 a contiguous range of every 32 (hipExtStreamCreateWithCUMask; either
+                                   // way each lane keeps CUs on all 8 XCDs)
     bool fuse_galois = true;       // HEC_FUSE_GALOIS=0: materialise apply_galois before the key switch
     bool fused_modup_mac = true;  // HEC_FUSED_MODUP_MAC=0: separate mod-up pass B and key MAC kernels
     // profiling (ProfScope in hec_engine.hip)

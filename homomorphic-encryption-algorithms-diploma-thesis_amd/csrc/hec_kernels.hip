@@ -513,6 +513,7 @@ struct FanModUpT {  // source (b, J) = D[b][J] (inverse pass-B domain) -> E[b][I
         return Tgt{I != J, p, E + (((u64)((b * (l + 1) + I) * l + J)) << logN), qI, primes[p].r1,
                    qJ <= qI ? 0 : (qJ <= 2 * qI ? 1 : 2)};
     }
+    __device__ u64 src_fix(u64 d) const { return d; }
     __device__ u64 xf(const Tgt &t, u64 d) const
     {
         return t.red == 0 ? d : t.red == 1 ? csub(d, t.q) : barrett64(d, t.q, t.r1);
@@ -549,24 +550,41 @@ struct FanDivRound {  // source (b, k) = last limb (inverse pass-B domain) -> Z[
     u64 last, half;
     const DevPrime *primes;
     u64 fix[HEC_MAXL];
+    double c30[HEC_MAXL];  // 2^30 mod q_i (split reduction at FP64 targets with q_i > 2^32, else 0)
     struct Src { const u64 *in; int prime; };
-    struct Tgt { bool valid; int prime; u64 *out; u64 q, r1, fix; };
+    struct Tgt { bool valid; int prime; u64 *out; u64 q, r1, fix; double qd, qinv, c30; };
     __device__ int ntargets() const { return nl; }
     __device__ Src src(int job) const { return Src{Y + (u64)(job / nk) * ysb + (u64)(job % nk) * ysk, last_idx}; }
     __device__ Tgt tgt(int job, int i) const
     {
-        return Tgt{true, i, Z + ((u64)(job * nl + i) << logN), primes[i].q, primes[i].r1, fix[i]};
+        const DevPrime &p = primes[i];
+        return Tgt{true, i, Z + ((u64)(job * nl + i) << logN), p.q, p.r1, fix[i], p.qd, p.qinv, c30[i]};
     }
-    __device__ u64 xf(const Tgt &t, u64 d) const
+    // y -> (y + floor(P/2)) mod P, once per source value (the rounding offset is the same for every target)
+    __device__ u64 src_fix(u64 d) const
     {
-        u64 v = d + half;
-        v = v >= last ? v - last : v;
-        return barrett64(v, t.q, t.r1) + t.fix;
+        const u64 v = d + half;
+        return v >= last ? v - last : v;
     }
-    // (an FP64 split reduction here, (y >> 32) (2^32 mod q_i) by the exact FP64 product plus the low word,
-    // measured slower: 276 VGPRs, one wave per SIMD, mod-down fan-out 1,396 vs 1,045 ms per step)
+    __device__ u64 xf(const Tgt &t, u64 d) const { return barrett64(d, t.q, t.r1) + t.fix; }
+    // FP64 targets with q_i > 2^32: y = hi 2^30 + lo, y mod q_i == fp_mulmod(hi, 2^30 mod q_i) + lo (+ fix), an
+    // integer-valued double in (-0.53 q_i, 1.53 q_i + 2^30) within the FP64 forward NTT's |x| < 2 q_i input range
+    // (no 64-bit Barrett: ~8 FP64 operations per value instead of 7 integer multiplies).  Smaller FP64 primes
+    // and the integer targets keep Barrett.
     __device__ void xf16(const Tgt &t, bool fp, const u64 *d, u64 *v) const
     {
+        if (fp && t.c30 != 0.0) {
+            const double fx = (double)t.fix;
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                u64 y = d[k];
+                asm volatile("" : "+v"(y));  // per target: hoisting the 32 split doubles out of the target loop
+                                             // would keep them live beside d (274 VGPRs, one wave per SIMD)
+                const double hi = u2d(y >> 30), lo = u2d(y & 0x3fffffffull);
+                v[k] = (u64)__double_as_longlong(fp_mulmod(hi, t.c30, t.qd, t.qinv) + (lo + fx));
+            }
+            return;
+        }
 #pragma unroll
         for (int k = 0; k < 16; ++k) v[k] = xf(t, d[k]);
         if (fp) {
@@ -623,6 +641,7 @@ __global__ void __launch_bounds__(NSEG *(1 << LOGP) / 16)
             const u64 v = lds[lidx(it)];
             if (ps.fp) d[it] = fp_canon(fp_mulmod(__longlong_as_double((long long)v), ps.ninv_d, ps.qd, ps.qinv), ps.qd, ps.qinv);
             else d[it] = shoup(v, ps.ninv, ps.ninv_q, ps.q);
+            d[it] = fan.src_fix(d[it]);
         }
     }
     // target group blockIdx.z of gridDim.z: more blocks per launch when the job count is small (the
@@ -739,6 +758,8 @@ __global__ void __launch_bounds__(NSEG *(1 << LOGP) / 16)
 #pragma unroll
             for (int k = 0; k < 16; ++k) d[k] = shoup(v[k], ps.ninv, ps.ninv_q, ps.q);
         }
+#pragma unroll
+        for (int k = 0; k < 16; ++k) d[k] = fan.src_fix(d[k]);
     }
     const int nt = fan.ntargets(), t0 = blockIdx.z * nt / gridDim.z, t1 = (blockIdx.z + 1) * nt / gridDim.z;
     for (int t = t0; t < t1; ++t) {
@@ -1242,6 +1263,7 @@ void fan_divide_round(Ctx &c, const u64 *Y, u64 ysb, u64 ysk, u64 *Z, int B, int
     f.last = c.q[last_idx]; f.half = f.last >> 1; f.primes = c.primes;
     for (int i = 0; i < nl; ++i) {
         f.fix[i] = c.q[i] - (f.half % c.q[i]);
+        f.c30[i] = c.fan_split && c.q[i] < (1ull << 42) && c.q[i] > (1ull << 32) ? (double)((1ull << 30) % c.q[i]) : 0.0;
     }
     fan_dispatch(c, B * nk, f, std::min(c.fan_groups_moddown, nl));
 }
