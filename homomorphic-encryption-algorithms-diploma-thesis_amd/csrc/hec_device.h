@@ -33,6 +33,18 @@ __device__ __forceinline__ u64 shoup(u64 x, u64 w, u64 wq, u64 q) { return csub(
 // SEAL util::barrett_reduce_64: any 64-bit x -> x mod q
 __device__ __forceinline__ u64 barrett64(u64 x, u64 q, u64 r1) { return csub(x - mulhi64(x, r1) * q, q); }
 
+// full 64x64 -> 128 product from the four 32x32 -> 64 partial products (v_mad_u64_u32 each); the compiler's
+// separate a * b and __umul64hi(a, b) take six multiplies
+__device__ __forceinline__ void mul128(u64 a, u64 b, u64 &lo, u64 &hi)
+{
+    const u32 a0 = (u32)a, a1 = (u32)(a >> 32), b0 = (u32)b, b1 = (u32)(b >> 32);
+    const u64 p00 = (u64)a0 * b0;
+    const u64 p01 = (u64)a0 * b1 + (p00 >> 32);  // < 2^64
+    const u64 p10 = (u64)a1 * b0 + (u32)p01;     // < 2^64
+    hi = (u64)a1 * b1 + ((p01 >> 32) + (p10 >> 32));
+    lo = (p10 << 32) | (u32)p00;
+}
+
 // SEAL util::barrett_reduce_128: 128-bit (hi:lo) -> mod q
 __device__ __forceinline__ u64 barrett128(u64 lo, u64 hi, u64 q, u64 r0, u64 r1)
 {
@@ -59,7 +71,8 @@ struct U128 {
 };
 __device__ __forceinline__ void mac128(U128 &acc, u64 a, u64 b)
 {
-    const u64 plo = a * b, phi = mulhi64(a, b);
+    u64 plo, phi;
+    mul128(a, b, plo, phi);
     acc.lo += plo;
     acc.hi += phi + (acc.lo < plo);
 }

@@ -231,25 +231,18 @@ struct LdsTw {  // entry k = 2^s - 1 + i of this segment; FP: one word (double b
     }
 };
 
-template <int LOGP, int S0, int S1, int EPT, bool INV, bool FP, bool TO_REG, class AddrF, class TwG>
-__device__ __forceinline__ void ntt_round_g(u64 *lds, const AddrF &addr, int ts, const TwG &twg, const DevPrime &pr,
-                                            u64 *regs)
-{
-    constexpr int LE = EPT == 16 ? 4 : EPT == 8 ? 3 : EPT == 4 ? 2 : 1;
-    constexpr int D = S1 - S0, G = 1 << (LE - D), NQ = 1 << D;
-    static_assert(D >= 1 && D <= LE, "round covers 1..log2(EPT) stages");
-    const u64 q = pr.q, two_q = 2 * q;
-#pragma unroll
-    for (int gi = 0; gi < G; ++gi) {
-        const int g = ts * G + gi;
-        const int lo = g & ((1 << (LOGP - S1)) - 1);
-        const int hi = g >> (LOGP - S1);
-        const int xb = (hi << (LOGP - S0)) | lo;
-        // the group's 2^D - 1 twiddles do not depend on data: issue their loads before the LDS
-        // reads so their latency overlaps.  Round-stage st uses index twidx(S0+st, hi 2^st + m),
-        // m = a >> (D - st) the top st bits of the element slot a.
-        double wf[FP ? NQ - 1 : 1];
-        ulonglong2 wi[FP ? 1 : NQ - 1];
+// The D = S1 - S0 stages of one element group (NQ = 2^D registers): group g of a round, hi = its index above
+// the round's stages.  Round-stage st uses twiddle twidx(S0+st, hi 2^st + m), m = a >> (D - st) the top st bits
+// of the element slot a.  The group's 2^D - 1 twiddles do not depend on data: GroupTw loads them first, so their
+// latency overlaps the data loads.
+template <int S0, int D, bool FP>
+struct GroupTw {
+    static constexpr int NQ = 1 << D;
+    double wf[FP ? NQ - 1 : 1];
+    ulonglong2 wi[FP ? 1 : NQ - 1];
+    template <class TwG>
+    __device__ __forceinline__ void load(int hi, const TwG &twg)
+    {
 #pragma unroll
         for (int st = 0; st < D; ++st)
 #pragma unroll
@@ -257,9 +250,11 @@ __device__ __forceinline__ void ntt_round_g(u64 *lds, const AddrF &addr, int ts,
                 if constexpr (FP) wf[(1 << st) - 1 + m] = twg.f(S0 + st, (hi << st) | m);
                 else wi[(1 << st) - 1 + m] = twg.w(S0 + st, (hi << st) | m);
             }
-        u64 v[NQ];
-#pragma unroll
-        for (int a = 0; a < NQ; ++a) v[a] = lds[addr(xb | (a << (LOGP - S1)))];
+    }
+    template <bool INV>
+    __device__ __forceinline__ void run(u64 *v, const DevPrime &pr) const
+    {
+        const u64 q = pr.q, two_q = 2 * q;
 #pragma unroll
         for (int k = 0; k < D; ++k) {
             const int st = INV ? D - 1 - k : k;
@@ -280,6 +275,30 @@ __device__ __forceinline__ void ntt_round_g(u64 *lds, const AddrF &addr, int ts,
                 }
             }
         }
+    }
+};
+
+// One round (stages [S0, S1)) of a P = 2^LOGP point transform through LDS: thread ts owns G = EPT / 2^D groups;
+// group g holds the elements xb | (a << (LOGP - S1)), xb = (hi << (LOGP - S0)) | lo, g = hi 2^(LOGP - S1) + lo.
+template <int LOGP, int S0, int S1, int EPT, bool INV, bool FP, bool TO_REG, class AddrF, class TwG>
+__device__ __forceinline__ void ntt_round_g(u64 *lds, const AddrF &addr, int ts, const TwG &twg, const DevPrime &pr,
+                                            u64 *regs)
+{
+    constexpr int LE = EPT == 16 ? 4 : EPT == 8 ? 3 : EPT == 4 ? 2 : 1;
+    constexpr int D = S1 - S0, G = 1 << (LE - D), NQ = 1 << D;
+    static_assert(D >= 1 && D <= LE, "round covers 1..log2(EPT) stages");
+#pragma unroll
+    for (int gi = 0; gi < G; ++gi) {
+        const int g = ts * G + gi;
+        const int lo = g & ((1 << (LOGP - S1)) - 1);
+        const int hi = g >> (LOGP - S1);
+        const int xb = (hi << (LOGP - S0)) | lo;
+        GroupTw<S0, D, FP> gt;
+        gt.load(hi, twg);
+        u64 v[NQ];
+#pragma unroll
+        for (int a = 0; a < NQ; ++a) v[a] = lds[addr(xb | (a << (LOGP - S1)))];
+        gt.template run<INV>(v, pr);
 #pragma unroll
         for (int a = 0; a < NQ; ++a) {
             if constexpr (TO_REG) regs[gi * NQ + a] = v[a];
