@@ -88,6 +88,7 @@ struct Ctx {
     int fan_groups_moddown = 1;    // HEC_FANG="moddown,modup,hoist": target groups per k_fan source (blocks
     int fan_groups_modup = 1;      // per launch x groups; the source's inverse pass is repeated per group)
     int fan_groups_hoist = 1;
+    int ntt_rd = 1;                // HEC_NTT_RD=0: k_ntt stages every round through LDS (ntt_pass_body)
     int fan_split = 1;             // HEC_FANSPLIT=0: Barrett (not the FP64 split) for the mod-down rounding limbs
                                    // at FP64 targets (FanDivRound::xf16)
     int fan2 = 1;                  // HEC_FAN2=0: the LDS-round k_fan instead of the register-direct k_fan2

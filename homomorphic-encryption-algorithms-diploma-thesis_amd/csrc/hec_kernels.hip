@@ -410,18 +410,154 @@ __device__ __forceinline__ void ntt_pass_body(u64 *lds, const Bound &bio, const 
     }
 }
 
+// ------------------------------------------------------------------ register-direct NTT pass (RD)
+// One round on 16 register-resident elements (the twiddles of each group issued first): thread ts holds, for
+// stages [S0, S1), v[gi 2^D + a] <-> x = xb(ts G + gi) | (a << (LOGP - S1)) as in ntt_round_g.
+template <int LOGP, int S0, int S1, bool INV, bool FP, class TwG>
+__device__ __forceinline__ void ntt_round_rg(u64 *v, int ts, const TwG &twg, const DevPrime &pr)
+{
+    constexpr int D = S1 - S0, G = 1 << (4 - D), NQ = 1 << D;
+    static_assert(D >= 1 && D <= 4, "round covers 1..4 stages");
+#pragma unroll
+    for (int gi = 0; gi < G; ++gi) {
+        GroupTw<S0, D, FP> gt;
+        gt.load((ts * G + gi) >> (LOGP - S1), twg);
+        gt.template run<INV>(v + gi * NQ, pr);
+    }
+}
+
+// LDS word stride of a pass-B chunk in ntt_pass_body_rd: at least P + P/8 (two pad words per 16 elements) and
+// 16 mod 32, so the 16-B pair reads of two chunks fill the 64 banks and the 16-element block reads of 8 threads
+// land 36 dwords apart
+constexpr int nttb_ld(int logp) { return ((1 << logp) + (1 << logp) / 8 + 15) / 32 * 32 + 16; }
+
+// A pass of the two-pass NTT with its rounds on registers (k_fan2's scheme for k_ntt).  Rounds [0, SM) and
+// [SM, LOGP), SM = LOGP - 4, on two element sets of a P-point column / chunk per thread ts:
+//   set 0 (stages [0, SM)): x0(k) = ts G0 + k / 2^SM + 16 (k % 2^SM), G0 = 2^(4 - SM)
+//                           (pass A at P = 256: the stride set ts + 16 k; pass B at P = 128: pairs x, x + 1)
+//   set 1 (stages [SM, LOGP)): x1(k) = 16 ts + k (the block set).
+// Pass A (columns, lanes = consecutive columns): both sets load and store coalesced, so a pass exchanges
+// through LDS once instead of three times.  Pass B (contiguous chunks, lanes = consecutive pairs of a chunk):
+// set 0 is coalesced (16-B pairs), set 1 is not, so the forward pass stores through one more exchange and the
+// inverse pass loads through one (two exchanges instead of three).
+template <int LOGP, int NSEG, bool INV, bool PASS_A, bool FINAL, bool FP, class Bound>
+__device__ __forceinline__ void ntt_pass_body_rd(u64 *lds, const Bound &bio, const DevPrime &pr, const TwTables &tt,
+                                                 int logN)
+{
+    constexpr int P = 1 << LOGP, TPS = P / 16, SM = LOGP - 4, NQ0 = 1 << SM, G0 = 16 / NQ0;
+    constexpr int LDA = NSEG + 1, LDB = nttb_ld(LOGP), TILE = PASS_A ? P * LDA : NSEG * LDB;
+    constexpr bool FIRST = !FINAL;
+    static_assert(LOGP >= 5 && LOGP <= 8, "two rounds: [0, LOGP - 4) and 4 stages");
+    const u64 q = pr.q, two_q = 2 * q;
+    const int seg0 = blockIdx.x * NSEG, lc = logN - LOGP;
+    const ulonglong2 *tw = (PASS_A ? tt.a : tt.b) + ((u64)bio.prime << logN);
+    const double *twf = (PASS_A ? tt.fa : tt.fb) + ((u64)bio.prime << logN);
+    const int ts = PASS_A ? (int)threadIdx.x / NSEG : (int)threadIdx.x % TPS;
+    const int sg = PASS_A ? (int)threadIdx.x % NSEG : (int)threadIdx.x / TPS;
+    auto gidx = [&](int x) -> u64 { return PASS_A ? ((u64)x << lc) + seg0 + sg : ((u64)(seg0 + sg) << LOGP) + x; };
+    auto addr = [sg](int x) { return PASS_A ? x * LDA + sg : sg * LDB + x + 2 * (x >> 4); };
+    auto x0 = [ts](int k) { return ts * G0 + k / NQ0 + 16 * (k % NQ0); };
+    auto x1 = [ts](int k) { return 16 * ts + k; };
+    const u64 R = 1ull << lc, chunk = (u64)(seg0 + sg);
+    auto twidx = [=](int s, int i) -> u64 {
+        if constexpr (PASS_A) return (1ull << s) + (u64)i;
+        else return R * ((1ull << s) - 1) + (u64)i * R + chunk;
+    };
+    const GlobalTw<decltype(twidx)> twg{twidx, tw, twf};
+    constexpr bool IN_X1 = INV;              // the first round's set: forward set 0, inverse set 1
+    constexpr bool OUT_X1 = !INV;            // the last round's set
+    constexpr bool IN_T = !PASS_A && IN_X1;  // pass B loads set 1 through an LDS transposition
+    constexpr bool OUT_T = !PASS_A && OUT_X1;
+    auto xin = [&](int k) { return (IN_X1 && !IN_T) ? x1(k) : x0(k); };    // loaded positions
+    auto xout = [&](int k) { return (OUT_X1 && !OUT_T) ? x1(k) : x0(k); }; // stored positions
+    // one LDS tile (a second one would halve the pass-B blocks per CU); a barrier before each reuse
+    u64 *t0 = lds, *t1 = lds;
+    auto ad0 = [&](int x) { return addr(x); };
+    (void)TILE;
+
+    u64 v[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        u64 t = bio.load(gidx(xin(k)));
+        if constexpr (FP && FIRST) t = (u64)__double_as_longlong(u2d(t));  // integer input -> double bits
+        v[k] = t;
+    }
+    typename Bound::Pre pre[FINAL ? 16 : 1];  // post-op operands of the outputs, issued before the rounds
+    if constexpr (FINAL) {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) pre[k] = bio.pre(gidx(xout(k)));
+    }
+    if constexpr (IN_T) {  // pass B inverse: loaded as set 0, the first round needs set 1
+#pragma unroll
+        for (int k = 0; k < 16; ++k) t1[ad0(x0(k))] = v[k];
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < 16; ++k) v[k] = t1[ad0(x1(k))];
+        __syncthreads();  // the tile is rewritten by the round exchange
+    }
+    if constexpr (!INV) {
+        ntt_round_rg<LOGP, 0, SM, false, FP>(v, ts, twg, pr);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) t0[ad0(x0(k))] = v[k];
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < 16; ++k) v[k] = t0[ad0(x1(k))];
+        ntt_round_rg<LOGP, SM, LOGP, false, FP>(v, ts, twg, pr);
+    } else {
+        ntt_round_rg<LOGP, SM, LOGP, true, FP>(v, ts, twg, pr);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) t0[ad0(x1(k))] = v[k];
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < 16; ++k) v[k] = t0[ad0(x0(k))];
+        ntt_round_rg<LOGP, 0, SM, true, FP>(v, ts, twg, pr);
+    }
+    if constexpr (OUT_T) {  // pass B forward: the last round left set 1, store set 0
+        __syncthreads();  // every thread has read the round exchange
+#pragma unroll
+        for (int k = 0; k < 16; ++k) t1[ad0(x1(k))] = v[k];
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < 16; ++k) v[k] = t1[ad0(x0(k))];
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const u64 g = gidx(xout(k));
+        u64 val = v[k];
+        if constexpr (FINAL) {
+            if constexpr (FP) {
+                double d = __longlong_as_double((long long)val);
+                if constexpr (INV) d = fp_mulmod(d, pr.ninv_d, pr.qd, pr.qinv);
+                val = fp_canon(d, pr.qd, pr.qinv);
+            } else {
+                if constexpr (!INV) val = csub(csub(val, two_q), q);
+                else val = shoup(val, pr.ninv, pr.ninv_q, q);
+            }
+            bio.store(g, val, pre[k]);
+        } else {
+            bio.store(g, val, typename Bound::Pre{});
+        }
+    }
+}
+
 // CLS 0: per-block branch on the prime's arithmetic class; 1 / 2: an FP64-only / integer-only launch
 // (a smaller register budget for the FP64 kernel when a launch's jobs are all of one class)
-template <int LOGP, int NSEG, bool INV, bool PASS_A, bool FINAL, class IO, int CLS = 0>
+// RD: the register-direct pass (ntt_pass_body_rd)
+template <int LOGP, int NSEG, bool INV, bool PASS_A, bool FINAL, class IO, int CLS = 0, bool RD = false>
 __global__ void __launch_bounds__(NSEG *(1 << LOGP) / 16)
     k_ntt(const IO io, TwTables tt, const DevPrime *__restrict__ primes, int logN)
 {
     static_assert(LOGP >= 5 && LOGP <= 8, "two rounds of 4 stages");
-    __shared__ u64 lds[PASS_A ? (1 << LOGP) * (NSEG + 1) : NSEG * ((1 << LOGP) + 1)];
+    constexpr int WORDS = !RD ? (PASS_A ? (1 << LOGP) * (NSEG + 1) : NSEG * ((1 << LOGP) + 1))
+                              : (PASS_A ? (1 << LOGP) * (NSEG + 1) : NSEG * nttb_ld(LOGP));
+    __shared__ u64 lds[WORDS];
     const auto bio = io.bind(blockIdx.y);
     if (!bio.valid) return;  // uniform per block
     const DevPrime pr = primes[bio.prime];
-    if constexpr (CLS == 1) ntt_pass_body<LOGP, NSEG, INV, PASS_A, FINAL, true>(lds, bio, pr, tt, logN);
+    if constexpr (RD) {
+        if (pr.fp) ntt_pass_body_rd<LOGP, NSEG, INV, PASS_A, FINAL, true>(lds, bio, pr, tt, logN);
+        else ntt_pass_body_rd<LOGP, NSEG, INV, PASS_A, FINAL, false>(lds, bio, pr, tt, logN);
+    } else if constexpr (CLS == 1) ntt_pass_body<LOGP, NSEG, INV, PASS_A, FINAL, true>(lds, bio, pr, tt, logN);
     else if constexpr (CLS == 2) ntt_pass_body<LOGP, NSEG, INV, PASS_A, FINAL, false>(lds, bio, pr, tt, logN);
     else if (pr.fp) ntt_pass_body<LOGP, NSEG, INV, PASS_A, FINAL, true>(lds, bio, pr, tt, logN);
     else ntt_pass_body<LOGP, NSEG, INV, PASS_A, FINAL, false>(lds, bio, pr, tt, logN);
@@ -434,7 +570,16 @@ static void run_ntt2(Ctx &c, int njobs, const IO1 &first, const IO2 &second, int
     const dim3 gA(C / NA, njobs), gB(R / NB, njobs);
     constexpr int TA = NA * R / 16, TB = NB * C / 16;
     const TwTables fwd{c.tw, c.twb, c.twf, c.twbf}, inv{c.itw, c.itwb, c.itwf, c.itwbf};
-    if constexpr (!INV) {
+    if (c.ntt_rd) {
+        if constexpr (!INV) {  // the forward pass B stays on ntt_pass_body (register-direct measured slower:
+                               // divide-and-round pass B 1,948 vs 1,894 ms, mod-up pass B 1,152 vs 1,077 ms per step)
+            if (stages & 1) k_ntt<LOGR, NA, false, true, false, IO1, 0, true><<<gA, TA, 0, c.stream>>>(first, fwd, c.primes, c.logN);
+            if (stages & 2) k_ntt<LOGC, NB, false, false, true><<<gB, TB, 0, c.stream>>>(second, fwd, c.primes, c.logN);
+        } else {
+            if (stages & 1) k_ntt<LOGC, NB, true, false, false, IO1, 0, true><<<gB, TB, 0, c.stream>>>(first, inv, c.primes, c.logN);
+            if (stages & 2) k_ntt<LOGR, NA, true, true, true, IO2, 0, true><<<gA, TA, 0, c.stream>>>(second, inv, c.primes, c.logN);
+        }
+    } else if constexpr (!INV) {
         if (stages & 1) k_ntt<LOGR, NA, false, true, false><<<gA, TA, 0, c.stream>>>(first, fwd, c.primes, c.logN);
         if (stages & 2) k_ntt<LOGC, NB, false, false, true><<<gB, TB, 0, c.stream>>>(second, fwd, c.primes, c.logN);
     } else {
