@@ -572,7 +572,9 @@ static void run_ntt2(Ctx &c, int njobs, const IO1 &first, const IO2 &second, int
     const TwTables fwd{c.tw, c.twb, c.twf, c.twbf}, inv{c.itw, c.itwb, c.itwf, c.itwbf};
     if (c.ntt_rd) {
         if constexpr (!INV) {  // the forward pass B stays on ntt_pass_body (register-direct measured slower:
-                               // divide-and-round pass B 1,948 vs 1,894 ms, mod-up pass B 1,152 vs 1,077 ms per step)
+                               // divide-and-round pass B 1,948 vs 1,894 ms, mod-up pass B 1,152 vs 1,077 ms per step;
+                               // SQ counters: a third fewer LDS and VMEM instructions, no bank conflicts either way,
+                               // but 2.2x the cycles waiting on load dependencies and 15 % more wave cycles)
             if (stages & 1) k_ntt<LOGR, NA, false, true, false, IO1, 0, true><<<gA, TA, 0, c.stream>>>(first, fwd, c.primes, c.logN);
             if (stages & 2) k_ntt<LOGC, NB, false, false, true><<<gB, TB, 0, c.stream>>>(second, fwd, c.primes, c.logN);
         } else {
