@@ -457,6 +457,21 @@ void hoist_node(Ctx &c, PolyArr X, int B, int l, const Hoist &h)
     const u64 N = c.N;
     int pmap[HEC_MAXL + 1];
     for (int i = 0; i <= HEC_MAXL; ++i) pmap[i] = i;
+    if (c.fan2 && c.hoist_scan) {  // the fan-out finishes the INTT and lists the zeros: no D round trip
+        {
+            ProfScope ps(c, "ks_intt");
+            ProfScope k(c, "k:k_ntt/intt_b", 2.0 * B * l);
+            ntt_strided(c, true, X.p + X.sk, X.sb, h.D, l * N, l, pmap, B * l, 1, 1);
+        }
+        ProfScope ps(c, "ks_modup_h");
+        {
+            ProfScope k(c, "k:k_fan2/hoist", (double)B * l * (l + 1));
+            fan_modup(c, h.D, h.E, B, l, false, h.zl);
+        }
+        ProfScope k(c, "k:k_ntt/modup_h_b", 2.0 * B * l * l);
+        ks_modup(c, h.D, h.E, B, l, 2);  // pass B, canonical NTT-form digits
+        return;
+    }
     {
         ProfScope ps(c, "ks_intt");
         {
@@ -1201,6 +1216,7 @@ int hec_context_create(uint64_t N, const uint64_t *mod, uint64_t K, int device, 
         if (const char *f = std::getenv("HEC_FAN2")) c.fan2 = std::atoi(f);
         if (const char *f = std::getenv("HEC_FANSPLIT")) c.fan_split = std::atoi(f);
         if (const char *f = std::getenv("HEC_NTT_RD")) c.ntt_rd = std::atoi(f);
+        if (const char *f = std::getenv("HEC_HOIST_SCAN")) c.hoist_scan = std::atoi(f);
         if (const char *f = std::getenv("HEC_TENSOR_BG")) c.tensor_bg = std::atoi(f);
         if (const char *f = std::getenv("HEC_LANES")) c.lanes = std::max(1, std::atoi(f));
         if (const char *f = std::getenv("HEC_LANE_CUMASK")) c.lane_cumask = std::atoi(f);

@@ -88,6 +88,8 @@ struct Ctx {
     int fan_groups_moddown = 1;    // HEC_FANG="moddown,modup,hoist": target groups per k_fan source (blocks
     int fan_groups_modup = 1;      // per launch x groups; the source's inverse pass is repeated per group)
     int fan_groups_hoist = 1;
+    int hoist_scan = 1;            // HEC_HOIST_SCAN=0: hoisted node as INTT pass B, pass A, k_zscan, direct fan-out
+                                   // (1: INTT pass B, then the fan-out finishes the INTT and lists the zeros)
     int ntt_rd = 1;                // HEC_NTT_RD=0: k_ntt stages every round through LDS (ntt_pass_body)
     int fan_split = 1;             // HEC_FANSPLIT=0: Barrett (not the FP64 split) for the mod-down rounding limbs
                                    // at FP64 targets (FanDivRound::xf16)
@@ -143,7 +145,8 @@ void divide_round(Ctx &c, const u64 *Y, u64 ysb, u64 ysk, PolyArr X, PolyArr IN,
 // the forward pass A of every target prime from registers.
 //   mod-up:  D[b][J] -> E[b][I][J] (I != J), the input of k_bmac / ks_modup's pass B
 //   mod-down: last limb (b, k) at Y + b ysb + k ysk -> Z[b][k][i], the input of divide_round pass B
-void fan_modup(Ctx &c, const u64 *D, u64 *E, int B, int l, bool direct = false);
+// zl (non-direct only): also list the zero coefficients of the INTT's canonical values (zero_scan's format)
+void fan_modup(Ctx &c, const u64 *D, u64 *E, int B, int l, bool direct = false, int *zl = nullptr);
 // hoisted mod-up (hec_kernels.hip): zero_scan lists the zero coefficients of nlimbs canonical limbs
 // (zl: per limb count + HEC_ZCAP positions; more raises c.zflag); hoisted_mac is one child's key MAC
 // from the node's NTT-form digits E, the child's sign-mask NTTs W (K limbs) and X1 = the node's c1.

@@ -659,13 +659,26 @@ void divide_round(Ctx &c, const u64 *Y, u64 ysb, u64 ysk, PolyArr X, PolyArr IN,
 // pass-A-domain tile for the following pass-B kernel (k_bmac / the divide-and-round pass B).  The
 // coefficient-form limb is never stored, and it is read once instead of once per target.
 // kDirect: D already holds the canonical coefficient form (hoisted mod-up), so there is no inverse pass.
+// one zero coefficient g of digit limb `limb` in the zero lists (layout: see k_zscan)
+__device__ __forceinline__ void zero_record(int *zl, int *zflag, int limb, int g)
+{
+    atomicAdd(zl, 1);
+    int *z = zl + 1 + limb * (HEC_ZCAP + 1);
+    const int k = atomicAdd(z, 1);
+    if (k < HEC_ZCAP) z[1 + k] = g;
+    else atomicOr(zflag, 1);
+}
+
 template <bool DIRECT>
 struct FanModUpT {  // source (b, J) = D[b][J] (inverse pass-B domain) -> E[b][I][J], I != J, mod q_I
     static constexpr bool kDirect = DIRECT;
+    static constexpr bool kScan = !DIRECT;
     const u64 *D;
     u64 *E;
     int l, logN, kP;
     const DevPrime *primes;
+    int *zl = nullptr, *zflag = nullptr;  // non-direct hoisted mod-up: list the zero coefficients of the source
+                                          // (k_zscan's format) while the INTT's values are in registers
     struct Src { const u64 *in; int prime; };
     // red: how digit J (canonical, < q_J) reduces mod q_I: 0 nothing (q_J <= q_I: the 40-bit digits at the
     // 60-bit targets), 1 one conditional subtraction (q_J <= 2 q_I: 40-bit digit, 40-bit target), 2 Barrett
@@ -709,6 +722,8 @@ struct FanModUpT {  // source (b, J) = D[b][J] (inverse pass-B domain) -> E[b][I
 using FanModUp = FanModUpT<false>;
 struct FanDivRound {  // source (b, k) = last limb (inverse pass-B domain) -> Z[b][k][i] for i < nl
     static constexpr bool kDirect = false;
+    static constexpr bool kScan = false;
+    int *zl = nullptr, *zflag = nullptr;
     const u64 *Y;
     u64 ysb, ysk;
     u64 *Z;
@@ -926,6 +941,13 @@ __global__ void __launch_bounds__(NSEG *(1 << LOGP) / 16)
         }
 #pragma unroll
         for (int k = 0; k < 16; ++k) d[k] = fan.src_fix(d[k]);
+        if constexpr (FAN::kScan) {
+            if (fan.zl != nullptr && blockIdx.z == 0) {  // the canonical coefficient form's zeros (k_zscan)
+#pragma unroll
+                for (int k = 0; k < 16; ++k)
+                    if (d[k] == 0) zero_record(fan.zl, fan.zflag, (int)blockIdx.y, (int)gstride(k) & ((1 << logN) - 1));
+            }
+        }
     }
     const int nt = fan.ntargets(), t0 = blockIdx.z * nt / gridDim.z, t1 = (blockIdx.z + 1) * nt / gridDim.z;
     for (int t = t0; t < t1; ++t) {
@@ -981,11 +1003,20 @@ static void fan_dispatch(Ctx &c, int njobs, const FAN &fan, int groups = 1)
     }
 }
 
-void fan_modup(Ctx &c, const u64 *D, u64 *E, int B, int l, bool direct)
+void fan_modup(Ctx &c, const u64 *D, u64 *E, int B, int l, bool direct, int *zl)
 {
-    const int g = std::min(direct ? c.fan_groups_hoist : c.fan_groups_modup, l + 1);
-    if (direct) fan_dispatch(c, B * l, FanModUpT<true>{D, E, l, c.logN, (int)c.K - 1, c.primes}, g);
-    else fan_dispatch(c, B * l, FanModUp{D, E, l, c.logN, (int)c.K - 1, c.primes}, g);
+    const int g = std::min(direct || zl ? c.fan_groups_hoist : c.fan_groups_modup, l + 1);
+    if (direct) {
+        fan_dispatch(c, B * l, FanModUpT<true>{D, E, l, c.logN, (int)c.K - 1, c.primes}, g);
+        return;
+    }
+    FanModUp f{D, E, l, c.logN, (int)c.K - 1, c.primes};
+    if (zl) {
+        HEC_HIP(hipMemsetAsync(zl, 0, (1 + (std::size_t)B * l * (HEC_ZCAP + 1)) * sizeof(int), c.stream));
+        f.zl = zl;
+        f.zflag = c.zflag;
+    }
+    fan_dispatch(c, B * l, f, g);
 }
 
 // ================================================================================ hoisted mod-up ==
@@ -1007,13 +1038,7 @@ __global__ void __launch_bounds__(256) k_zscan(const u64 *__restrict__ D, int *_
     const u64 g = (u64)blockIdx.x * 256 + threadIdx.x;
     if (g >= N) return;
     const int limb = blockIdx.y;
-    if (D[((u64)limb << logN) + g] == 0) {
-        atomicAdd(zl, 1);
-        int *z = zl + 1 + limb * (HEC_ZCAP + 1);
-        const int k = atomicAdd(z, 1);
-        if (k < HEC_ZCAP) z[1 + k] = (int)g;
-        else atomicOr(zflag, 1);
-    }
+    if (D[((u64)limb << logN) + g] == 0) zero_record(zl, zflag, limb, (int)g);
 }
 
 void zero_scan(Ctx &c, const u64 *D, int nlimbs, int *zl)
