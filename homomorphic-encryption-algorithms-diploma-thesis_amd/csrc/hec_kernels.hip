@@ -703,6 +703,17 @@ struct FanModUpT {  // source (b, J) = D[b][J] (inverse pass-B domain) -> E[b][I
     // reduction at all, only the conversion
     __device__ void xf16(const Tgt &t, bool fp, const u64 *d, u64 *v) const
     {
+        if (t.red == 2 && fp && t.q > (1ull << 32)) {  // the 60-bit digit at an FP64 target: hi 2^30 + lo as above
+            const DevPrime &p = primes[t.prime];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                u64 y = d[k];
+                asm volatile("" : "+v"(y));  // per target (see FanDivRound::xf16)
+                const double hi = u2d(y >> 30) * 1073741824.0, lo = u2d(y & 0x3fffffffull);
+                v[k] = (u64)__double_as_longlong(fp_reduce(hi, p.qd, p.qinv) + lo);  // (-0.51 q, 0.51 q + 2^30)
+            }
+            return;
+        }
         if (t.red == 2) {
 #pragma unroll
             for (int k = 0; k < 16; ++k) v[k] = barrett64(d[k], t.q, t.r1);
@@ -732,14 +743,16 @@ struct FanDivRound {  // source (b, k) = last limb (inverse pass-B domain) -> Z[
     const DevPrime *primes;
     u64 fix[HEC_MAXL];
     double c30[HEC_MAXL];  // 2^30 mod q_i (split reduction at FP64 targets with q_i > 2^32, else 0)
+    unsigned sub1;         // bit i: P < 2 q_i, so y < P reduces mod q_i by one conditional subtraction
     struct Src { const u64 *in; int prime; };
-    struct Tgt { bool valid; int prime; u64 *out; u64 q, r1, fix; double qd, qinv, c30; };
+    struct Tgt { bool valid; int prime; u64 *out; u64 q, r1, fix; double qd, qinv, c30; bool sub1; };
     __device__ int ntargets() const { return nl; }
     __device__ Src src(int job) const { return Src{Y + (u64)(job / nk) * ysb + (u64)(job % nk) * ysk, last_idx}; }
     __device__ Tgt tgt(int job, int i) const
     {
         const DevPrime &p = primes[i];
-        return Tgt{true, i, Z + ((u64)(job * nl + i) << logN), p.q, p.r1, fix[i], p.qd, p.qinv, c30[i]};
+        return Tgt{true, i, Z + ((u64)(job * nl + i) << logN), p.q, p.r1, fix[i], p.qd, p.qinv, c30[i],
+                   ((sub1 >> i) & 1u) != 0};
     }
     // y -> (y + floor(P/2)) mod P, once per source value (the rounding offset is the same for every target)
     __device__ u64 src_fix(u64 d) const
@@ -747,9 +760,11 @@ struct FanDivRound {  // source (b, k) = last limb (inverse pass-B domain) -> Z[
         const u64 v = d + half;
         return v >= last ? v - last : v;
     }
-    __device__ u64 xf(const Tgt &t, u64 d) const { return barrett64(d, t.q, t.r1) + t.fix; }
-    // FP64 targets with q_i > 2^32: y = hi 2^30 + lo, y mod q_i == fp_mulmod(hi, 2^30 mod q_i) + lo (+ fix), an
-    // integer-valued double in (-0.53 q_i, 1.53 q_i + 2^30) within the FP64 forward NTT's |x| < 2 q_i input range
+    __device__ u64 xf(const Tgt &t, u64 d) const { return (t.sub1 ? csub(d, t.q) : barrett64(d, t.q, t.r1)) + t.fix; }
+    // FP64 targets with q_i > 2^32: y = hi 2^30 + lo, y == fp_reduce(hi 2^30) + lo (+ fix) mod q_i: hi 2^30 < 2^60 is
+    // an exact double and its reduction r = hi 2^30 - rint(hi 2^30 / q_i) q_i is exact in one FMA (|r| <= 0.5 q_i),
+    // so the value is an integer-valued double in (-0.51 q_i, 1.51 q_i + 2^30), within the FP64 forward NTT's
+    // |x| < 2 q_i input range
     // (no 64-bit Barrett: ~8 FP64 operations per value instead of 7 integer multiplies).  Smaller FP64 primes
     // and the integer targets keep Barrett.
     __device__ void xf16(const Tgt &t, bool fp, const u64 *d, u64 *v) const
@@ -761,8 +776,8 @@ struct FanDivRound {  // source (b, k) = last limb (inverse pass-B domain) -> Z[
                 u64 y = d[k];
                 asm volatile("" : "+v"(y));  // per target: hoisting the 32 split doubles out of the target loop
                                              // would keep them live beside d (274 VGPRs, one wave per SIMD)
-                const double hi = u2d(y >> 30), lo = u2d(y & 0x3fffffffull);
-                v[k] = (u64)__double_as_longlong(fp_mulmod(hi, t.c30, t.qd, t.qinv) + (lo + fx));
+                const double hi = u2d(y >> 30) * 1073741824.0, lo = u2d(y & 0x3fffffffull);  // hi: exact, < 2^60
+                v[k] = (u64)__double_as_longlong(fp_reduce(hi, t.qd, t.qinv) + (lo + fx));
             }
             return;
         }
@@ -1455,6 +1470,7 @@ void fan_divide_round(Ctx &c, const u64 *Y, u64 ysb, u64 ysk, u64 *Z, int B, int
     for (int i = 0; i < nl; ++i) {
         f.fix[i] = c.q[i] - (f.half % c.q[i]);
         f.c30[i] = c.fan_split && c.q[i] < (1ull << 42) && c.q[i] > (1ull << 32) ? (double)((1ull << 30) % c.q[i]) : 0.0;
+        if (c.fan_split && f.last < 2 * c.q[i] && i < 32) f.sub1 |= 1u << i;
     }
     fan_dispatch(c, B * nk, f, std::min(c.fan_groups_moddown, nl));
 }
