@@ -712,12 +712,15 @@ void walk_trie_hoisted(Ctx &c, Scratch &s, const RotTrie &t, int node, PolyArr s
             kids[q] = HChildSpec{e, (u32)invm(e, 2 * N), gk.keys.at(e), galois_negw(ctx, gk, e), h.acc[q],
                                  galois_kw(ctx, gk, e, l)};
         }
-        for (int q0 = 0; q0 < ng; q0 += (int)grp) {  // one profile scope per launch (bench.py's roofline)
-            const int nk = std::min((int)grp, ng - q0);
+        for (int q0 = 0, nk = 0; q0 < ng; q0 += nk) {  // one profile scope per launch (bench.py's roofline)
+            nk = std::min((int)grp, ng - q0);
+            // an odd group's last three children as one 3-child launch (the digits read once, not twice)
+            if (c.hmac_odd3 && grp == 2 && ng - q0 == 3) nk = 3;
             const double K = l + 1;  // digits E (B l^2) + c1 (B l); per child key (2 l K), W (K), KW (2 K), ACC (2 B K)
             ProfScope ps(c, "ks_hmac");
             ProfScope k(c, "k:k_hmacm", (double)B * (l * l + l) + nk * (2.0 * l * K + 3.0 * K + 2.0 * B * K));
-            hoisted_mac_multi(c, PolyArr{src.p + src.sk, src.sb, 0}, h.E, h.zl, kids + q0, nk, B, l);
+            if (nk == 3 && grp == 2) hoisted_mac_3(c, PolyArr{src.p + src.sk, src.sb, 0}, h.E, h.zl, kids + q0, B, l);
+            else hoisted_mac_multi(c, PolyArr{src.p + src.sk, src.sb, 0}, h.E, h.zl, kids + q0, nk, B, l);
         }
         if ((int)bufs.b[depth + 1].size() < ng) {  // too few rotation buffers to hold the group at once
             for (int q = 0; q < ng; ++q) {
@@ -1224,6 +1227,7 @@ int hec_context_create(uint64_t N, const uint64_t *mod, uint64_t K, int device, 
             std::sscanf(f, "%d,%d,%d", &c.fan_groups_moddown, &c.fan_groups_modup, &c.fan_groups_hoist);
         if (const char *f = std::getenv("HEC_HOIST")) c.hoist = f[0] != '0';
         if (const char *f = std::getenv("HEC_HMAC")) c.hmac_cfg = std::atoi(f);
+        if (const char *f = std::getenv("HEC_HMAC_ODD3")) c.hmac_odd3 = std::atoi(f);
         if (const char *f = std::getenv("HEC_HOIST_MIN")) c.hoist_min_children = std::max(1, std::atoi(f));
         if (const char *f = std::getenv("HEC_SPLIT_CLASSES")) c.split_classes = f[0] - '0';
         if (const char *f = std::getenv("HEC_TENSOR_DEFER")) c.tensor_defer_max = std::max(1, std::atoi(f));

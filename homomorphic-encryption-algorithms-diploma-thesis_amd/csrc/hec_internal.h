@@ -91,6 +91,7 @@ struct Ctx {
     int hoist_scan = 1;            // HEC_HOIST_SCAN=0: hoisted node as INTT pass B, pass A, k_zscan, direct fan-out
                                    // (1: INTT pass B, then the fan-out finishes the INTT and lists the zeros)
     int ntt_rd = 1;                // HEC_NTT_RD=0: k_ntt stages every round through LDS (ntt_pass_body)
+    int hmac_odd3 = 1;             // HEC_HMAC_ODD3=0: an odd sibling group ends in a pair and a single-child launch
     int fan_split = 1;             // HEC_FANSPLIT=0: Barrett (not the FP64 split) for the mod-down rounding limbs
                                    // at FP64 targets (FanDivRound::xf16)
     int fan2 = 1;                  // HEC_FAN2=0: the LDS-round k_fan instead of the register-direct k_fan2
@@ -166,6 +167,8 @@ constexpr int HMAC_MAX_CHILDREN = 6;  // largest hoisted_group()
 void key_wsum(Ctx &c, const u64 *key, u64 *KW, int l);
 void hoisted_mac_multi(Ctx &c, PolyArr X1, const u64 *E, const int *zl, const HChildSpec *kids, int nkids, int B,
                        int l);
+// three children in one sibling-fused launch (3 x 4 FP64 / 3 x 2 integer batch entries per thread)
+void hoisted_mac_3(Ctx &c, PolyArr X1, const u64 *E, const int *zl, const HChildSpec *kids, int B, int l);
 int hoisted_group(const Ctx &c);  // children per hoisted_mac_multi call for c.hmac_cfg
 void fan_divide_round(Ctx &c, const u64 *Y, u64 ysb, u64 ysk, u64 *Z, int B, int nk, int nl, int last_idx);
 void galois_permute(Ctx &c, PolyArr in, PolyArr out, int B, int nk, int nl, u32 elt);

@@ -1461,6 +1461,11 @@ void hoisted_mac_multi(Ctx &c, PolyArr X1, const u64 *E, const int *zl, const HC
     }
 }
 
+void hoisted_mac_3(Ctx &c, PolyArr X1, const u64 *E, const int *zl, const HChildSpec *kids, int B, int l)
+{
+    launch_hmacm<4, 2, 3>(c, X1, E, zl, kids, 3, B, l);
+}
+
 void fan_divide_round(Ctx &c, const u64 *Y, u64 ysb, u64 ysk, u64 *Z, int B, int nk, int nl, int last_idx)
 {
     if (nl > HEC_MAXL) throw std::invalid_argument("too many limbs");
