@@ -40,6 +40,10 @@ struct hec_context {
     // batch lanes (matvec_lanes): contexts sharing this one's device tables, each with its own HIP
     // stream, workspace and zero flag, built on first use
     std::vector<hec_context *> lanes;
+    // persistent events of matvec_lanes (created with the first lane, destroyed with the context): the lanes
+    // wait on lanes_start, the context stream waits on each lane's lane_done.  An event destroyed right after
+    // a hipStreamWaitEvent on it could let that wait pass early (a rare whole-lane race seen at full size).
+    hipEvent_t lanes_start = nullptr, lane_done = nullptr;
     // multi-GPU (hec_comm_init): this process's rank in a world of one process per GPU, RCCL communicator
     int rank = 0, world = 1;
     void *comm = nullptr;  // ncclComm_t
@@ -957,12 +961,14 @@ hec_context *make_lane(hec_context *parent, int index)
     HEC_HIP(hipEventCreateWithFlags(&c.ev_fork, hipEventDisableTiming));
     HEC_HIP(hipEventCreateWithFlags(&c.ev_join, hipEventDisableTiming));
     HEC_HIP(hipMalloc(&c.zflag, sizeof(int)));
+    HEC_HIP(hipEventCreateWithFlags(&l->lane_done, hipEventDisableTiming));
     return l;
 }
 void free_lane(hec_context *l)
 {
     Ctx &c = l->c;
     (void)hipStreamSynchronize(c.stream);
+    if (l->lane_done) (void)hipEventDestroy(l->lane_done);
     c.ws.release();
     (void)hipFree(c.zflag);
     (void)hipStreamDestroy(c.stream);
@@ -991,10 +997,10 @@ void matvec_lanes(hec_context *ctx, const hec_ciphertext *const *diags, const he
         }
     }
     while ((int)ctx->lanes.size() < nl) ctx->lanes.push_back(make_lane(ctx, (int)ctx->lanes.size()));
-    hipEvent_t start;
-    HEC_HIP(hipEventCreateWithFlags(&start, hipEventDisableTiming));
+    if (!ctx->lanes_start) HEC_HIP(hipEventCreateWithFlags(&ctx->lanes_start, hipEventDisableTiming));
+    hipEvent_t start = ctx->lanes_start;
     HEC_HIP(hipEventRecord(start, c.stream));  // the inputs were produced on the context's stream
-    std::vector<hipEvent_t> done(nl, nullptr);
+    std::vector<char> done(nl, 0);
     std::vector<std::exception_ptr> err(nl);
     std::vector<std::thread> th;
     for (int i = 0; i < nl; ++i) {
@@ -1003,22 +1009,18 @@ void matvec_lanes(hec_context *ctx, const hec_ciphertext *const *diags, const he
             try {
                 Ctx &lc = ctx->lanes[i]->c;
                 HEC_HIP(hipSetDevice(lc.device));
-                HEC_HIP(hipEventCreateWithFlags(&done[i], hipEventDisableTiming));
                 HEC_HIP(hipStreamWaitEvent(lc.stream, start, 0));
                 matvec_core(ctx, diags, pdiags, n, js, cols + b0, b1 - b0, rk, gk, finish, out + b0, &lc);
-                HEC_HIP(hipEventRecord(done[i], lc.stream));
+                HEC_HIP(hipEventRecord(ctx->lanes[i]->lane_done, lc.stream));
+                done[i] = 1;
             } catch (...) {
                 err[i] = std::current_exception();
             }
         });
     }
     for (auto &t : th) t.join();
-    for (int i = 0; i < nl; ++i)
-        if (done[i]) {
-            HEC_HIP(hipStreamWaitEvent(c.stream, done[i], 0));  // later work on the context sees the outputs
-            (void)hipEventDestroy(done[i]);
-        }
-    (void)hipEventDestroy(start);
+    for (int i = 0; i < nl; ++i)  // later work on the context sees the outputs
+        if (done[i]) HEC_HIP(hipStreamWaitEvent(c.stream, ctx->lanes[i]->lane_done, 0));
     for (auto &e : err)
         if (e) std::rethrow_exception(e);
 }
@@ -1366,8 +1368,9 @@ int hec_context_destroy(hec_context *ctx)
         if (!ctx) return;
         Ctx &c = ctx->c;
         (void)hipSetDevice(c.device);
-        for (hec_context *l : ctx->lanes) free_lane(l);
         (void)hipStreamSynchronize(c.stream);
+        for (hec_context *l : ctx->lanes) free_lane(l);
+        if (ctx->lanes_start) (void)hipEventDestroy(ctx->lanes_start);
         if (ctx->comm) (void)rccl().destroy((ncclComm_t)ctx->comm);
         c.ws.release();
         (void)hipFree(c.primes);
