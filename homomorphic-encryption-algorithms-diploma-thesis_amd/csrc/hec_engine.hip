@@ -888,6 +888,7 @@ void matvec_core(hec_context *ctx, const hec_ciphertext *const *diags, const hec
         HEC_HIP(hipMemcpyAsync(&zf, c.zflag, sizeof(int), hipMemcpyDeviceToHost, c.stream));
         HEC_HIP(hipStreamSynchronize(c.stream));
         if (zf) {
+            if (std::getenv("HEC_DEBUG")) std::fprintf(stderr, "hec: zero-list overflow, matvec recomputed without hoisting (p=%zu)\n", p);
             c.hoist = false;
             try {
                 matvec_core(ctx, diags, pdiags, n, js, cols, p, rk, gk, finish, out, exec);
@@ -1148,17 +1149,16 @@ void nccl_check(ncclResult_t e, const char *what)
 void hec::Workspace::reserve(std::size_t w)
 {
     if (w <= words) return;
-    if (base) {
-        HEC_HIP(hipDeviceSynchronize());
-        HEC_HIP(hipFree(base));
-        base = nullptr;
-    }
+    if (std::getenv("HEC_DEBUG")) std::fprintf(stderr, "hec: workspace %zu -> %zu words\n", words, w);
+    if (base) retired.push_back(base);  // kernels already enqueued may still use it
     base = dalloc(w);
     words = w;
 }
 void hec::Workspace::release()
 {
     if (base) (void)hipFree(base);
+    for (u64 *p : retired) (void)hipFree(p);
+    retired.clear();
     base = nullptr;
     words = 0;
 }

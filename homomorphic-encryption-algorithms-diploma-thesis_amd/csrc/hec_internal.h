@@ -34,6 +34,10 @@ struct Ctx;
 struct Workspace {
     u64 *base = nullptr;
     std::size_t words = 0;
+    // outgrown bases, freed with the workspace: a lane that grows its workspace while the other lanes are
+    // launching must not free device memory under them (hipFree from a lane thread coincided with rare wrong
+    // lanes at full size)
+    std::vector<u64 *> retired;
     void reserve(std::size_t w);
     void release();
 };
