@@ -1222,6 +1222,7 @@ int hec_context_create(uint64_t N, const uint64_t *mod, uint64_t K, int device, 
         if (const char *f = std::getenv("HEC_FANSPLIT")) c.fan_split = std::atoi(f);
         if (const char *f = std::getenv("HEC_NTT_RD")) c.ntt_rd = std::atoi(f);
         if (const char *f = std::getenv("HEC_HOIST_SCAN")) c.hoist_scan = std::atoi(f);
+        if (const char *f = std::getenv("HEC_DIVROUND_FP")) c.divround_fp = std::atoi(f);
         if (const char *f = std::getenv("HEC_TENSOR_BG")) c.tensor_bg = std::atoi(f);
         if (const char *f = std::getenv("HEC_LANES")) c.lanes = std::max(1, std::atoi(f));
         if (const char *f = std::getenv("HEC_LANE_CUMASK")) c.lane_cumask = std::atoi(f);

@@ -92,6 +92,7 @@ struct Ctx {
     int fan_groups_moddown = 1;    // HEC_FANG="moddown,modup,hoist": target groups per k_fan source (blocks
     int fan_groups_modup = 1;      // per launch x groups; the source's inverse pass is repeated per group)
     int fan_groups_hoist = 1;
+    int divround_fp = 1;           // HEC_DIVROUND_FP=0: the mod-down post-op on u64 (Shoup) at FP64 primes too
     int hoist_scan = 1;            // HEC_HOIST_SCAN=0: hoisted node as INTT pass B, pass A, k_zscan, direct fan-out
                                    // (1: INTT pass B, then the fan-out finishes the INTT and lists the zeros)
     int ntt_rd = 1;                // HEC_NTT_RD=0: k_ntt stages every round through LDS (ntt_pass_body)

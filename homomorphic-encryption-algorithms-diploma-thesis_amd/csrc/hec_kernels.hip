@@ -158,20 +158,29 @@ struct DivRoundIO_A {
         return Bound{Y + b * ysb + k * ysk, Z + ((u64)job << logN), last, half, primes[i].q, primes[i].r1, fix[i], i};
     }
 };
+// Bound types with a store_fp(g, double, Pre, prime) post-op for FP64 primes (HasFpStore)
+template <class T, class = void>
+struct HasFpStore : std::false_type {};
+template <class T>
+struct HasFpStore<T, std::void_t<decltype(T::kFpStore)>> : std::bool_constant<T::kFpStore> {};
+
 struct DivRoundIO_B {
     u64 *Z;
     PolyArr X, IN, OUT;
     int nk, nl, logN, in_nk;  // IN is added for polys k < in_nk only
     u32 elt;                  // IN is read through the Galois permutation (elt != 1)
+    int fpstore;              // FP64 primes: the post-op in FP64 (store_fp)
     const DevPrime *primes;
     u64 inv[HEC_MAXL], inv_q[HEC_MAXL];
     struct Bound {
+        static constexpr bool kFpStore = true;
         const u64 *z, *x, *in;
         u64 *out;
         u64 q, w, wq;
         int prime;
         u32 elt;
         int logN;
+        bool fpstore;
         bool valid = true;
         struct Pre {  // operands of the post-op, loaded before the butterfly rounds
             u64 x, in;
@@ -187,6 +196,14 @@ struct DivRoundIO_B {
             if (in) r = addmod(r, p.in, q);
             out[g] = r;
         }
+        // v: the FP64 NTT output before canonicalisation (|v| < 10 q): (x - v) P^-1 (+ in) with one exact
+        // fp_mulmod (|x - v| < 11 q) and one canonicalisation, instead of Shoup on u64 plus fp_canon
+        __device__ void store_fp(u64 g, double v, Pre p, const DevPrime &pr) const
+        {
+            double r = fp_mulmod(u2d(p.x) - v, u2d(w), pr.qd, pr.qinv);
+            if (in) r += u2d(p.in);
+            out[g] = fp_canon(r, pr.qd, pr.qinv);
+        }
     };
     __device__ Bound bind(int job) const
     {
@@ -194,7 +211,7 @@ struct DivRoundIO_B {
         const u64 li = (u64)i << logN;
         return Bound{Z + ((u64)job << logN), X.p + b * X.sb + k * X.sk + li,
                      (IN.p && k < in_nk) ? IN.p + b * IN.sb + k * IN.sk + li : nullptr, OUT.p + b * OUT.sb + k * OUT.sk + li,
-                     primes[i].q, inv[i], inv_q[i], i, elt, logN};
+                     primes[i].q, inv[i], inv_q[i], i, elt, logN, fpstore != 0};
     }
 };
 
@@ -398,6 +415,12 @@ __device__ __forceinline__ void ntt_pass_body(u64 *lds, const Bound &bio, const 
             if constexpr (FP) {
                 double d = __longlong_as_double((long long)v);
                 if constexpr (INV) d = fp_mulmod(d, pr.ninv_d, pr.qd, pr.qinv);
+                if constexpr (HasFpStore<Bound>::value) {  // the post-op in FP64 on the uncanonicalised value
+                    if (bio.fpstore) {
+                        bio.store_fp(g, d, pre[it], pr);
+                        continue;
+                    }
+                }
                 v = fp_canon(d, pr.qd, pr.qinv);
             } else {
                 if constexpr (!INV) v = csub(csub(v, two_q), q);
@@ -647,6 +670,7 @@ void divide_round(Ctx &c, const u64 *Y, u64 ysb, u64 ysk, PolyArr X, PolyArr IN,
     DivRoundIO_B b{};
     b.Z = Z; b.X = X; b.IN = IN; b.OUT = OUT; b.nk = nk; b.nl = nl; b.logN = c.logN; b.in_nk = in_nk; b.elt = in_elt;
     b.primes = c.primes;
+    b.fpstore = c.divround_fp;
     for (int i = 0; i < nl; ++i) { b.inv[i] = inv[i]; b.inv_q[i] = inv_q[i]; }
     ntt_dispatch<false>(c, B * nk * nl, a, b, stages);
 }
