@@ -127,6 +127,9 @@ def lib():
             "hec_seal_parms_id": [C.c_uint64, u64p, C.c_uint64, u64p],
             "hec_seal_ciphertext_load": [vp, C.c_uint64, u64p, u64p, u64p, C.POINTER(C.c_double), u64p, u64p,
                                          C.c_uint64, u64p],
+            "hec_seal_ciphertext_load_ex": [vp, C.c_uint64, u64p, C.c_uint64, u64p, u64p, u64p,
+                                            C.POINTER(C.c_double), u64p, u64p, C.c_uint64, u64p],
+            "hec_seal_blake2xb": [vp, C.c_uint64, vp, C.c_uint64, C.c_uint64, vp],
             "hec_seal_ciphertext_save": [u64p, C.c_uint64, C.c_uint64, C.c_uint64, C.c_double, u64p, C.c_int, vp,
                                          C.c_uint64, u64p],
             "hec_seal_parms_load": [vp, C.c_uint64, u64p, u64p, C.c_uint64, u64p, u64p],
@@ -238,16 +241,26 @@ def seal_ciphertext_save(data: np.ndarray, scale: float, moduli, compr=COMPR_ZST
     return _sized_out(lambda o, c, w: lib().hec_seal_ciphertext_save(_p(d), size, level, N, scale, _p(m), compr, o, c, w))
 
 
-def seal_ciphertext_load(b: bytes):
-    """-> (data u64[size][level][N], scale, parms_id, bytes consumed)"""
+def seal_blake2xb(data: bytes, key: bytes, outlen: int) -> bytes:
+    """BLAKE2Xb XOF output (SEAL's Blake2xbPRNG core)."""
+    out = C.create_string_buffer(outlen)
+    _seal_check(lib().hec_seal_blake2xb(C.c_char_p(data), len(data), C.c_char_p(key), len(key), outlen, out))
+    return out.raw
+
+
+def seal_ciphertext_load(b: bytes, moduli=None):
+    """-> (data u64[size][level][N], scale, parms_id, bytes consumed).  With the context's data-level moduli a
+    seeded ciphertext (encrypt_symmetric(...).save) is expanded as Ciphertext::expand_seed does."""
     size, level, N, used = C.c_uint64(), C.c_uint64(), C.c_uint64(), C.c_uint64()
     scale = C.c_double()
     pid = np.zeros(4, dtype=np.uint64)
+    m = None if moduli is None else np.ascontiguousarray(np.array(moduli, dtype=np.uint64))
+    mp, mc = (None, 0) if m is None else (_p(m), len(m))
     src, n = _bytes_in(b)
-    _seal_check(lib().hec_seal_ciphertext_load(src, n, C.byref(size), C.byref(level), C.byref(N), C.byref(scale),
-                                               _p(pid), None, 0, C.byref(used)))
+    _seal_check(lib().hec_seal_ciphertext_load_ex(src, n, mp, mc, C.byref(size), C.byref(level), C.byref(N),
+                                                  C.byref(scale), _p(pid), None, 0, C.byref(used)))
     d = np.zeros((size.value, level.value, N.value), dtype=np.uint64)
-    _seal_check(lib().hec_seal_ciphertext_load(src, n, None, None, None, None, None, _p(d), d.size, None))
+    _seal_check(lib().hec_seal_ciphertext_load_ex(src, n, mp, mc, None, None, None, None, None, _p(d), d.size, None))
     return d, scale.value, pid, used.value
 
 

@@ -1845,15 +1845,17 @@ int hec_ciphertext_load_seal(hec_ciphertext *ct, const void *bytes, uint64_t nby
         Ctx &c = ct->ctx->c;
         uint64_t size = 0, level = 0, N = 0, pid[4], used = 0;
         double scale = 0;
-        seal_rc(hec_seal_ciphertext_load(bytes, nbytes, &size, &level, &N, &scale, pid, nullptr, 0, &used));
+        // the context's data-level primes expand a seeded object (client.cpp:113-114 sends those)
+        seal_rc(hec_seal_ciphertext_load_ex(bytes, nbytes, c.q.data(), c.L, &size, &level, &N, &scale, pid, nullptr, 0,
+                                            &used));
         // Ciphertext::load(context, ...): the data must be valid for the context (is_valid_for)
         need(N == c.N && level >= 1 && level <= c.L && size >= 2, "ciphertext data is invalid");
         uint64_t want[4];
         seal_rc(hec_seal_parms_id(c.N, c.q.data(), level, want));
         need(std::memcmp(want, pid, 32) == 0, "ciphertext data is invalid");
         std::vector<u64> host(size * level * N);
-        seal_rc(hec_seal_ciphertext_load(bytes, nbytes, nullptr, nullptr, nullptr, nullptr, nullptr, host.data(),
-                                         host.size(), nullptr));
+        seal_rc(hec_seal_ciphertext_load_ex(bytes, nbytes, c.q.data(), c.L, nullptr, nullptr, nullptr, nullptr, nullptr,
+                                            host.data(), host.size(), nullptr));
         const int rc = hec_ciphertext_upload(ct, host.data(), size, level, scale);
         if (rc != HEC_OK) throw std::logic_error(hec_last_error());
         if (consumed) *consumed = used;

@@ -81,12 +81,25 @@ void blake2b_compress(u64 h[8], const u8 block[128], u64 t, bool last)
     for (int i = 0; i < 8; ++i) h[i] ^= v[i] ^ v[i + 8];
 }
 
-// unkeyed BLAKE2b with an outlen-byte digest
-void blake2b(u8 *out, std::size_t outlen, const u8 *in, std::size_t inlen)
+// BLAKE2b over an explicit 64-byte parameter block (RFC 7693 §2.5; BLAKE2 paper §2.8), keyed when keylen > 0:
+// the key, zero-padded to one 128-byte block, is hashed ahead of the input.
+void blake2b_param(u8 *out, std::size_t outlen, const u8 *in, std::size_t inlen, const u8 *key, std::size_t keylen,
+                   const u8 param[64])
 {
     u64 h[8];
-    for (int i = 0; i < 8; ++i) h[i] = kIV[i];
-    h[0] ^= 0x01010000ULL ^ (u64)outlen;
+    for (int i = 0; i < 8; ++i) {
+        u64 w;
+        std::memcpy(&w, param + 8 * i, 8);
+        h[i] = kIV[i] ^ w;
+    }
+    std::vector<u8> msg;
+    if (keylen) {
+        msg.assign(128, 0);
+        std::memcpy(msg.data(), key, keylen);
+        msg.insert(msg.end(), in, in + inlen);
+        in = msg.data();
+        inlen = msg.size();
+    }
     u8 block[128];
     u64 t = 0;
     while (inlen > 128) {
@@ -96,12 +109,93 @@ void blake2b(u8 *out, std::size_t outlen, const u8 *in, std::size_t inlen)
         inlen -= 128;
     }
     std::memset(block, 0, 128);
-    std::memcpy(block, in, inlen);
+    if (inlen) std::memcpy(block, in, inlen);
     t += inlen;
     blake2b_compress(h, block, t, true);
     u8 full[64];
     std::memcpy(full, h, 64);
     std::memcpy(out, full, outlen);
+}
+
+// unkeyed sequential BLAKE2b with an outlen-byte digest (util::HashFunction behind parms_id)
+void blake2b(u8 *out, std::size_t outlen, const u8 *in, std::size_t inlen)
+{
+    u8 param[64] = {};
+    param[0] = (u8)outlen;
+    param[2] = 1;  // fanout
+    param[3] = 1;  // depth
+    blake2b_param(out, outlen, in, inlen, nullptr, 0, param);
+}
+
+// BLAKE2Xb (the BLAKE2X note; reference blake2xb.c, which SEAL 4.1 vendors as util/blake2xb.c): a keyed
+// root hash whose parameter block carries the XOF length, then ceil(outlen / 64) unkeyed leaf hashes of the
+// root, leaf i with node_offset i and digest length min(64, remaining).
+void blake2xb(u8 *out, std::size_t outlen, const u8 *in, std::size_t inlen, const u8 *key, std::size_t keylen)
+{
+    u8 param[64] = {};
+    param[0] = 64;
+    param[1] = (u8)keylen;
+    param[2] = 1;
+    param[3] = 1;
+    const uint32_t xof = (uint32_t)outlen;
+    std::memcpy(param + 12, &xof, 4);
+    u8 root[64];
+    blake2b_param(root, 64, in, inlen, key, keylen, param);
+    param[1] = 0;     // key_length
+    param[2] = 0;     // fanout
+    param[3] = 0;     // depth
+    param[4] = 64;    // leaf_length (u32 LE)
+    param[17] = 64;   // inner_length
+    for (uint32_t i = 0; outlen > 0; ++i) {
+        const std::size_t bs = outlen < 64 ? outlen : 64;
+        param[0] = (u8)bs;
+        std::memcpy(param + 8, &i, 4);  // node_offset
+        blake2b_param(out, bs, root, 64, nullptr, 0, param);
+        out += bs;
+        outlen -= bs;
+    }
+}
+
+// SEAL 4.1 Blake2xbPRNG (randomgen.cpp): a byte stream of 4096-byte buffers, buffer k = BLAKE2Xb(input = the
+// u64 counter k, key = the 64-byte prng_seed_type), served in order by UniformRandomGenerator::generate.
+struct Blake2xbStream {
+    u8 seed[64];
+    u64 counter = 0;
+    u8 buf[4096];
+    std::size_t head = sizeof(buf);
+    void generate(u8 *dst, std::size_t n)
+    {
+        while (n) {
+            if (head == sizeof(buf)) {
+                blake2xb(buf, sizeof(buf), reinterpret_cast<const u8 *>(&counter), 8, seed, 64);
+                ++counter;
+                head = 0;
+            }
+            const std::size_t k = std::min(n, sizeof(buf) - head);
+            std::memcpy(dst, buf + head, k);
+            head += k;
+            dst += k;
+            n -= k;
+        }
+    }
+};
+
+// SEAL 4.1 sample_poly_uniform (util/rlwe.cpp), which Ciphertext::expand_seed runs into c1 for a version-4
+// object: fill the level x N words from the stream in one draw, then per prime q_j reject each word
+// >= max_multiple = (2^64 - 1) - ((2^64 - 1) mod q_j) - 1 by redrawing it from the stream's continuation,
+// and reduce mod q_j.  In NTT form (CKKS) the uniform c1 is used as drawn.
+void sample_poly_uniform(Blake2xbStream &prng, const u64 *q, u64 level, u64 N, u64 *dst)
+{
+    prng.generate(reinterpret_cast<u8 *>(dst), level * N * 8);
+    const u64 max_random = ~0ULL;
+    for (u64 j = 0; j < level; ++j, dst += N) {
+        const u64 max_multiple = max_random - max_random % q[j] - 1;
+        for (u64 i = 0; i < N; ++i) {
+            u64 v = dst[i];
+            while (v >= max_multiple) prng.generate(reinterpret_cast<u8 *>(&v), 8);
+            dst[i] = v % q[j];
+        }
+    }
 }
 
 // ------------------------------------------------------------------ framing
@@ -319,6 +413,9 @@ struct CtData {
     double scale = 1.0;
     std::vector<u64> data;  // u64[size][level][N]
     bool seeded = false;
+    int major = 4;
+    u8 prng_type = 0;  // UniformRandomGeneratorInfo of a seeded ciphertext: 1 blake2xb, 2 shake256
+    u8 seed[64] = {};
 };
 
 CtData parse_ciphertext(Reader &outer, int major)
@@ -341,7 +438,14 @@ CtData parse_ciphertext(Reader &outer, int major)
     if (count != full && !(c.size == 2 && count == c.N * c.level)) throw std::invalid_argument("ciphertext data is invalid");
     c.data.resize(count);
     d.bytes(c.data.data(), count * 8);
-    if (count != full) c.seeded = true;  // c0 only + UniformRandomGeneratorInfo: Ciphertext::expand_seed
+    c.major = major;
+    if (count != full) {  // c0 only + UniformRandomGeneratorInfo (u8 prng_type, 8 x u64 seed): expand_seed
+        c.seeded = true;
+        std::vector<u8> im = open_object(r);
+        Reader ir{im.data(), im.data() + im.size()};
+        c.prng_type = ir.get<u8>();
+        ir.bytes(c.seed, 64);
+    }
     return c;
 }
 void emit_ciphertext(Writer &w, const CtData &c, int compr)
@@ -369,6 +473,26 @@ void parms_id_of(u64 N, const u64 *moduli, u64 count, u64 out[4])
     for (u64 i = 0; i < count; ++i) words.push_back(moduli[i]);
     words.push_back(0);  // plain_modulus (zero for CKKS)
     blake2b(reinterpret_cast<u8 *>(out), 32, reinterpret_cast<const u8 *>(words.data()), words.size() * 8);
+}
+
+// Ciphertext::expand_seed (ciphertext.cpp) for a version-4 object: c1 = sample_poly_uniform over the
+// ciphertext's own primes q_0..q_{level-1}, drawn from the seed's Blake2xbPRNG.
+void expand_seed(CtData &c, const u64 *q, u64 count)
+{
+    if (!q) throw std::invalid_argument("seeded ciphertext: the context's coeff_modulus is needed to expand it");
+    if (count < c.level) throw std::invalid_argument("ciphertext data is invalid");
+    u64 want[4];
+    parms_id_of(c.N, q, c.level, want);
+    if (std::memcmp(want, c.parms_id, 32) != 0) throw std::invalid_argument("ciphertext data is invalid");
+    if (c.major != 4) throw std::invalid_argument("seeded ciphertext: only SEAL 4.x seed expansion is supported");
+    if (c.prng_type != 1)
+        throw std::invalid_argument("seeded ciphertext: unsupported prng_type (only blake2xb, SEAL's default)");
+    const u64 half = c.N * c.level;
+    c.data.resize(2 * half);
+    Blake2xbStream prng;
+    std::memcpy(prng.seed, c.seed, 64);
+    sample_poly_uniform(prng, q, c.level, c.N, c.data.data() + half);
+    c.seeded = false;
 }
 
 template <class F>
@@ -414,19 +538,24 @@ int hec_seal_parms_id(uint64_t N, const uint64_t *coeff_modulus, uint64_t count,
     });
 }
 
-int hec_seal_ciphertext_load(const void *bytes, uint64_t nbytes, uint64_t *size, uint64_t *level, uint64_t *N,
-                             double *scale, uint64_t parms_id[4], uint64_t *data, uint64_t data_words,
-                             uint64_t *consumed)
+int hec_seal_ciphertext_load_ex(const void *bytes, uint64_t nbytes, const uint64_t *coeff_modulus, uint64_t count,
+                                uint64_t *size, uint64_t *level, uint64_t *N, double *scale, uint64_t parms_id[4],
+                                uint64_t *data, uint64_t data_words, uint64_t *consumed)
 {
     return io_guard([&] {
         if (!bytes) throw std::invalid_argument("invalid argument");
         Reader r{static_cast<const u8 *>(bytes), static_cast<const u8 *>(bytes) + nbytes};
         Header h;
         std::memcpy(&h, bytes, std::min<uint64_t>(nbytes, sizeof(h)));
-        const CtData c = parse_ciphertext(r, h.major);
-        if (c.seeded)
-            throw std::invalid_argument("seeded ciphertext: expand it with the caller's SEAL (Ciphertext::expand_seed) "
-                                        "before handing it over");
+        CtData c = parse_ciphertext(r, h.major);
+        if (c.seeded) {
+            if (!coeff_modulus)
+                throw std::invalid_argument("seeded ciphertext: load it with hec_seal_ciphertext_load_ex and the "
+                                            "context's coeff_modulus (Ciphertext::expand_seed)");
+            // the expansion is only paid for when the caller asks for the words
+            if (data) expand_seed(c, coeff_modulus, count);
+            else if (count < c.level) throw std::invalid_argument("ciphertext data is invalid");
+        }
         if (!c.ntt) throw std::invalid_argument("CKKS ciphertext is not in NTT form");
         if (size) *size = c.size;
         if (level) *level = c.level;
@@ -438,6 +567,23 @@ int hec_seal_ciphertext_load(const void *bytes, uint64_t nbytes, uint64_t *size,
             if (data_words < c.data.size()) throw std::invalid_argument("output buffer is too small");
             std::memcpy(data, c.data.data(), c.data.size() * 8);
         }
+    });
+}
+
+int hec_seal_ciphertext_load(const void *bytes, uint64_t nbytes, uint64_t *size, uint64_t *level, uint64_t *N,
+                             double *scale, uint64_t parms_id[4], uint64_t *data, uint64_t data_words,
+                             uint64_t *consumed)
+{
+    return hec_seal_ciphertext_load_ex(bytes, nbytes, nullptr, 0, size, level, N, scale, parms_id, data, data_words,
+                                       consumed);
+}
+
+int hec_seal_blake2xb(const void *in, uint64_t n, const void *key, uint64_t keylen, uint64_t outlen, void *out)
+{
+    return io_guard([&] {
+        if (!out || outlen < 1 || outlen > 0xFFFFFFFFull || keylen > 64 || (!in && n) || (!key && keylen))
+            throw std::invalid_argument("invalid argument");
+        blake2xb(static_cast<u8 *>(out), outlen, static_cast<const u8 *>(in), n, static_cast<const u8 *>(key), keylen);
     });
 }
 

@@ -74,3 +74,20 @@ def test_server_flow_on_seal_bytes(env, hecdna, tmp_path):
     exp = e.o.rescale(e.o.relinearize(e.o.multiply(op1, op2), e.rk_h))
     assert used == len(res) and np.array_equal(data, exp.data) and scale == exp.scale
     assert np.array_equal(pid, sf.parms_id(e.N, e.m[:exp.level]))
+
+
+def test_seeded_ciphertext_load_on_device(env, hecdna):
+    """The reference client sends encrypt_symmetric(...).save (client.cpp:113-114): c0 + a Blake2xbPRNG seed.
+    Ciphertext::load(context, ...) on the device object expands c1 over the ciphertext's primes (SEAL 4.1
+    expand_seed / sample_poly_uniform), equal to the independent Python restatement."""
+    e = env
+    level = len(e.m) - 1
+    seed = np.random.default_rng(5).integers(0, 2**63, 8, dtype=np.uint64).tobytes()
+    c0 = e.rand_ct(1, level).data
+    d = np.concatenate([c0, np.zeros_like(c0)])
+    b = sf.ciphertext(d, 2.0**40, e.m, seeded_c0_only=True, seed=seed)
+    g = hecdna.Ciphertext(e.ctx)
+    assert g.load_seal(b) == len(b)
+    want = np.stack([c0[0], sf.expand_seed_c1(seed, e.m[:level], e.N)])
+    assert np.array_equal(g.download(), want)
+    assert g.info()[:2] == (2, level)

@@ -83,4 +83,75 @@ def test_malformed_and_seeded_inputs_follow_seal(hecdna):
         hecdna.seal_ciphertext_load(b[:100])
     seeded = sf.ciphertext(d, 2.0**40, MOD, seeded_c0_only=True)
     with pytest.raises(hecdna.InvalidArgument, match="seeded ciphertext"):
-        hecdna.seal_ciphertext_load(seeded)
+        hecdna.seal_ciphertext_load(seeded)       # no context moduli: SEAL's load needs the context too
+
+
+# ---- seeded ciphertexts: Ciphertext::expand_seed (SEAL 4.1 Blake2xbPRNG + sample_poly_uniform)
+def test_python_blake2b_param_restatement_matches_hashlib():
+    """Pin the test restatement's compression to hashlib wherever hashlib can express the parameter block."""
+    for n in (0, 5, 128, 300):
+        data = bytes(range(256))[: n % 256] * (1 + n // 256)
+        data = data[:n]
+        assert sf.blake2b_param(data, sf.param_block(64)) == hashlib.blake2b(data).digest()
+        key = bytes(range(64))
+        assert sf.blake2b_param(data, sf.param_block(64, 64), key) == hashlib.blake2b(data, key=key).digest()
+        root = hashlib.blake2b(data, key=key, fanout=1, depth=1, node_offset=4096 << 32).digest()
+        assert sf.blake2b_param(data, sf.param_block(64, 64, xof=4096), key) == root  # the BLAKE2Xb root node
+
+
+@pytest.mark.parametrize("outlen", [1, 63, 64, 65, 200, 4096])
+def test_blake2xb_equals_restatement(hecdna, outlen):
+    key = bytes((7 * i + 3) & 0xFF for i in range(64))
+    data = (5).to_bytes(8, "little")
+    assert hecdna.seal_blake2xb(data, key, outlen) == sf.blake2xb(data, key, outlen)
+    # a prefix of a longer XOF output is NOT the shorter output (the length is in every node's parameters)
+    if outlen > 8:
+        assert hecdna.seal_blake2xb(data, key, outlen)[:8] != hecdna.seal_blake2xb(data, key, 8)
+
+
+@pytest.mark.parametrize("level,compr", [(1, 0), (3, 1), (4, 2)])
+def test_seeded_ciphertext_expands_like_seal(hecdna, level, compr):
+    """encrypt_symmetric(...).save writes c0 + seed (client.cpp:113-114); Ciphertext::load expands c1."""
+    d = rand_ct(2, level, seed=level)
+    seed = np.random.default_rng(100 + level).integers(0, 2**63, 8, dtype=np.uint64).tobytes()
+    b = sf.ciphertext(d, 2.0**40, MOD, seeded_c0_only=True, seed=seed, compr=min(compr, 1))  # zstd: round trip
+    got, scale, pid, used = hecdna.seal_ciphertext_load(b + b"tail", moduli=MOD)
+    assert used == len(b) and scale == 2.0**40 and got.shape == (2, level, N)
+    assert np.array_equal(got[0], d[0])
+    want = sf.expand_seed_c1(seed, MOD[:level], N)
+    assert np.array_equal(got[1], want)
+    for j in range(level):
+        assert int(got[1][j].max()) < MOD[j]
+    # the expanded ciphertext saves as an ordinary (unseeded) object and loads back unchanged
+    again, _, _, _ = hecdna.seal_ciphertext_load(hecdna.seal_ciphertext_save(got, 2.0**40, MOD, compr))
+    assert np.array_equal(again, got)
+
+
+def test_seeded_ciphertext_rejections(hecdna):
+    d = rand_ct(2, 2)
+    seed = bytes(range(64))
+    with pytest.raises(hecdna.InvalidArgument, match="ciphertext data is invalid"):       # parms_id of 3 primes
+        hecdna.seal_ciphertext_load(sf.ciphertext(d, 1.0, MOD, seeded_c0_only=True, seed=seed,
+                                                  pid=sf.parms_id(N, MOD[:3])), moduli=MOD)
+    with pytest.raises(hecdna.InvalidArgument, match="ciphertext data is invalid"):       # fewer context primes
+        hecdna.seal_ciphertext_load(sf.ciphertext(d, 1.0, MOD, seeded_c0_only=True, seed=seed), moduli=MOD[:1])
+    with pytest.raises(hecdna.InvalidArgument, match="prng_type"):                        # shake256
+        hecdna.seal_ciphertext_load(sf.ciphertext(d, 1.0, MOD, seeded_c0_only=True, seed=seed, prng_type=2),
+                                    moduli=MOD)
+
+
+def test_prng_rejection_redraws_from_stream_continuation(hecdna):
+    """A word is redrawn with probability ((2^64-1) mod q + 2) / 2^64 — about 2^-40 for SEAL's primes, so the
+    redraw path is exercised with a modulus whose remainder is large (q = 3 * 2^61 + 1, about 1 in 4 words):
+    redraws come from the stream after the bulk draw, in the C++ loader and the restatement alike."""
+    q = 3 * (1 << 61) + 1
+    n = 256
+    c1 = sf.expand_seed_c1(bytes(64), [q], n)
+    words = np.frombuffer(sf.Blake2xbStream(bytes(64)).take(n * 8), dtype=np.uint64)
+    rejected = words >= np.uint64(((1 << 64) - 1) - ((1 << 64) - 1) % q - 1)
+    assert 20 < int(rejected.sum()) < 120
+    keep = ~rejected
+    assert np.array_equal(c1[0][keep], words[keep] % np.uint64(q))
+    d = np.zeros((2, 1, n), dtype=np.uint64)
+    got, _, _, _ = hecdna.seal_ciphertext_load(sf.ciphertext(d, 1.0, [q], seeded_c0_only=True), moduli=[q])
+    assert np.array_equal(got[1], c1)
