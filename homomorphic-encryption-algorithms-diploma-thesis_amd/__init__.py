@@ -130,6 +130,7 @@ def lib():
             "hec_seal_ciphertext_load_ex": [vp, C.c_uint64, u64p, C.c_uint64, u64p, u64p, u64p,
                                             C.POINTER(C.c_double), u64p, u64p, C.c_uint64, u64p],
             "hec_seal_blake2xb": [vp, C.c_uint64, vp, C.c_uint64, C.c_uint64, vp],
+            "hec_seal_shake256": [vp, C.c_uint64, C.c_uint64, vp],
             "hec_seal_ciphertext_save": [u64p, C.c_uint64, C.c_uint64, C.c_uint64, C.c_double, u64p, C.c_int, vp,
                                          C.c_uint64, u64p],
             "hec_seal_parms_load": [vp, C.c_uint64, u64p, u64p, C.c_uint64, u64p, u64p],
@@ -245,6 +246,13 @@ def seal_blake2xb(data: bytes, key: bytes, outlen: int) -> bytes:
     """BLAKE2Xb XOF output (SEAL's Blake2xbPRNG core)."""
     out = C.create_string_buffer(outlen)
     _seal_check(lib().hec_seal_blake2xb(C.c_char_p(data), len(data), C.c_char_p(key), len(key), outlen, out))
+    return out.raw
+
+
+def seal_shake256(data: bytes, outlen: int) -> bytes:
+    """SHAKE256 XOF output (SEAL's Shake256PRNG core)."""
+    out = C.create_string_buffer(outlen)
+    _seal_check(lib().hec_seal_shake256(C.c_char_p(data), len(data), outlen, out))
     return out.raw
 
 

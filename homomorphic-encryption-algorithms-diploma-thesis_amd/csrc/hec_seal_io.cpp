@@ -156,21 +156,85 @@ void blake2xb(u8 *out, std::size_t outlen, const u8 *in, std::size_t inlen, cons
     }
 }
 
-// SEAL 4.1 Blake2xbPRNG (randomgen.cpp): a byte stream of 4096-byte buffers, buffer k = BLAKE2Xb(input = the
-// u64 counter k, key = the 64-byte prng_seed_type), served in order by UniformRandomGenerator::generate.
-struct Blake2xbStream {
+// SHAKE256 (FIPS 202: Keccak-f[1600], rate 136 bytes, domain byte 0x1F), behind SEAL's Shake256PRNG.
+void keccak_f1600(u64 a[25])
+{
+    static const u64 rc[24] = {
+        0x0000000000000001ULL, 0x0000000000008082ULL, 0x800000000000808aULL, 0x8000000080008000ULL,
+        0x000000000000808bULL, 0x0000000080000001ULL, 0x8000000080008081ULL, 0x8000000000008009ULL,
+        0x000000000000008aULL, 0x0000000000000088ULL, 0x0000000080008009ULL, 0x000000008000000aULL,
+        0x000000008000808bULL, 0x800000000000008bULL, 0x8000000000008089ULL, 0x8000000000008003ULL,
+        0x8000000000008002ULL, 0x8000000000000080ULL, 0x000000000000800aULL, 0x800000008000000aULL,
+        0x8000000080008081ULL, 0x8000000000008080ULL, 0x0000000080000001ULL, 0x8000000080008008ULL};
+    static const int rho[25] = {0, 1, 62, 28, 27, 36, 44, 6, 55, 20, 3, 10, 43, 25, 39, 41, 45, 15, 21, 8, 18, 2, 61, 56, 14};
+    auto rotl = [](u64 x, int n) { return n ? (x << n) | (x >> (64 - n)) : x; };
+    for (int r = 0; r < 24; ++r) {
+        u64 c[5], b[25];
+        for (int x = 0; x < 5; ++x) c[x] = a[x] ^ a[x + 5] ^ a[x + 10] ^ a[x + 15] ^ a[x + 20];
+        for (int x = 0; x < 5; ++x) {
+            const u64 d = c[(x + 4) % 5] ^ rotl(c[(x + 1) % 5], 1);
+            for (int y = 0; y < 25; y += 5) a[y + x] ^= d;
+        }
+        for (int x = 0; x < 5; ++x)
+            for (int y = 0; y < 5; ++y) b[y + 5 * ((2 * x + 3 * y) % 5)] = rotl(a[x + 5 * y], rho[x + 5 * y]);
+        for (int y = 0; y < 25; y += 5)
+            for (int x = 0; x < 5; ++x) a[y + x] = b[y + x] ^ (~b[y + (x + 1) % 5] & b[y + (x + 2) % 5]);
+        a[0] ^= rc[r];
+    }
+}
+void shake256(u8 *out, std::size_t outlen, const u8 *in, std::size_t inlen)
+{
+    constexpr std::size_t rate = 136;
+    u64 a[25] = {};
+    auto absorb = [&](const u8 *blk) {
+        for (std::size_t i = 0; i < rate / 8; ++i) {
+            u64 w;
+            std::memcpy(&w, blk + 8 * i, 8);
+            a[i] ^= w;
+        }
+        keccak_f1600(a);
+    };
+    for (; inlen >= rate; in += rate, inlen -= rate) absorb(in);
+    u8 last[rate] = {};
+    if (inlen) std::memcpy(last, in, inlen);
+    last[inlen] ^= 0x1F;
+    last[rate - 1] ^= 0x80;
+    absorb(last);
+    while (outlen) {
+        const std::size_t k = std::min(outlen, rate);
+        std::memcpy(out, a, k);  // little-endian lanes
+        out += k;
+        outlen -= k;
+        if (outlen) keccak_f1600(a);
+    }
+}
+
+// SEAL 4.1 UniformRandomGenerator (randomgen.cpp): a byte stream of 4096-byte buffers served in order by
+// generate(); buffer k is Blake2xbPRNG's BLAKE2Xb(input = the u64 counter k, key = the 64-byte
+// prng_seed_type) or Shake256PRNG's SHAKE256(seed || u64 counter k).
+struct PrngStream {
+    int type = 1;  // prng_type: 1 blake2xb, 2 shake256
     u8 seed[64];
     u64 counter = 0;
     u8 buf[4096];
     std::size_t head = sizeof(buf);
+    void refill()
+    {
+        if (type == 1) {
+            blake2xb(buf, sizeof(buf), reinterpret_cast<const u8 *>(&counter), 8, seed, 64);
+        } else {
+            u8 ext[72];
+            std::memcpy(ext, seed, 64);
+            std::memcpy(ext + 64, &counter, 8);
+            shake256(buf, sizeof(buf), ext, sizeof(ext));
+        }
+        ++counter;
+        head = 0;
+    }
     void generate(u8 *dst, std::size_t n)
     {
         while (n) {
-            if (head == sizeof(buf)) {
-                blake2xb(buf, sizeof(buf), reinterpret_cast<const u8 *>(&counter), 8, seed, 64);
-                ++counter;
-                head = 0;
-            }
+            if (head == sizeof(buf)) refill();
             const std::size_t k = std::min(n, sizeof(buf) - head);
             std::memcpy(dst, buf + head, k);
             head += k;
@@ -184,7 +248,7 @@ struct Blake2xbStream {
 // object: fill the level x N words from the stream in one draw, then per prime q_j reject each word
 // >= max_multiple = (2^64 - 1) - ((2^64 - 1) mod q_j) - 1 by redrawing it from the stream's continuation,
 // and reduce mod q_j.  In NTT form (CKKS) the uniform c1 is used as drawn.
-void sample_poly_uniform(Blake2xbStream &prng, const u64 *q, u64 level, u64 N, u64 *dst)
+void sample_poly_uniform(PrngStream &prng, const u64 *q, u64 level, u64 N, u64 *dst)
 {
     prng.generate(reinterpret_cast<u8 *>(dst), level * N * 8);
     const u64 max_random = ~0ULL;
@@ -476,7 +540,8 @@ void parms_id_of(u64 N, const u64 *moduli, u64 count, u64 out[4])
 }
 
 // Ciphertext::expand_seed (ciphertext.cpp) for a version-4 object: c1 = sample_poly_uniform over the
-// ciphertext's own primes q_0..q_{level-1}, drawn from the seed's Blake2xbPRNG.
+// ciphertext's own primes q_0..q_{level-1}, drawn from the seed's PRNG (Blake2xbPRNG, SEAL's default, or
+// Shake256PRNG).
 void expand_seed(CtData &c, const u64 *q, u64 count)
 {
     if (!q) throw std::invalid_argument("seeded ciphertext: the context's coeff_modulus is needed to expand it");
@@ -485,11 +550,12 @@ void expand_seed(CtData &c, const u64 *q, u64 count)
     parms_id_of(c.N, q, c.level, want);
     if (std::memcmp(want, c.parms_id, 32) != 0) throw std::invalid_argument("ciphertext data is invalid");
     if (c.major != 4) throw std::invalid_argument("seeded ciphertext: only SEAL 4.x seed expansion is supported");
-    if (c.prng_type != 1)
-        throw std::invalid_argument("seeded ciphertext: unsupported prng_type (only blake2xb, SEAL's default)");
+    if (c.prng_type != 1 && c.prng_type != 2)
+        throw std::invalid_argument("seeded ciphertext: unsupported prng_type");
     const u64 half = c.N * c.level;
     c.data.resize(2 * half);
-    Blake2xbStream prng;
+    PrngStream prng;
+    prng.type = c.prng_type;
     std::memcpy(prng.seed, c.seed, 64);
     sample_poly_uniform(prng, q, c.level, c.N, c.data.data() + half);
     c.seeded = false;
@@ -576,6 +642,14 @@ int hec_seal_ciphertext_load(const void *bytes, uint64_t nbytes, uint64_t *size,
 {
     return hec_seal_ciphertext_load_ex(bytes, nbytes, nullptr, 0, size, level, N, scale, parms_id, data, data_words,
                                        consumed);
+}
+
+int hec_seal_shake256(const void *in, uint64_t n, uint64_t outlen, void *out)
+{
+    return io_guard([&] {
+        if (!out || !outlen || (!in && n)) throw std::invalid_argument("invalid argument");
+        shake256(static_cast<u8 *>(out), outlen, static_cast<const u8 *>(in), n);
+    });
 }
 
 int hec_seal_blake2xb(const void *in, uint64_t n, const void *key, uint64_t keylen, uint64_t outlen, void *out)

@@ -218,12 +218,14 @@ int hec_seal_ciphertext_load(const void *bytes, uint64_t nbytes, uint64_t *size,
 /* Ciphertext::load(context, ...) including a seeded object (c0 + UniformRandomGeneratorInfo, as
  * Encryptor::encrypt_symmetric(...).save writes it: src/demos/client.cpp:113-114): c1 is expanded with SEAL 4.1's
  * Ciphertext::expand_seed (Blake2xbPRNG + sample_poly_uniform) over coeff_modulus[0..level); the parms_id must
- * match.  coeff_modulus = NULL behaves as hec_seal_ciphertext_load (a seeded object is an error). */
+ * match; prng_type blake2xb (SEAL's default) or shake256.  coeff_modulus = NULL behaves as hec_seal_ciphertext_load (a seeded object is an error). */
 int hec_seal_ciphertext_load_ex(const void *bytes, uint64_t nbytes, const uint64_t *coeff_modulus, uint64_t count,
                                 uint64_t *size, uint64_t *level, uint64_t *poly_modulus_degree, double *scale,
                                 uint64_t parms_id[4], uint64_t *data, uint64_t data_words, uint64_t *consumed);
 /* BLAKE2Xb XOF (SEAL util/blake2xb.c, behind Blake2xbPRNG): outlen bytes of BLAKE2Xb(in) keyed with key */
 int hec_seal_blake2xb(const void *in, uint64_t nbytes, const void *key, uint64_t keylen, uint64_t outlen, void *out);
+/* SHAKE256 XOF (behind SEAL's Shake256PRNG) */
+int hec_seal_shake256(const void *in, uint64_t nbytes, uint64_t outlen, void *out);
 int hec_seal_ciphertext_save(const uint64_t *data, uint64_t size, uint64_t level, uint64_t poly_modulus_degree,
                              double scale, const uint64_t *coeff_modulus, int compr_mode, void *out, uint64_t cap,
                              uint64_t *written);

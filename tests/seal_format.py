@@ -135,22 +135,25 @@ def blake2xb(data: bytes, key: bytes, outlen: int) -> bytes:
 
 
 class Blake2xbStream:
-    """SEAL 4.1 Blake2xbPRNG as a byte stream: buffer k = BLAKE2Xb(u64 k, key = seed, 4096 bytes)."""
+    """SEAL 4.1 Blake2xbPRNG as a byte stream: buffer k = BLAKE2Xb(u64 k, key = seed, 4096 bytes); with
+    prng_type 2, Shake256PRNG: buffer k = SHAKE256(seed || u64 k, 4096 bytes) (hashlib)."""
 
-    def __init__(self, seed: bytes):
-        self.seed, self.counter, self.buf = seed, 0, b""
+    def __init__(self, seed: bytes, prng_type=1):
+        self.seed, self.counter, self.buf, self.type = seed, 0, b"", prng_type
 
     def take(self, n: int) -> bytes:
         while len(self.buf) < n:
-            self.buf += blake2xb(struct.pack("<Q", self.counter), self.seed, 4096)
+            ctr = struct.pack("<Q", self.counter)
+            self.buf += (blake2xb(ctr, self.seed, 4096) if self.type == 1
+                         else hashlib.shake_256(self.seed + ctr).digest(4096))
             self.counter += 1
         out, self.buf = self.buf[:n], self.buf[n:]
         return out
 
 
-def expand_seed_c1(seed: bytes, moduli, N) -> np.ndarray:
+def expand_seed_c1(seed: bytes, moduli, N, prng_type=1) -> np.ndarray:
     """Ciphertext::expand_seed for a version-4 object: sample_poly_uniform over moduli -> u64[level][N]."""
-    prng = Blake2xbStream(seed)
+    prng = Blake2xbStream(seed, prng_type)
     words = list(struct.unpack("<%dQ" % (len(moduli) * N), prng.take(8 * len(moduli) * N)))
     out = np.zeros((len(moduli), N), dtype=np.uint64)
     for j, q in enumerate(moduli):

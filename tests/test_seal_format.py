@@ -135,9 +135,24 @@ def test_seeded_ciphertext_rejections(hecdna):
                                                   pid=sf.parms_id(N, MOD[:3])), moduli=MOD)
     with pytest.raises(hecdna.InvalidArgument, match="ciphertext data is invalid"):       # fewer context primes
         hecdna.seal_ciphertext_load(sf.ciphertext(d, 1.0, MOD, seeded_c0_only=True, seed=seed), moduli=MOD[:1])
-    with pytest.raises(hecdna.InvalidArgument, match="prng_type"):                        # shake256
-        hecdna.seal_ciphertext_load(sf.ciphertext(d, 1.0, MOD, seeded_c0_only=True, seed=seed, prng_type=2),
+    with pytest.raises(hecdna.InvalidArgument, match="prng_type"):                        # prng_type::unknown
+        hecdna.seal_ciphertext_load(sf.ciphertext(d, 1.0, MOD, seeded_c0_only=True, seed=seed, prng_type=0),
                                     moduli=MOD)
+
+
+@pytest.mark.parametrize("n,outlen", [(0, 32), (72, 4096), (135, 136), (136, 137), (300, 500)])
+def test_shake256_matches_hashlib(hecdna, n, outlen):
+    data = bytes((3 * i + 1) & 0xFF for i in range(n))
+    assert hecdna.seal_shake256(data, outlen) == hashlib.shake_256(data).digest(outlen)
+
+
+def test_seeded_ciphertext_shake256_prng(hecdna):
+    d = rand_ct(2, 2, seed=9)
+    seed = bytes(range(100, 164))
+    got, _, _, _ = hecdna.seal_ciphertext_load(sf.ciphertext(d, 1.0, MOD, seeded_c0_only=True, seed=seed,
+                                                             prng_type=2), moduli=MOD)
+    assert np.array_equal(got[1], sf.expand_seed_c1(seed, MOD[:2], N, prng_type=2))
+    assert np.array_equal(got[0], d[0])
 
 
 def test_prng_rejection_redraws_from_stream_continuation(hecdna):
