@@ -91,3 +91,24 @@ def test_seeded_ciphertext_load_on_device(env, hecdna):
     want = np.stack([c0[0], sf.expand_seed_c1(seed, e.m[:level], e.N)])
     assert np.array_equal(g.download(), want)
     assert g.info()[:2] == (2, level)
+
+
+def test_server_flow_on_seeded_client_ciphertext(env, hecdna, tmp_path):
+    """server.cpp:99-152 on what client.cpp:113-114 really sends: op1 as a seeded encrypt_symmetric(...).save
+    object (c0 + seed).  The C++ drop-in's ct.load expands c1; the result is bit-exact against the oracle run
+    on the expanded operand."""
+    e = env
+    op1, op2 = e.enc(seed=21), e.enc(seed=22)
+    seed = bytes((11 * i + 5) & 0xFF for i in range(64))
+    c1 = sf.expand_seed_c1(seed, e.m[:op1.level], e.N)
+    op1x = e.orc.Ct(np.stack([op1.data[0], c1]), op1.scale)
+    buf = (sf.parms(e.N, e.m) + sf.kswitch_keys(e.N, e.m, [e.rk_h])
+           + sf.ciphertext(op1.data, op1.scale, e.m, seeded_c0_only=True, seed=seed)
+           + sf.ciphertext(op2.data, op2.scale, e.m))
+    inp, outp = tmp_path / "client.bin", tmp_path / "server.bin"
+    inp.write_bytes(buf)
+    subprocess.check_call(["make", "-s", "-C", PKG, "bin/he_demo"])
+    subprocess.check_call([os.path.join(PKG, "bin", "he_demo"), "server", str(inp), str(outp)])
+    data, scale, _, _ = hecdna.seal_ciphertext_load(outp.read_bytes())
+    exp = e.o.rescale(e.o.relinearize(e.o.multiply(op1x, op2), e.rk_h))
+    assert np.array_equal(data, exp.data) and scale == exp.scale
