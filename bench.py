@@ -326,6 +326,10 @@ def main():
             "cpu_baseline": cpu,
             "whole_step_algorithmic_GBps": round(algo_mv * total / dt / 1e9, 2),
             "breakdown_ms_one_step": breakdown,
+            "profile_schedule": (None if args.no_profile else
+                                 f"one extra untimed step after the timed ones, the batch of {args.batch} as ONE lane "
+                                 f"on the context stream (profiling turns the concurrent lanes off so each launch "
+                                 f"has the GPU to itself); asynchronous HIP event pairs per launch"),
         }
         print(json.dumps(line))
     if dist is not None:
