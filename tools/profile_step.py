@@ -11,13 +11,14 @@ trace, bench, out = sys.argv[1:4]
 line = json.loads(open(bench).read().strip().splitlines()[-1])
 roof = line["roofline"]
 kern, nlast = roof["kernel"], roof["launches_per_step"]
-durs = []
+by_kernel = {}
 for r in csv.DictReader(open(trace)):
     name = r["Kernel_Name"]
     base = name[name.find("k_"):].split("<")[0].split("(")[0] if "k_" in name else name
-    if base == kern:
-        durs.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]) - int(r["Start_Timestamp"])))
-durs.sort()
+    by_kernel.setdefault(base, []).append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]) - int(r["Start_Timestamp"])))
+for v in by_kernel.values():
+    v.sort()
+durs = by_kernel.get(kern, [])
 last = [d for _, d in durs[-nlast:]]
 res = {"kernel": kern, "profile_step_dispatches": len(last),
        "profile_step_avg_us": round(sum(last) / len(last) / 1e3, 2),
@@ -25,5 +26,17 @@ res = {"kernel": kern, "profile_step_dispatches": len(last),
        "all_dispatches": len(durs), "all_dispatch_avg_us": round(sum(d for _, d in durs) / len(durs) / 1e3, 2),
        "note": "timed steps run the batch as concurrent lanes (smaller, overlapping launches); the profile "
                "step runs one lane, as the event-timed roofline does"}
+# every kernel of the bench's per-kernel table over the same profile step (its last `launches` dispatches):
+# rocprof's own time shares for the single-lane step, to set beside the whole-run stats CSV, whose shares
+# are inflated for kernels that overlap each other in the concurrent lanes
+step = {}
+for k, v in line.get("kernels_one_step", {}).items():
+    d = by_kernel.get(k, [])[-v["launches"]:]
+    if d:
+        step[k] = {"rocprof_ms": round(sum(x for _, x in d) / 1e6, 3), "event_ms": v["ms"], "dispatches": len(d)}
+tot = sum(v["rocprof_ms"] for v in step.values()) or 1.0
+for v in step.values():
+    v["share"] = round(v["rocprof_ms"] / tot, 3)
+res["profile_step_kernels"] = step
 json.dump(res, open(out, "w"), indent=1)
 print(json.dumps(res))
