@@ -68,7 +68,23 @@ def pmc_traffic(kernel, B, logn, level, n):
     return p["traffic_bytes_per_dispatch"]
 
 
+def cgroup_cpu_quota():
+    """CPUs granted by the cgroup's CPU quota (cgroup v2 cpu.max, else v1 cfs_quota/period), or None."""
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else max(1, int(-(-int(q) // int(p))))
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        p = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        return None if q <= 0 else max(1, -(-q // p))
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_info():
+    """(model, host CPUs, affinity CPUs, threads the CPU leg uses, why that many)."""
     model = "unknown"
     try:
         for ln in open("/proc/cpuinfo"):
@@ -78,11 +94,28 @@ def cpu_info():
     except OSError:
         pass
     share = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
-    # the GPU pool gives one GPU job a CPU share of OMP_NUM_THREADS cores (16) on a larger host: use all of
-    # that share; os.cpu_count() is the whole host
+    quota = cgroup_cpu_quota()
     omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
-    threads = min(share, omp) if omp > 0 else share
-    return model, os.cpu_count(), share, threads
+    if quota is not None and quota < share:
+        return model, os.cpu_count(), share, quota, f"cgroup CPU quota ({quota} CPUs)"
+    if omp > 0 and omp < share:
+        # the GPU pool's per-job CPU share (16 per GPU) is announced through OMP_NUM_THREADS and not enforced by
+        # a cgroup quota or the affinity mask, which span the whole host: the leg uses that share
+        return model, os.cpu_count(), share, omp, f"the job's CPU share OMP_NUM_THREADS={omp} (affinity {share})"
+    return model, os.cpu_count(), share, share, f"affinity mask ({share} CPUs)"
+
+
+def free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launcher_cmd(ngpus, argv, port):
+    """The one-process-per-GPU launch of this script (torch.distributed.run, rendezvous on 127.0.0.1)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={ngpus}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
 
 
 def cpu_baseline(N, moduli, n, sample_diags, threads):
@@ -124,6 +157,31 @@ def cpu_baseline(N, moduli, n, sample_diags, threads):
     return {"full_s": full, "one_core_s": one * ks_total(N, n) / ks_sample, "ks_sample": ks_sample}
 
 
+def dry_run(args, world, rank):
+    """--dry-run: the launcher, the process group, the max-over-ranks timing and the rank-0 line over gloo,
+    with no GPU and no engine (tests/test_bench_measurement.py runs it at world size 2 on the CPU)."""
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("gloo")
+    t0 = time.perf_counter()
+    for _ in range(args.warmup + args.steps):
+        if world > 1:
+            dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    if rank == 0:
+        print(json.dumps({"metric": "CKKS matvec ciphertexts/sec (N=2^15, L=10)", "value": 0.0, "unit": "matvec/s",
+                          "n_gpus": world, "rccl_world": dist.get_world_size() if world > 1 else 1,
+                          "dist_backend": "gloo", "dry_run": True, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": round(dt / max(1, args.steps) * 1e3, 3)}))
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -147,15 +205,31 @@ def main():
                     help="cfg3: the BASELINE metric (4096x4096 matvec, N=2^15, L=10); cfg5: BASELINE configs[4], "
                          "the 1024x1024x1024 ct x ct matmul at N=2^16, L=16, measured as output columns per second "
                          "(a step = --batch columns of the product; not the metric)")
+    ap.add_argument("--sharded-steps", type=int, default=None,
+                    help="throughput mode at N > 1: after the timed steps, also time this many row-sharded steps of "
+                         "one batch (the cfg4 strong-scaling figure, reported under 'sharded'; default 1 at N > 1)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="exercise the launcher and the rank-0 line over gloo without touching a GPU (CPU tests)")
     args = ap.parse_args()
     if args.config == "cfg5":
         args.logn, args.n = 16, 1024
         if args.batch == ap.get_default("batch"):
             args.batch = 32
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # one process per GPU: start the N ranks as a child launcher before anything touches a GPU, relay its
+        # exit status (rank 0 prints the line)
+        import subprocess
+        env = dict(os.environ)
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        sys.stdout.flush()
+        sys.exit(subprocess.call(launcher_cmd(args.gpus, sys.argv[1:], free_port()), env=env))
+
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dry_run:
+        return dry_run(args, world, rank)
     # torch first, at every N: libhecdna then binds to torch's HIP runtime, so the RCCL buffers and
     # the engine share one runtime and the 1-GPU and N-GPU runs execute the same code
     import torch
@@ -206,9 +280,19 @@ def main():
             torch.cuda.synchronize(local)
             dist.barrier()
 
+    def max_over_ranks(dt):
+        if dist is None:
+            return dt
+        import torch
+        t = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    last_sharded = [None]
+
     def step():
         if sharded:
-            shard.sharded_matvec(ctx, diags, cols, rk, gk, rank, world, plan=plan)
+            last_sharded[0] = shard.sharded_matvec(ctx, diags, cols, rk, gk, rank, world, plan=plan)
         elif ctpt:
             ctx.matmul_diagpt_col(diags, cols, gk, out=outs)
         else:
@@ -223,17 +307,49 @@ def main():
         step()
     ctx.synchronize()
     barrier()
-    dt = time.perf_counter() - t0
-    if dist is not None:
-        import torch
-        t = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local}")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+    dt = max_over_ranks(time.perf_counter() - t0)
 
     ms_per_step = dt / args.steps * 1e3
     total = args.batch * (1 if sharded else world) * args.steps
     value = total / dt
     ks = ks_total(N, args.n)
+
+    def sharded_selfcheck(res, cols_used):
+        """Rank 0: its first finished outputs of a sharded step against a 1-rank matmul_diag_col of the same inputs
+        (every diagonal; the ones rank 0 does not hold are regenerated from their seeds).  Local, no collective."""
+        mine, fin = res
+        k = min(2, len(mine))
+        full = [d if d is not None else ctx.ciphertext().fill_uniform(2, L, scale, 10_000 + j)
+                for j, d in enumerate(diags)]
+        ref = ctx.matmul_diag_col(full, [cols_used[i] for i in mine[:k]], rk, gk)
+        ok = all(np.array_equal(a.download(), b.download()) and a.info() == b.info() for a, b in zip(fin[:k], ref))
+        return {"outputs_checked": k, "bitexact": bool(ok)}
+
+    # cfg4 (BASELINE configs[3]) beside the metric: one batch split over the ranks by rotation-trie subtrees of the
+    # diagonals, one RCCL reduce-scatter of the size-3 partials (strong scaling), timed after the metric's steps
+    sharded_extra = None
+    nsh = args.sharded_steps if args.sharded_steps is not None else (1 if world > 1 else 0)
+    if not sharded and not ctpt and nsh > 0:
+        import hecdna.shard as shard
+        splan = shard.plan_diagonal_shards(N, args.n, world)
+        scols = cols if rank == 0 else [ctx.ciphertext().fill_uniform(2, L, scale, 90_000 + i)
+                                        for i in range(args.batch)]  # rank 0's batch on every rank
+        res = shard.sharded_matvec(ctx, diags, scols, rk, gk, rank, world, plan=splan)  # warmup
+        ctx.synchronize()
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(nsh):
+            res = shard.sharded_matvec(ctx, diags, scols, rk, gk, rank, world, plan=splan)
+        ctx.synchronize()
+        barrier()
+        sdt = max_over_ranks(time.perf_counter() - t0)
+        sharded_extra = {"value": round(args.batch * nsh / sdt, 6), "unit": "matvec/s", "steps": nsh,
+                         "ms_per_step": round(sdt / nsh * 1e3, 3), "scaling": "strong", "batch": args.batch,
+                         "key_switches_per_rank": [shard.trie_cost(N, p) for p in splan]}
+        if rank == 0:
+            sharded_extra["self_check"] = sharded_selfcheck(res, scols)
+    if sharded and rank == 0 and last_sharded[0] is not None:
+        sharded_extra = {"self_check": sharded_selfcheck(last_sharded[0], cols)}
 
     # per-phase breakdown: one extra (untimed) step with asynchronous HIP event pairs recorded on the
     # context's stream around every phase (no host synchronisation inside the step)
@@ -289,13 +405,14 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not ctpt:
-        model, host_cpus, share, threads = cpu_info()
+        model, host_cpus, share, threads, why = cpu_info()
         res = cpu_baseline(N, moduli, args.n, args.cpu_sample_diags, threads)
         cpu = {"value": round(1.0 / res["full_s"], 6), "unit": "matvec/s", "cores": threads, "kind": "port",
                "sample": f"one full n={args.n} N=2^{args.logn} L={L} diag x col matvec ({ks} key switches, SEAL's "
                          f"per-rotation schedule, relinearize + rescale) by the oracle (C++ SEAL-semantics port, "
                          f"-march=native) on {threads} threads",
-               "cpu_model": model, "host_cpus": host_cpus, "cpus_available": share,
+               "cpu_model": model, "host_cpus": host_cpus, "cpus_available": share, "cores_reason": why,
+               "cgroup_cpu_quota": cgroup_cpu_quota(),
                "full_matvec_s": round(res["full_s"], 2),
                "one_core": {"value": round(1.0 / res["one_core_s"], 6), "cores": 1, "extrapolated": True,
                             "sample": f"diagonals j<{args.cpu_sample_diags} ({res['ks_sample']} key switches) "
@@ -307,7 +424,7 @@ def main():
             "metric": ("CKKS matvec ciphertexts/sec (N=2^15, L=10)" if args.config == "cfg3" else
                        "CKKS matmul output columns/sec (1024x1024x1024, N=2^16, L=16)"),
             "value": round(value, 6), "unit": "matvec/s" if args.config == "cfg3" else "columns/s",
-            "n_gpus": world, "steps": args.steps,
+            "n_gpus": world, "rccl_world": dist.get_world_size() if dist is not None else 1, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
             "scaling": "strong" if sharded else "weak", "vs_baseline": None, "dtype": "u64", "data": "synthetic",
             "config": {"workload": f"he_linalg BatchedMatrix::matmul diag x col, {args.n}x{args.n} "
@@ -322,6 +439,7 @@ def main():
                                               "key sums KW, galois_negw / galois_kw) are built once per key "
                                               "and level before the timed steps, like the keys themselves"},
             "roofline": roof,
+            "sharded": sharded_extra,
             "kernels_one_step": kernels,
             "cpu_baseline": cpu,
             "whole_step_algorithmic_GBps": round(algo_mv * total / dt / 1e9, 2),

@@ -138,6 +138,7 @@ def lib():
             "hec_seal_kswitch_keys_load": [vp, C.c_uint64, C.c_uint64, u64p, u64p, C.c_uint64, u64p, u64p],
             "hec_seal_kswitch_keys_save": [C.c_uint64, u64p, C.c_uint64, C.POINTER(u64p), u64p, C.c_uint64, C.c_int,
                                            vp, C.c_uint64, u64p],
+            "hec_seal_kswitch_keys_foreach": [vp, C.c_uint64, KEYLIST_VISIT, vp, u64p, u64p],
             "hec_ciphertext_load_seal": [vp, vp, C.c_uint64, u64p],
             "hec_ciphertext_save_seal": [vp, C.c_int, vp, C.c_uint64, u64p],
             "hec_kswitch_key_load_seal": [vp, vp, C.c_uint64, C.POINTER(vp), u64p],
@@ -294,6 +295,24 @@ def seal_kswitch_keys_save(N, moduli, key_lists, compr=COMPR_NONE) -> bytes:
     digits = np.array([0 if k is None else k.shape[0] for k in keep] or [0], dtype=np.uint64)
     return _sized_out(lambda o, c, w: lib().hec_seal_kswitch_keys_save(N, _p(m), len(m), ptrs, _p(digits), len(keep),
                                                                      compr, o, c, w))
+
+
+KEYLIST_VISIT = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_uint64, u64p, C.c_uint64)
+
+
+def seal_kswitch_keys_lists(b: bytes):
+    """hec_seal_kswitch_keys_foreach: every non-empty key list in one pass -> ({index: u64 words}, list count,
+    bytes consumed)"""
+    got = {}
+
+    def visit(_user, index, words, nwords):
+        got[int(index)] = np.ctypeslib.as_array(words, shape=(int(nwords),)).copy()
+        return 0
+    cb = KEYLIST_VISIT(visit)
+    lists, used = C.c_uint64(), C.c_uint64()
+    src, n = _bytes_in(b)
+    _seal_check(lib().hec_seal_kswitch_keys_foreach(src, n, cb, None, C.byref(lists), C.byref(used)))
+    return got, lists.value, used.value
 
 
 def seal_kswitch_keys_load(b: bytes, index):

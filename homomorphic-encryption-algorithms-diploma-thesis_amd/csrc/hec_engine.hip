@@ -251,7 +251,22 @@ void ensure(hec_ciphertext *ct, std::size_t words)
 struct Scratch {
     Ctx &c;
     std::size_t top = 0;
-    explicit Scratch(Ctx &cc, std::size_t words) : c(cc) { c.ws.reserve(words); }
+    explicit Scratch(Ctx &cc, std::size_t words) : c(cc)
+    {
+        c.ws.reserve(words, c.stream);
+        ++c.ws.depth;
+    }
+    ~Scratch()
+    {
+        if (--c.ws.depth == 0 && !c.ws.defer_free && !c.ws.retired.empty()) {
+            try {
+                c.ws.reclaim(c.stream);
+            } catch (...) {  // keep them for release(); a destructor must not throw
+            }
+        }
+    }
+    Scratch(const Scratch &) = delete;
+    Scratch &operator=(const Scratch &) = delete;
     u64 *take(std::size_t w)
     {
         w = (w + 63) & ~(std::size_t)63;
@@ -936,6 +951,7 @@ hec_context *make_lane(hec_context *parent, int index)
     Ctx &c = l->c;
     c = parent->c;  // shared device tables (twiddles, primes, maps), host constants and knobs
     c.ws = Workspace{};
+    c.ws.defer_free = true;  // grown from the lane's thread while the other lanes launch
     c.prof_mode = 0;
     c.prof_tab.clear();
     c.prof_pend.clear();
@@ -997,6 +1013,16 @@ void matvec_lanes(hec_context *ctx, const hec_ciphertext *const *diags, const he
             galois_kw(ctx, gkm, kv.first, (int)cols[0]->level);
         }
     }
+    // the outputs are sized here, on the calling thread, so no lane thread frees or allocates them (matvec_core's
+    // ensure() then finds them large enough)
+    {
+        const std::size_t l = cols[0]->level, N = c.N;
+        const std::size_t w = finish ? 2 * (l - 1) * N : (pdiags ? 2 : 3) * l * N;
+        for (std::size_t i = 0; i < p; ++i) {
+            need(out[i] != nullptr, "null argument");
+            ensure(out[i], w);
+        }
+    }
     while ((int)ctx->lanes.size() < nl) ctx->lanes.push_back(make_lane(ctx, (int)ctx->lanes.size()));
     if (!ctx->lanes_start) HEC_HIP(hipEventCreateWithFlags(&ctx->lanes_start, hipEventDisableTiming));
     hipEvent_t start = ctx->lanes_start;
@@ -1022,6 +1048,8 @@ void matvec_lanes(hec_context *ctx, const hec_ciphertext *const *diags, const he
     for (auto &t : th) t.join();
     for (int i = 0; i < nl; ++i)  // later work on the context sees the outputs
         if (done[i]) HEC_HIP(hipStreamWaitEvent(c.stream, ctx->lanes[i]->lane_done, 0));
+    for (int i = 0; i < nl; ++i)  // outgrown lane workspaces, now that no lane thread runs (waits only after a growth)
+        ctx->lanes[i]->c.ws.reclaim(ctx->lanes[i]->c.stream);
     for (auto &e : err)
         if (e) std::rethrow_exception(e);
 }
@@ -1146,13 +1174,21 @@ void nccl_check(ncclResult_t e, const char *what)
 }  // namespace
 
 // =============================================================================== workspace ==
-void hec::Workspace::reserve(std::size_t w)
+void hec::Workspace::reserve(std::size_t w, hipStream_t stream)
 {
     if (w <= words) return;
     if (std::getenv("HEC_DEBUG")) std::fprintf(stderr, "hec: workspace %zu -> %zu words\n", words, w);
-    if (base) retired.push_back(base);  // kernels already enqueued may still use it
+    (void)stream;
+    if (base) retired.push_back(base);  // reclaimed later (see Workspace)
     base = dalloc(w);
     words = w;
+}
+void hec::Workspace::reclaim(hipStream_t stream)
+{
+    if (retired.empty()) return;
+    HEC_HIP(hipStreamSynchronize(stream));
+    for (u64 *p : retired) HEC_HIP(hipFree(p));
+    retired.clear();
 }
 void hec::Workspace::release()
 {
@@ -1896,20 +1932,31 @@ int hec_galois_keys_load_seal(hec_galois_keys *gk, const void *bytes, uint64_t n
 {
     return guard([&] {
         need(gk && bytes, "null argument");
-        const Ctx &c = gk->ctx->c;
-        uint64_t lists = 0, used = 0;
-        seal_rc(hec_seal_kswitch_keys_load(bytes, nbytes, UINT64_MAX, &lists, nullptr, 0, nullptr, &used));
-        std::vector<u64> host;
-        for (uint64_t i = 0; i < lists; ++i) {  // GaloisKeys::get_index(elt) = (elt - 1) / 2
-            uint64_t words = 0;
-            seal_rc(hec_seal_kswitch_keys_load(bytes, nbytes, i, nullptr, nullptr, 0, &words, nullptr));
-            if (!words) continue;
-            need(words == c.L * 2 * c.K * c.N, "galois_keys is not valid for encryption parameters");
-            host.resize(words);
-            seal_rc(hec_seal_kswitch_keys_load(bytes, nbytes, i, nullptr, host.data(), words, nullptr, nullptr));
-            const int rc = hec_galois_keys_add(gk, (uint32_t)(2 * i + 1), host.data());
-            if (rc != HEC_OK) throw std::logic_error(hec_last_error());
+        struct Visit {
+            hec_galois_keys *gk;
+            std::string err;
+            int rc = HEC_OK;
+        } v{gk, {}};
+        // one pass over the object: GaloisKeys::get_index(elt) = (elt - 1) / 2, every non-empty list uploaded as it
+        // is parsed
+        auto cb = [](void *user, uint64_t index, const uint64_t *words, uint64_t nwords) -> int {
+            auto *st = static_cast<Visit *>(user);
+            const Ctx &c = st->gk->ctx->c;
+            if (nwords != c.L * 2 * c.K * c.N) {
+                st->err = "galois_keys is not valid for encryption parameters";
+                return st->rc = HEC_EINVAL;
+            }
+            const int rc = hec_galois_keys_add(st->gk, (uint32_t)(2 * index + 1), words);
+            if (rc != HEC_OK) st->err = hec_last_error();
+            return st->rc = rc;
+        };
+        uint64_t used = 0;
+        const int rc = hec_seal_kswitch_keys_foreach(bytes, nbytes, cb, &v, nullptr, &used);
+        if (v.rc != HEC_OK) {
+            if (v.rc == HEC_EINVAL) throw std::invalid_argument(v.err);
+            throw std::logic_error(v.err);
         }
+        seal_rc(rc);
         if (consumed) *consumed = used;
     });
 }
@@ -2231,6 +2278,9 @@ int hec_comm_init(hec_context *ctx, int rank, int world, const void *unique_id)
     return guard([&] {
         set_device(ctx);
         need(world >= 1 && rank >= 0 && rank < world, "invalid rank / world");
+        // the exchange adds `world` canonical residues < 2^60 in u64 (hec_matmul_diag_col_sharded); shard.py's
+        // int64 exchange has the same bound
+        need(world <= 8, "world must be at most 8 (exact u64 partial-sum exchange)");
         need(ctx->comm == nullptr, "communicator already initialised");
         if (world > 1 || unique_id) {  // world 1 with an id: a one-rank communicator (exercises the RCCL path)
             need(unique_id != nullptr, "null argument");
@@ -2259,17 +2309,58 @@ int hec_matmul_diag_col_sharded(hec_context *ctx, const hec_ciphertext *const *d
 {
     return guard([&] {
         set_device(ctx);
-        need(diags && cols && out && n >= 1 && p >= 1, "empty matrix operand");
-        need(gk && gk->ctx == ctx, "galois_keys is not valid for encryption parameters");
         need(ctx->world == 1 || ctx->comm, "hec_comm_init has not been called");
         Ctx &c = ctx->c;
-        std::vector<std::size_t> all(n);
-        for (uint64_t j = 0; j < n; ++j) all[j] = j;
-        matvec_check(ctx, diags, nullptr, n, all, cols, p, rk, gk, true);  // SEAL's errors, same on every rank
-        std::set<u32> keys;
-        for (const auto &kv : gk->keys) keys.insert(kv.first);
-        const auto plan = plan_shards(c.N, n, ctx->world, keys);
-        const std::vector<std::size_t> &mine = plan[ctx->rank];
+        // The argument checks run on this rank's planned diagonals only (the others are never dereferenced), then
+        // the ranks agree on them before any data-path collective, so a bad argument on one rank is an error on
+        // every rank instead of a rank left waiting in the exchange.  The product scales of the ranks' diagonals
+        // are compared across ranks too (SEAL's add_inplace "scale mismatch" over the whole sum).
+        std::vector<std::size_t> mine;
+        std::vector<double> ps;
+        int status = HEC_OK;
+        std::string msg;
+        try {
+            need(diags && cols && out && n >= 1 && p >= 1, "empty matrix operand");
+            need(gk && gk->ctx == ctx, "galois_keys is not valid for encryption parameters");
+            std::set<u32> keys;
+            for (const auto &kv : gk->keys) keys.insert(kv.first);
+            mine = plan_shards(c.N, n, ctx->world, keys)[ctx->rank];
+            ps = matvec_check(ctx, diags, nullptr, n, mine, cols, p, rk, gk, true);
+        } catch (const std::invalid_argument &e) {
+            status = HEC_EINVAL; msg = e.what();
+        } catch (const std::logic_error &e) {
+            status = HEC_ELOGIC; msg = e.what();
+        }
+        const Rccl *nc = ctx->comm ? &rccl() : nullptr;
+        if (nc) {
+            // [0] status << 8 | (rank + 1) of a failing rank (max), [1 .. p] product scales (min), [p+1 .. 2p] (max)
+            const uint64_t words = 1 + p;
+            std::vector<double> hv(words, 0.0), hmin(words), hmax(words);
+            hv[0] = status ? (double)((status << 8) | (ctx->rank + 1)) : 0.0;
+            for (uint64_t i = 0; i < p && i < ps.size(); ++i) hv[1 + i] = ps[i];
+            double *dv = nullptr;
+            HEC_HIP(hipMallocAsync((void **)&dv, 2 * words * sizeof(double), c.stream));
+            HEC_HIP(hipMemcpyAsync(dv, hv.data(), words * sizeof(double), hipMemcpyHostToDevice, c.stream));
+            HEC_HIP(hipMemcpyAsync(dv + words, hv.data(), words * sizeof(double), hipMemcpyHostToDevice, c.stream));
+            nccl_check(nc->all_reduce(dv, dv, words, ncclFloat64, ncclMin, (ncclComm_t)ctx->comm, c.stream), "ncclAllReduce");
+            nccl_check(nc->all_reduce(dv + words, dv + words, words, ncclFloat64, ncclMax, (ncclComm_t)ctx->comm, c.stream),
+                       "ncclAllReduce");
+            HEC_HIP(hipMemcpyAsync(hmin.data(), dv, words * sizeof(double), hipMemcpyDeviceToHost, c.stream));
+            HEC_HIP(hipMemcpyAsync(hmax.data(), dv + words, words * sizeof(double), hipMemcpyDeviceToHost, c.stream));
+            HEC_HIP(hipFreeAsync(dv, c.stream));
+            HEC_HIP(hipStreamSynchronize(c.stream));
+            const int agreed = (int)hmax[0];
+            if (!status && agreed) {
+                status = agreed >> 8;
+                msg = "matmul_diag_col_sharded: the arguments failed SEAL's checks on rank " +
+                      std::to_string((agreed & 0xff) - 1);
+            }
+            if (!status)
+                for (uint64_t i = 0; i < p; ++i)
+                    if (!are_close(hmin[1 + i], hmax[1 + i])) { status = HEC_EINVAL; msg = "scale mismatch"; }
+        }
+        if (status == HEC_EINVAL) throw std::invalid_argument(msg);
+        if (status) throw std::logic_error(msg);
         const std::size_t l = cols[0]->level, S3 = 3 * l * c.N;
         // this rank's size-3 partials over its trie subtrees of diagonals
         std::vector<hec_ciphertext> acc(p);
@@ -2280,13 +2371,13 @@ int hec_matmul_diag_col_sharded(hec_context *ctx, const hec_ciphertext *const *d
             ~Free() { for (auto &x : a) if (x.d) (void)hipFree(x.d); }
         } free_acc{acc};
         matvec_lanes(ctx, diags, nullptr, n, mine, cols, p, nullptr, gk, false, accp.data());
-        if (ctx->comm) {
+        if (nc) {
             // the one exchange: a plain u64 sum of the world's canonical residues (< world 2^60 < 2^64), then
             // reduce mod q; every rank then holds the full accumulators (he_linalg.cpp:977-997 summed)
             u64 *buf = nullptr;
             HEC_HIP(hipMallocAsync((void **)&buf, p * S3 * sizeof(u64), c.stream));
             for (uint64_t i = 0; i < p; ++i) d2d(c, buf + i * S3, acc[i].d, S3);
-            nccl_check(rccl().all_reduce(buf, buf, p * S3, ncclUint64, ncclSum, (ncclComm_t)ctx->comm, c.stream),
+            nccl_check(nc->all_reduce(buf, buf, p * S3, ncclUint64, ncclSum, (ncclComm_t)ctx->comm, c.stream),
                        "ncclAllReduce");
             ew_reduce(c, buf, (int)(3 * p), (int)l);
             for (uint64_t i = 0; i < p; ++i) d2d(c, acc[i].d, buf + i * S3, S3);

@@ -34,11 +34,16 @@ struct Ctx;
 struct Workspace {
     u64 *base = nullptr;
     std::size_t words = 0;
-    // outgrown bases, freed with the workspace: a lane that grows its workspace while the other lanes are
-    // launching must not free device memory under them (hipFree from a lane thread coincided with rare wrong
-    // lanes at full size)
+    // An outgrown base is retired, not freed: carved pointers of an enclosing Scratch and kernels already enqueued
+    // may still use it.  It is reclaimed (stream drained, then hipFree) when the outermost Scratch of the context
+    // ends; for batch lanes (defer_free) only by matvec_lanes after the lanes have joined, because a lane grows its
+    // workspace from its own host thread while the other lanes are launching, and hipFree there (it synchronises
+    // the device) coincided with rare wrong lanes at full size.  So a long-lived context does not accumulate them.
+    bool defer_free = false;
+    int depth = 0;  // live Scratch scopes on this workspace
     std::vector<u64 *> retired;
-    void reserve(std::size_t w);
+    void reserve(std::size_t w, hipStream_t stream);
+    void reclaim(hipStream_t stream);
     void release();
 };
 

@@ -367,18 +367,32 @@ const Zlib &zlib()
     return z;
 }
 
-std::vector<u8> inflate_zlib(const u8 *src, std::size_t n)
+// Decompressed member bytes are bounded: a client's bytes arrive over the socket (server.cpp:110-122), so a small
+// compressed payload must not expand without limit.  kMaxCtObject covers a ciphertext object (size <= 16 polys,
+// N <= 2^17, <= 64 limbs of u64: 1 GiB of words); kMaxKeysObject a KSwitchKeys object (GaloisKeys at N = 2^17,
+// every rotation key).
+constexpr std::size_t kMaxCtObject = (std::size_t)1 << 31;
+constexpr std::size_t kMaxKeysObject = (std::size_t)1 << 40;
+void check_growth(std::size_t want, std::size_t max_out)
+{
+    if (want > max_out) throw std::invalid_argument("decompressed SEAL object exceeds the size limit");
+}
+
+std::vector<u8> inflate_zlib(const u8 *src, std::size_t n, std::size_t max_out)
 {
     const Zlib &z = zlib();
     for (int wbits : {15 + 32, -15}) {  // zlib / gzip framing, then a raw deflate stream
         z_stream s{};
         if (z.inflate_init2(&s, wbits, ZLIB_VERSION, (int)sizeof(z_stream)) != Z_OK) continue;
-        std::vector<u8> out(std::max<std::size_t>(4 * n, 4096));
+        std::vector<u8> out(std::min(std::max<std::size_t>(4 * n, 4096), max_out + 1));
         s.next_in = const_cast<Bytef *>(src);
         s.avail_in = (uInt)n;
         int rc = Z_OK;
         while (rc == Z_OK) {
-            if (s.total_out == out.size()) out.resize(2 * out.size());
+            if (s.total_out == out.size()) {
+                check_growth(s.total_out, max_out);
+                out.resize(std::min(2 * out.size(), max_out + 1));
+            }
             s.next_out = out.data() + s.total_out;
             s.avail_out = (uInt)(out.size() - s.total_out);
             rc = z.inflate(&s, Z_NO_FLUSH);
@@ -387,24 +401,26 @@ std::vector<u8> inflate_zlib(const u8 *src, std::size_t n)
         const std::size_t got = s.total_out;
         z.inflate_end(&s);
         if (rc == Z_STREAM_END) {
+            check_growth(got, max_out);
             out.resize(got);
             return out;
         }
     }
     throw std::invalid_argument("zlib payload of the SEAL object is corrupt");
 }
-std::vector<u8> inflate_zstd(const u8 *src, std::size_t n)
+std::vector<u8> inflate_zstd(const u8 *src, std::size_t n, std::size_t max_out)
 {
     const Zstd &z = zstd();
     void *ds = z.create_d();
     z.init_d(ds);
-    std::vector<u8> out(std::max<std::size_t>(4 * n, 4096));
+    std::vector<u8> out(std::min(std::max<std::size_t>(4 * n, 4096), max_out + 1));
     ZInBuf in{src, n, 0};
     ZOutBuf ob{out.data(), out.size(), 0};
     std::size_t rc = 1;
     while (in.pos < in.size || rc != 0) {
         if (ob.pos == ob.size) {
-            out.resize(2 * out.size());
+            if (ob.pos > max_out) { z.free_d(ds); check_growth(ob.pos, max_out); }
+            out.resize(std::min(2 * out.size(), max_out + 1));
             ob.dst = out.data();
             ob.size = out.size();
         }
@@ -418,13 +434,14 @@ std::vector<u8> inflate_zstd(const u8 *src, std::size_t n)
         }
     }
     z.free_d(ds);
+    check_growth(ob.pos, max_out);
     out.resize(ob.pos);
     return out;
 }
 
-// One SEAL object: its header, then the members (decompressed when needed).  Returns the member bytes and
-// advances r past the whole object.
-std::vector<u8> open_object(Reader &r)
+// One SEAL object: its header, then the members (decompressed when needed, at most max_out bytes).  Returns the
+// member bytes and advances r past the whole object.
+std::vector<u8> open_object(Reader &r, std::size_t max_out = kMaxCtObject)
 {
     const Header h = r.get<Header>();
     if (h.magic != kMagic || h.header_size != kHeaderSize) throw std::invalid_argument("loaded SEALHeader is invalid");
@@ -436,8 +453,8 @@ std::vector<u8> open_object(Reader &r)
     r.p += n;
     switch (h.compr) {
     case 0: return std::vector<u8>(payload, payload + n);
-    case 1: return inflate_zlib(payload, n);
-    case 2: return inflate_zstd(payload, n);
+    case 1: return inflate_zlib(payload, n, max_out);
+    case 2: return inflate_zstd(payload, n, max_out);
     default: throw std::invalid_argument("unsupported compression mode");
     }
 }
@@ -500,6 +517,7 @@ CtData parse_ciphertext(Reader &outer, int major)
     const u64 count = d.get<u64>();
     const u64 full = c.size * c.N * c.level;
     if (count != full && !(c.size == 2 && count == c.N * c.level)) throw std::invalid_argument("ciphertext data is invalid");
+    d.need(count * 8);  // before allocating: the payload must hold the words it announces
     c.data.resize(count);
     d.bytes(c.data.data(), count * 8);
     c.major = major;
@@ -582,6 +600,39 @@ void copy_out(const std::vector<u8> &b, void *out, uint64_t cap, uint64_t *writt
     if (cap < b.size()) throw std::invalid_argument("output buffer is too small");
     std::memcpy(out, b.data(), b.size());
 }
+// KSwitchKeys (RelinKeys / GaloisKeys) in one pass: the object is opened and decompressed once, and every
+// non-empty key list (its PublicKeys' data back to back, the engine's key layout u64[L][2][K][N]) is handed to
+// visit(index, words, nwords) as soon as it is parsed.  SEAL's GaloisKeys carry N key lists, almost all empty
+// (KeyGenerator::create_galois_keys resizes the list array to the ring degree), so a per-list reparse would cost
+// N full parses.
+template <class F>
+void walk_kswitch_keys(const void *bytes, uint64_t nbytes, uint64_t *lists, uint64_t *consumed, F &&visit)
+{
+    if (!bytes) throw std::invalid_argument("invalid argument");
+    Reader outer{static_cast<const u8 *>(bytes), static_cast<const u8 *>(bytes) + nbytes};
+    Header h;
+    std::memcpy(&h, bytes, std::min<uint64_t>(nbytes, sizeof(h)));
+    std::vector<u8> m = open_object(outer, kMaxKeysObject);
+    Reader r{m.data(), m.data() + m.size()};
+    u64 pid[4];
+    r.bytes(pid, 32);
+    const u64 dim1 = r.get<u64>();
+    if (lists) *lists = dim1;
+    std::vector<u64> got;
+    for (u64 i = 0; i < dim1; ++i) {
+        const u64 dim2 = r.get<u64>();
+        got.clear();
+        for (u64 j = 0; j < dim2; ++j) {
+            std::vector<u8> pk = open_object(r, kMaxCtObject);  // PublicKey
+            Reader rp{pk.data(), pk.data() + pk.size()};
+            const CtData c = parse_ciphertext(rp, h.major);
+            got.insert(got.end(), c.data.begin(), c.data.end());
+        }
+        if (dim2) visit(i, got);
+    }
+    if (consumed) *consumed = (uint64_t)(outer.p - static_cast<const u8 *>(bytes));
+}
+
 }  // namespace
 
 extern "C" {
@@ -731,39 +782,36 @@ int hec_seal_parms_save(uint64_t N, const uint64_t *coeff_modulus, uint64_t coun
     });
 }
 
-// KSwitchKeys (RelinKeys / GaloisKeys): key list `index` (RelinKeys: 0; GaloisKeys: (galois_elt - 1) / 2) as
-// the engine's key layout u64[L][2][K][N] (the L PublicKeys' data back to back).  With index = UINT64_MAX
-// only *lists (dim1) is reported; *words = the list's word count (0 when that list is empty).
+// KSwitchKeys key list `index` (RelinKeys: 0; GaloisKeys: (galois_elt - 1) / 2) as the engine's key layout
+// u64[L][2][K][N].  With index = UINT64_MAX only *lists (dim1) is reported; *words = the list's word count (0 when
+// that list is empty).
 int hec_seal_kswitch_keys_load(const void *bytes, uint64_t nbytes, uint64_t index, uint64_t *lists, uint64_t *out,
                                uint64_t cap_words, uint64_t *words, uint64_t *consumed)
 {
     return io_guard([&] {
-        if (!bytes) throw std::invalid_argument("invalid argument");
-        Reader outer{static_cast<const u8 *>(bytes), static_cast<const u8 *>(bytes) + nbytes};
-        Header h;
-        std::memcpy(&h, bytes, std::min<uint64_t>(nbytes, sizeof(h)));
-        std::vector<u8> m = open_object(outer);
-        Reader r{m.data(), m.data() + m.size()};
-        u64 pid[4];
-        r.bytes(pid, 32);
-        const u64 dim1 = r.get<u64>();
-        if (lists) *lists = dim1;
         std::vector<u64> got;
-        for (u64 i = 0; i < dim1; ++i) {
-            const u64 dim2 = r.get<u64>();
-            for (u64 j = 0; j < dim2; ++j) {
-                std::vector<u8> pk = open_object(r);  // PublicKey
-                Reader rp{pk.data(), pk.data() + pk.size()};
-                const CtData c = parse_ciphertext(rp, h.major);
-                if (i == index) got.insert(got.end(), c.data.begin(), c.data.end());
-            }
-        }
+        walk_kswitch_keys(bytes, nbytes, lists, consumed, [&](u64 i, const std::vector<u64> &w) {
+            if (i == index) got = w;
+        });
         if (words) *words = got.size();
         if (out && index != UINT64_MAX) {
             if (cap_words < got.size()) throw std::invalid_argument("output buffer is too small");
             std::memcpy(out, got.data(), got.size() * 8);
         }
-        if (consumed) *consumed = (uint64_t)(outer.p - static_cast<const u8 *>(bytes));
+    });
+}
+
+int hec_seal_kswitch_keys_foreach(const void *bytes, uint64_t nbytes,
+                                  int (*visit)(void *user, uint64_t index, const uint64_t *words, uint64_t nwords),
+                                  void *user, uint64_t *lists, uint64_t *consumed)
+{
+    return io_guard([&] {
+        if (!visit) throw std::invalid_argument("invalid argument");
+        walk_kswitch_keys(bytes, nbytes, lists, consumed, [&](u64 i, const std::vector<u64> &w) {
+            const int rc = visit(user, i, w.data(), w.size());
+            if (rc == HEC_EINVAL) throw std::invalid_argument("key list rejected by the caller");
+            if (rc != HEC_OK) throw std::logic_error("key list rejected by the caller");
+        });
     });
 }
 

@@ -11,7 +11,9 @@
  *     u64[level][N] in NTT form, a key-switching key (one RelinKeys / GaloisKeys entry, i.e. SEAL's
  *     vector<PublicKey>) u64[L][2][K][N], where K = #coeff_modulus, L = K-1 data primes and
  *     "level" = number of data primes a ciphertext currently has (SEAL chain index + 1);
- *   - all residues canonical in [0, q); results are bit-identical to SEAL 4.1's Evaluator;
+ *   - all residues canonical in [0, q); every result is bit-identical to this repository's CPU
+ *     restatement of SEAL 4.1's Evaluator (oracle/).  Against SEAL itself parity is unpinned:
+ *     SEAL is absent here and the reference ships no test vectors;
  *   - errors: SEAL throws std::invalid_argument / std::logic_error; here every call returns a
  *     status (HEC_OK, HEC_EINVAL for invalid_argument, HEC_ELOGIC for logic_error, HEC_EDEVICE for a
  *     HIP failure) and hec_last_error() returns SEAL's message text ("scale mismatch",
@@ -182,15 +184,18 @@ int hec_plan_diagonal_shards(uint64_t poly_modulus_degree, uint64_t n, int world
 /* ncclGetUniqueId: 128 bytes that rank 0 creates and every rank passes to hec_comm_init (RCCL is loaded on
  * first use from librccl.so.1; HEC_ELOGIC when it is absent). */
 int hec_comm_unique_id(void *unique_id);
-/* ncclCommInitRank on the context's device; world == 1 needs no id.  The communicator lives until
- * hec_context_destroy. */
+/* ncclCommInitRank on the context's device; world == 1 needs no id; 1 <= world <= 8 (the partial-sum exchange
+ * adds world canonical 60-bit residues in u64).  The communicator lives until hec_context_destroy. */
 int hec_comm_init(hec_context *ctx, int rank, int world, const void *unique_id);
 /* 1 when the context has a communicator (then *rank, *world are set), 0 when not, HEC_EINVAL on NULL */
 int hec_context_comm(const hec_context *ctx, int *rank, int *world);
 /* BatchedMatrix::matmul diag x col over the world (every rank calls it with the same arguments): rank r
- * computes the partial sums over its planned diagonals (only those diags[j] are read, others may be any
- * handle), one RCCL all-reduce (u64 sum, exact for world <= 8 and 60-bit primes) + reduction mod q, then every
- * rank relinearizes and rescales all p outputs: out[i] is bit-identical to hec_matmul_diag_col on one GPU. */
+ * computes the partial sums over its planned diagonals (hec_plan_diagonal_shards with the keys of gk): only those
+ * diags[j] are read and checked, every other entry is never dereferenced and may be NULL or any handle.  The
+ * ranks then agree on the argument checks (a one-int RCCL all-reduce, so an error on one rank is returned on all
+ * ranks instead of leaving the others in the exchange), run one RCCL all-reduce of the partials (u64 sum, exact
+ * for world <= 8 and 60-bit primes) + reduction mod q, and every rank relinearizes and rescales all p outputs:
+ * out[i] is bit-identical to hec_matmul_diag_col on one GPU. */
 int hec_matmul_diag_col_sharded(hec_context *ctx, const hec_ciphertext *const *diags, uint64_t n,
                                 const hec_ciphertext *const *cols, uint64_t p, const hec_kswitch_key *rk,
                                 const hec_galois_keys *gk, hec_ciphertext *const *out);
@@ -201,7 +206,10 @@ int hec_matmul_diag_col_sharded(hec_context *ctx, const hec_ciphertext *const *d
  * magic 0xA15E, header size, version 4.1, compr_mode, size) + members, compr_mode HEC_COMPR_NONE / ZLIB / ZSTD
  * (zlib, zstd loaded on first use).  Host-only functions return HEC_EINVAL with SEAL's wording for malformed
  * input ("loaded SEALHeader is invalid", ...); hec_seal_last_error() holds the message.  Seeded ciphertexts
- * (encrypt_symmetric().save(), client.cpp:113-114) must be expanded by the caller's SEAL (HEC_EINVAL). */
+ * (encrypt_symmetric().save(), client.cpp:113-114) are expanded by hec_seal_ciphertext_load_ex and by the device
+ * loader hec_ciphertext_load_seal (Ciphertext::expand_seed); hec_seal_ciphertext_load, which has no moduli,
+ * rejects them (HEC_EINVAL).  Decompressed objects are bounded (2 GiB per ciphertext, 1 TiB per key object) and a
+ * payload must hold the words it announces, since the bytes come from a client socket (server.cpp:110-122). */
 #define HEC_COMPR_NONE 0
 #define HEC_COMPR_ZLIB 1
 #define HEC_COMPR_ZSTD 2
@@ -238,6 +246,12 @@ int hec_seal_parms_save(uint64_t poly_modulus_degree, const uint64_t *coeff_modu
  * in the engine's key layout u64[L][2][K][N]; *lists = the object's list count, *words = that list's words */
 int hec_seal_kswitch_keys_load(const void *bytes, uint64_t nbytes, uint64_t index, uint64_t *lists, uint64_t *out,
                                uint64_t cap_words, uint64_t *words, uint64_t *consumed);
+/* The same object in ONE pass: visit(user, index, words, nwords) is called for every non-empty key list in order
+ * (GaloisKeys hold N lists, almost all empty, so a per-index hec_seal_kswitch_keys_load would reparse the object N
+ * times).  A non-zero return from visit stops the walk with that status.  *lists = the object's list count. */
+int hec_seal_kswitch_keys_foreach(const void *bytes, uint64_t nbytes,
+                                  int (*visit)(void *user, uint64_t index, const uint64_t *words, uint64_t nwords),
+                                  void *user, uint64_t *lists, uint64_t *consumed);
 int hec_seal_kswitch_keys_save(uint64_t poly_modulus_degree, const uint64_t *coeff_modulus, uint64_t K,
                                const uint64_t *const *keys, const uint64_t *digits, uint64_t nlists, int compr_mode,
                                void *out, uint64_t cap, uint64_t *written);

@@ -948,6 +948,58 @@ std::vector<Ciphertext> matmul_diag_col_set(const Context &ctx, const std::vecto
     return out;
 }
 
+// The ct x pt form of the same loop: BatchedMatrix::matmul's diag x col with plaintext
+// diagonals, `*=` = multiply_plain_inplace (he_operators.cpp:128-142), products stay size 2 (no relinearization),
+// then rescale_to_next per output when finish.  P[k] is diagonal js[k]; threads over (output, diagonal chunk) with
+// the chunk partials summed mod q (modular addition is exact and order free).
+std::vector<Ciphertext> matmul_diagpt_col_set(const Context &ctx, const std::vector<const Plaintext *> &P,
+                                              const std::vector<std::size_t> &js,
+                                              const std::vector<const Ciphertext *> &X, const GaloisKeys &gk,
+                                              int nthreads, bool finish)
+{
+    const std::size_t nj = js.size(), p = X.size();
+    if (nj == 0 || P.size() != nj) throw std::invalid_argument("empty diagonal range");
+    nthreads = std::max(1, nthreads);
+    const std::size_t chunks = std::min<std::size_t>((std::size_t)nthreads, nj);
+    std::vector<std::vector<Ciphertext>> part(p, std::vector<Ciphertext>(chunks));
+    std::atomic<std::size_t> next{0};
+    std::vector<std::string> errs(nthreads);
+    auto worker = [&](int tid) {
+        try {
+            for (;;) {
+                const std::size_t w = next.fetch_add(1);
+                if (w >= p * chunks) break;
+                const std::size_t i = w / chunks, c = w % chunks;
+                const std::size_t kb = nj * c / chunks, ke = nj * (c + 1) / chunks;
+                Ciphertext acc;
+                for (std::size_t k = kb; k < ke; ++k) {
+                    Ciphertext t = *X[i];
+                    rotate_vector_inplace(ctx, t, (int)js[k], gk);
+                    multiply_plain_inplace(ctx, t, *P[k]);
+                    if (k == kb) acc = std::move(t);
+                    else add_inplace(ctx, acc, t);
+                }
+                part[i][c] = std::move(acc);
+            }
+        } catch (const std::exception &e) { errs[tid] = e.what(); }
+    };
+    if (nthreads == 1) worker(0);
+    else {
+        std::vector<std::thread> th;
+        for (int t = 0; t < nthreads; ++t) th.emplace_back(worker, t);
+        for (auto &t : th) t.join();
+    }
+    for (auto &e : errs)
+        if (!e.empty()) throw std::invalid_argument(e);
+    std::vector<Ciphertext> out(p);
+    for (std::size_t i = 0; i < p; ++i) {
+        out[i] = std::move(part[i][0]);
+        for (std::size_t c = 1; c < chunks; ++c) add_inplace(ctx, out[i], part[i][c]);
+        if (finish) rescale_to_next_inplace(ctx, out[i]);
+    }
+    return out;
+}
+
 std::vector<Ciphertext> matmul_diag_col(const Context &ctx, const std::vector<const Ciphertext *> &A,
                                         const std::vector<const Ciphertext *> &X, const KSwitchKey &rk,
                                         const GaloisKeys &gk, int nthreads, std::size_t j_begin,

@@ -228,6 +228,11 @@ std::vector<Ciphertext> matmul_diag_col_set(const Context &ctx, const std::vecto
                                             const std::vector<std::size_t> &js,
                                             const std::vector<const Ciphertext *> &X, const KSwitchKey &rk,
                                             const GaloisKeys &gk, int nthreads, bool finish);
+// ct x pt form over the diagonal subset js (plaintext diagonals, multiply_plain, rescale when finish)
+std::vector<Ciphertext> matmul_diagpt_col_set(const Context &ctx, const std::vector<const Plaintext *> &P,
+                                              const std::vector<std::size_t> &js,
+                                              const std::vector<const Ciphertext *> &X, const GaloisKeys &gk,
+                                              int nthreads, bool finish);
 std::vector<Ciphertext> matmul_diag_col(const Context &ctx, const std::vector<const Ciphertext *> &A,
                                         const std::vector<const Ciphertext *> &X, const KSwitchKey &rk,
                                         const GaloisKeys &gk, int nthreads = 1, std::size_t j_begin = 0,

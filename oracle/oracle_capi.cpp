@@ -330,6 +330,24 @@ int orc_matmul_diag_col_set(void *c, const OrcCt *A, const u64 *js, u64 nj, cons
         for (u64 i = 0; i < p; ++i) out_ct(r[i], out + i);
     });
 }
+// pts: nj plaintexts u64[level][N] back to back, all at `level` with `pscale`
+int orc_matmul_diagpt_col_set(void *c, const u64 *pts, u64 level, double pscale, const u64 *js, u64 nj, const OrcCt *X,
+                              u64 p, const u32 *elts, const u64 *const *keys, u64 nkeys, OrcCt *out, int nthreads,
+                              int finish)
+{
+    return guard([&] {
+        auto &ctx = *static_cast<Context *>(c);
+        std::vector<Plaintext> P;
+        P.reserve(nj);
+        for (u64 k = 0; k < nj; ++k) P.push_back(pt_in(ctx, pts + k * level * ctx.N(), level, pscale));
+        std::vector<const Plaintext *> pp;
+        for (auto &x : P) pp.push_back(&x);
+        auto x = in_many(ctx, X, p);
+        auto r = matmul_diagpt_col_set(ctx, pp, std::vector<std::size_t>(js, js + nj), ptrs(x),
+                                       gkeys(elts, keys, nkeys), nthreads, finish != 0);
+        for (u64 i = 0; i < p; ++i) out_ct(r[i], out + i);
+    });
+}
 // CPU baseline (bench.py cpu_baseline leg): one full diag x col matvec (he_linalg.cpp:943-1006, relinearize +
 // rescale) of n diagonals over X, timed with steady_clock around the call as the reference's Timer does
 // (tic_toc.h:20-28).  The n diagonals cycle over the nA distinct ones given (every step is data-oblivious, so

@@ -355,6 +355,19 @@ class Oracle:
                                              *self._gk(gk), outs, C.c_int(nthreads), C.c_int(int(finish))))
         return self._outs(outs, len(X))
 
+    def matmul_diagpt_col_set(self, P, pscale, js, X, gk, nthreads=1, finish=True):
+        """ct x pt form over the diagonals js: P[k] (u64[level][N] NTT-form plaintext at scale pscale) is diagonal
+        js[k]; out[i] = rescale(sum_k multiply_plain(rot(X[i], js[k]), P[k])) (rescale only when finish)."""
+        pts = np.ascontiguousarray(np.stack([np.asarray(q, dtype=np.uint64) for q in P]))
+        x, xb = self._many(X)
+        jj = np.ascontiguousarray(np.array(js, dtype=np.uint64))
+        lvl = X[0].level
+        outs, ob = self._many([Ct(np.zeros((2, lvl, self.N), np.uint64), 1.0) for _ in X])
+        _check(lib().orc_matmul_diagpt_col_set(self.h, _p(pts), C.c_uint64(pts.shape[1]), C.c_double(pscale), _p(jj),
+                                               C.c_uint64(len(js)), x, C.c_uint64(len(X)), *self._gk(gk), outs,
+                                               C.c_int(nthreads), C.c_int(int(finish))))
+        return self._outs(outs, len(X))
+
     def bench_matvec(self, A, n, X, rk, gk, nthreads=1, j_begin=0, j_end=None, finish=True):
         """Seconds for one diag x col matvec of n diagonals (cycling over the distinct A) over X (C++ timer)."""
         a, ab = self._many(A)

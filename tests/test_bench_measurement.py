@@ -34,6 +34,36 @@ def test_key_switch_counts(bench):
     assert rotation_trie_stats(1 << 16, 1024)[0] == 1364  # cfg5
 
 
+def test_launcher_command(bench):
+    cmd = bench.launcher_cmd(8, ["--gpus", "8", "--steps", "3"], 29512)
+    assert cmd[1:8] == ["-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=8", "--master-addr=127.0.0.1",
+                        "--master-port=29512", os.path.join(ROOT, "bench.py")]
+    assert cmd[8:] == ["--gpus", "8", "--steps", "3"]
+
+
+def test_gpus_2_launches_two_ranks_one_line():
+    """`bench.py --gpus 2` with no WORLD_SIZE starts 2 ranks itself (gloo dry run: no GPU) and exactly one JSON line
+    comes out, from rank 0, with the world size the process group saw."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR",
+                                                             "MASTER_PORT")}
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run", "--steps", "2",
+                          "--warmup", "1"], capture_output=True, text=True, env=env, timeout=300, check=True)
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    r = json.loads(lines[0])
+    assert r["n_gpus"] == 2 and r["rccl_world"] == 2 and r["dry_run"] and r["steps"] == 2
+
+
+def test_cpu_leg_sizing(bench, monkeypatch):
+    monkeypatch.setattr(bench, "cgroup_cpu_quota", lambda: None)
+    monkeypatch.setenv("OMP_NUM_THREADS", "1")
+    model, host, share, threads, why = bench.cpu_info()
+    assert threads == 1 or share == 1
+    monkeypatch.setattr(bench, "cgroup_cpu_quota", lambda: 1)
+    monkeypatch.delenv("OMP_NUM_THREADS")
+    assert bench.cpu_info()[3] == 1
+
+
 def test_profile_step_tool(tmp_path):
     # 3 timed steps x 2 dispatches (lanes) then a 2-dispatch profile step of 10 us each
     trace = tmp_path / "trace.csv"

@@ -9,7 +9,13 @@
   outputs equal to the same vectors run alone (size-independent properties: the oracle would need
   18,204 key switches per vector);
 - cfg5 (N = 2^16, {60, 40 x 15, 60}): the same subset construction on the n = 1024 matmul with 32 columns
-  (2 lanes of 16) and only the keys the subset touches, bit-exact, then relinearize + rescale.
+  (2 lanes of 16) and only the keys the subset touches, bit-exact, then relinearize + rescale;
+- cfg3 in BASELINE's literal ct x pt form (configs[2], "ct x pt matvec 4096 x 4096"): the full n = 4096 matvec with
+  GPU-encoded plaintext diagonals over 48 vectors (3 lanes), bit-exact against the oracle on the 64-diagonal trie
+  subset (the other diagonals are zero plaintexts, whose products are exactly zero), and on a random M decrypted
+  against M @ x with lane independence;
+- cfg5 at full size: the whole 1024 x 1024 x 1024 product over 32 columns with the 31 default keys, decrypted
+  against M @ X, and lane independence.
 """
 import os
 
@@ -121,3 +127,107 @@ def test_cfg5_subset_bitexact(orc, hecdna):
     fin = e.ctx.matmul_finish([got[0], got[p - 1]], e.rk)
     e.same(fin[0], e.o.rescale(e.o.relinearize(exp[0], e.rk_h)))
     e.same(fin[1], e.o.rescale(e.o.relinearize(exp[p - 1], e.rk_h)))
+
+
+def _ctpt_full(e, vals_of, n, X):
+    """hec_matmul_diagpt_col over n GPU-encoded plaintext diagonals (row j of vals_of(j0, j1)), in chunks."""
+    L = len(e.m) - 1
+    P = []
+    for j0 in range(0, n, 512):
+        P += e.ctx.encode(vals_of(j0, min(n, j0 + 512)), 2.0**40, L)
+    return P, e.ctx.matmul_diagpt_col(P, X, e.gk)
+
+
+@pytest.mark.timeout(900)
+def test_cfg3_ctpt_full_matvec_subset_bitexact(env15):
+    """The n = 4096 ct x pt matvec at cfg3 (hec_matmul_diagpt_col, he_operators.cpp:128-142 multiply_plain) with 48
+    vectors = 3 lanes: diagonals outside the 64-diagonal trie subset are zero, so the outputs equal the oracle's
+    subset sum (rotate, multiply_plain, add, rescale) bit for bit while the GPU runs the whole trie."""
+    e = env15
+    n, p, L = 4096, 48, len(e.m) - 1
+    js = trie_subset(e.N, n, target=64)
+    where = {j: k for k, j in enumerate(js)}
+    sub = e.rng.uniform(-1, 1, (len(js), e.N // 2))
+
+    def vals_of(j0, j1):
+        v = np.zeros((j1 - j0, e.N // 2))
+        for j in range(j0, j1):
+            if j in where:
+                v[j - j0] = sub[where[j]]
+        return v
+    X = _enc_many(e, p, 6100, L)
+    P, got = _ctpt_full(e, vals_of, n, [e.up(x) for x in X])
+    exp = e.o.matmul_diagpt_col_set([P[j].download() for j in js], 2.0**40, js, X, e.gk_h, nthreads=THREADS)
+    assert len(got) == p
+    for g, c in zip(got, exp):
+        e.same(g, c)
+
+
+@pytest.mark.timeout(900)
+def test_cfg3_ctpt_full_n_decrypt_and_lane_independence(env15):
+    """cfg3 ct x pt over a random 4096 x 4096 M (GPU-encoded diagonals) and 48 encrypted x: decrypt(out_i) = M x_i
+    within CKKS error, and each lane's outputs equal the same vectors run alone."""
+    e = env15
+    n, p, L = 4096, 48, len(e.m) - 1
+    slots = e.N // 2
+    rng = np.random.default_rng(40960)
+    M = rng.uniform(-1, 1, (n, n))
+    xs = rng.uniform(-1, 1, (p, n))
+    r = np.arange(slots) % n
+
+    def vals_of(j0, j1):
+        return np.stack([M[r, (r + j) % n] for j in range(j0, j1)])
+    rawx = e.o.encrypt_many(e.sk, xs[:, r], 2.0**40, L, 91000, nthreads=THREADS)
+    gX = [e.ctx.ciphertext(rawx[i], 2.0**40) for i in range(p)]
+    P, out = _ctpt_full(e, vals_of, n, gX)
+    ref = xs @ M.T
+    worst = 0.0
+    for i, g in enumerate(out):
+        ct = e.orc.Ct(g.download(), g.scale)
+        assert ct.level == L - 1 and ct.size == 2
+        d = e.o.decode(e.o.decrypt(e.sk, ct), ct.scale).real
+        worst = max(worst, float(np.max(np.abs(d - ref[i][r]))))
+    assert worst < 1e-3, worst
+    alone_idx = [0, 16, 32, 47]
+    alone = e.ctx.matmul_diagpt_col(P, [gX[i] for i in alone_idx], e.gk)
+    for a, i in zip(alone, alone_idx):
+        assert np.array_equal(a.download(), out[i].download()) and a.scale == out[i].scale
+
+
+@pytest.mark.timeout(900)
+def test_cfg5_full_product_decrypt_and_lane_independence(orc, hecdna):
+    """BASELINE cfg5 at full size on one GPU: the 1024 x 1024 x 1024 ct x ct matmul as BatchedMatrix::matmul diag x
+    col (matrix_operations.cpp:844-850 parameters: N = 2^16, {60, 40 x 15, 60}, the 31 default keys) over 32 output
+    columns (2 lanes of 16): decrypt(out_c) = (M B)[:, c] within CKKS error; lane outputs equal columns run alone."""
+    from test_gpu_parity import Env
+    N, n, p = 1 << 16, 1024, 32
+    bits = [60] + [40] * 15 + [60]
+    e = Env(orc, hecdna, N, bits, seed=5151)
+    assert len(e.elts) == 31
+    L = len(e.m) - 1
+    slots = N // 2
+    rng = np.random.default_rng(1024)
+    M = rng.uniform(-1, 1, (n, n))
+    Bm = rng.uniform(-1, 1, (n, p))
+    r = np.arange(slots) % n
+    gA = []
+    for j0 in range(0, n, 256):
+        raw = e.o.encrypt_many(e.sk, np.stack([M[r, (r + j) % n] for j in range(j0, j0 + 256)]), 2.0**40, L,
+                               50000 + j0, nthreads=THREADS)
+        gA += [e.ctx.ciphertext(raw[k], 2.0**40) for k in range(256)]
+        del raw
+    rawx = e.o.encrypt_many(e.sk, Bm.T[:, r], 2.0**40, L, 60000, nthreads=THREADS)
+    gX = [e.ctx.ciphertext(rawx[c], 2.0**40) for c in range(p)]
+    out = e.ctx.matmul_diag_col(gA, gX, e.rk, e.gk)
+    ref = (M @ Bm).T
+    worst = 0.0
+    for c, g in enumerate(out):
+        ct = e.orc.Ct(g.download(), g.scale)
+        assert ct.level == L - 1 and ct.size == 2
+        d = e.o.decode(e.o.decrypt(e.sk, ct), ct.scale).real
+        worst = max(worst, float(np.max(np.abs(d - ref[c][r]))))
+    assert worst < 1e-3, worst
+    alone_idx = [0, 15, 16, 31]
+    alone = e.ctx.matmul_diag_col(gA, [gX[c] for c in alone_idx], e.rk, e.gk)
+    for a, c in zip(alone, alone_idx):
+        assert np.array_equal(a.download(), out[c].download()) and a.scale == out[c].scale

@@ -262,6 +262,21 @@ def test_matvec_batch_lanes_bitexact(env11):
         e.same(g, c)
 
 
+def test_lane_workspace_growth_while_lanes_run(orc, hecdna):
+    """A fresh context: a 3-lane matvec at a small shape, then at a larger one, so each lane grows its workspace
+    from its own host thread while the other lanes are launching (the round-2 lane hazard); then the small shape
+    again (the outgrown bases were reclaimed after the lanes joined).  Every output equals the oracle's."""
+    e = Env(orc, hecdna, 1 << 11, [50, 36, 36, 50], seed=5151)
+    X = [e.enc(seed=5000 + i) for i in range(48)]
+    gX = [e.up(x) for x in X]
+    for n in (3, 24, 3):
+        A = [e.enc(seed=5100 + j) for j in range(n)]
+        exp = e.o.matmul_diag_col(A, X, e.rk_h, e.gk_h, nthreads=8)
+        got = e.ctx.matmul_diag_col([e.up(a) for a in A], gX, e.rk, e.gk)
+        for g, c in zip(got, exp):
+            e.same(g, c)
+
+
 def test_matvec_partial_finish_equals_full(env11):
     e = env11
     n = 10

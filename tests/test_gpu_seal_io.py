@@ -57,6 +57,25 @@ def test_keys_load_on_device(env, hecdna):
     e.same(e.ctx.rotate_vector(e.up(b), 7, gk), e.o.rotate(b, 7, e.gk_h))
 
 
+def test_galois_keys_load_realistic_list_count(env, hecdna):
+    """SEAL's GaloisKeys hold N key lists (create_galois_keys resizes the list array to the ring degree), almost all
+    empty: the device loader parses the object once, so the load takes one pass, not N."""
+    import time
+    e = env
+    elts = sorted(e.gk_h)
+    lists = [None] * e.N
+    for elt in elts:
+        lists[(elt - 1) // 2] = e.gk_h[elt]
+    blob = sf.kswitch_keys(e.N, e.m, lists)
+    gk = hecdna.GaloisKeys(e.ctx)
+    t0 = time.perf_counter()
+    assert gk.load_seal(blob + b"tail") == len(blob)
+    assert time.perf_counter() - t0 < 30
+    assert all(gk.has(elt) for elt in elts) and not gk.has(5 if 5 not in elts else 7)
+    b = e.rand_ct(2, 3)
+    e.same(e.ctx.rotate_vector(e.up(b), 5, gk), e.o.rotate(b, 5, e.gk_h))
+
+
 def test_server_flow_on_seal_bytes(env, hecdna, tmp_path):
     """he_demo server = server.cpp:99-152 with hecdna:: types: EncryptionParameters / RelinKeys / 2 Ciphertexts loaded
     from the client's buffer, res = relin(op1 * op2) rescaled, saved with Ciphertext::save (zstd)."""

@@ -170,3 +170,40 @@ def test_prng_rejection_redraws_from_stream_continuation(hecdna):
     d = np.zeros((2, 1, n), dtype=np.uint64)
     got, _, _, _ = hecdna.seal_ciphertext_load(sf.ciphertext(d, 1.0, [q], seeded_c0_only=True), moduli=[q])
     assert np.array_equal(got[1], c1)
+
+
+def test_kswitch_keys_one_pass_walk(hecdna):
+    """hec_seal_kswitch_keys_foreach: the GaloisKeys shape SEAL writes (N lists, a few non-empty) in one pass, raw
+    and zstd-compressed, equal to the per-index reader and to the restated layout."""
+    import time
+    rng = np.random.default_rng(9)
+    lists = [None] * N
+    idx = [0, 1, 5, 170, 1023, N - 1]
+    for i in idx:
+        lists[i] = np.stack([rng.integers(0, MOD[k], (3, 2, N), dtype=np.uint64) for k in range(4)], axis=2)
+    for compr in (hecdna.COMPR_NONE, hecdna.COMPR_ZSTD):
+        b = hecdna.seal_kswitch_keys_save(N, MOD, lists, compr=compr)
+        if compr == hecdna.COMPR_NONE:
+            assert b == sf.kswitch_keys(N, MOD, lists)
+        t0 = time.perf_counter()
+        got, nl, used = hecdna.seal_kswitch_keys_lists(b + b"xyz")
+        assert time.perf_counter() - t0 < 10
+        assert nl == N and used == len(b) and sorted(got) == idx
+        for i in idx:
+            assert np.array_equal(got[i], lists[i].reshape(-1))
+        w, _, _ = hecdna.seal_kswitch_keys_load(b, 170)
+        assert np.array_equal(w, got[170])
+
+
+def test_truncated_dynarray_is_rejected_before_allocation(hecdna):
+    """a ciphertext whose DynArray announces more words than its payload holds (server input is untrusted)"""
+    d = rand_ct(2, 1, seed=3)
+    b = bytearray(sf.ciphertext(d, 2.0**40, MOD))
+    inner = 16 + 32 + 1 + 8 * 4 + 8              # outer header, parms_id, ntt flag, size/N/level/scale, correction
+    total = int.from_bytes(b[inner + 8:inner + 16], "little")
+    cut = 8 * 100                                  # drop 100 words from the inner object, fix both size fields
+    b = b[:len(b) - cut]
+    b[inner + 8:inner + 16] = (total - cut).to_bytes(8, "little")
+    b[8:16] = len(b).to_bytes(8, "little")
+    with pytest.raises(hecdna.InvalidArgument, match="truncated"):
+        hecdna.seal_ciphertext_load(bytes(b))
