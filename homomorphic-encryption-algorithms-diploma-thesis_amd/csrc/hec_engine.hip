@@ -1421,7 +1421,7 @@ int hec_context_destroy(hec_context *ctx)
         (void)hipFree(c.itwb);
         for (double *p : {c.twf, c.itwf, c.twbf, c.itwbf}) (void)hipFree(p);
         (void)hipFree(c.enc_map);
-        for (double *p : {c.enc_tw, c.enc_twist}) (void)hipFree(p);
+        (void)hipFree(c.enc_tw);
         if (c.own_stream) (void)hipStreamDestroy(c.stream);
         (void)hipStreamDestroy(c.side);
         (void)hipEventDestroy(c.ev_fork);
@@ -1668,13 +1668,35 @@ int hec_plaintext_info(const hec_plaintext *pt, uint64_t *level, double *scale)
 
 // ------------------------------------------------------------------ CKKS encoder ----------
 namespace {
-// host tables of the GPU encoder (hec_encode.hip), built once per context: the slot map of SEAL's
-// matrix_reps_index_map_ (generator 3) with the FFT's bit reversal folded in, the FFT stage twiddles
-// polar(1, (-2 pi / len) j) and the twist polar(1, -pi k / N), as std::polar over glibc cos/sin
+// host tables of the GPU encoder (hec_encode.hip), built once per context, as SEAL 4.1's CKKSEncoder constructor
+// builds them: matrix_reps_index_map_ (generator 3, bit-reversed positions) and inv_root_powers_[i] =
+// conj(ComplexRoots(2N).get_root(bitrev(i - 1, logN) + 1)), where ComplexRoots holds (cos t, sin t),
+// t = (i 6.283185307179586) / 2N for i <= 2N / 8 (glibc cos and sin as separate calls) and get_root extends them by
+// the 8-fold symmetry
+struct SealRoots {  // a class member: no C language linkage inside the C-ABI block
+static std::complex<double> get(u64 m, const std::vector<std::complex<double>> &roots, u64 index)
+{
+    index &= m - 1;
+    if (index <= m / 8) return roots[index];
+    if (index <= m / 4) {
+        const auto a = roots[m / 4 - index];
+        return {a.imag(), a.real()};
+    }
+    if (index <= m / 2) {
+        const auto a = get(m, roots, m / 2 - index);
+        return {-a.real(), a.imag()};
+    }
+    if (index <= 3 * m / 4) {
+        const auto a = get(m, roots, index - m / 2);
+        return {-a.real(), -a.imag()};
+    }
+    const auto a = get(m, roots, m - index);
+    return {a.real(), -a.imag()};
+}
+};
 void encoder_tables(Ctx &c)
 {
     if (c.enc_map) return;
-    constexpr double kPi = 3.14159265358979323846;
     const u64 N = c.N, slots = N / 2, m = 2 * N;
     std::vector<u32> map(N);
     u64 pos = 1;
@@ -1683,33 +1705,28 @@ void encoder_tables(Ctx &c)
         map[slots + i] = brev((u32)((m - pos - 1) >> 1), c.logN);
         pos = (pos * 3) & (m - 1);
     }
-    std::vector<double> tw(2 * (N - 1)), twist(2 * N);
-    const int sign = -1;
-    for (u64 len = 2; len <= N; len <<= 1) {
-        const double ang = sign * 2 * kPi / (double)len;
-        for (u64 j = 0; j < len / 2; ++j) {
-            const std::complex<double> w = std::polar(1.0, ang * (double)j);
-            tw[2 * (len / 2 - 1 + j)] = w.real();
-            tw[2 * (len / 2 - 1 + j) + 1] = w.imag();
-        }
+    double (*volatile vcos)(double) = std::cos;  // never fused into sincos
+    double (*volatile vsin)(double) = std::sin;
+    std::vector<std::complex<double>> roots(m / 8 + 1);
+    for (u64 i = 0; i <= m / 8; ++i) {
+        const double t = ((double)i * 6.283185307179586) / (double)m;
+        roots[i] = {vcos(t), vsin(t)};
     }
-    for (u64 k = 0; k < N; ++k) {
-        const std::complex<double> z = std::polar(1.0, -kPi * (double)k / (double)N);
-        twist[2 * k] = z.real();
-        twist[2 * k + 1] = z.imag();
+    std::vector<double> inv(2 * N, 0.0);
+    for (u64 i = 1; i < N; ++i) {
+        const auto r = SealRoots::get(m, roots, (u64)brev((u32)(i - 1), c.logN) + 1);
+        inv[2 * i] = r.real();
+        inv[2 * i + 1] = -r.imag();
     }
     u32 *dm = nullptr;
-    double *dt = nullptr, *dz = nullptr;
+    double *dt = nullptr;
     HEC_HIP(hipMalloc(&dm, N * sizeof(u32)));
-    HEC_HIP(hipMalloc(&dt, tw.size() * sizeof(double)));
-    HEC_HIP(hipMalloc(&dz, twist.size() * sizeof(double)));
+    HEC_HIP(hipMalloc(&dt, inv.size() * sizeof(double)));
     HEC_HIP(hipMemcpyAsync(dm, map.data(), N * sizeof(u32), hipMemcpyHostToDevice, c.stream));
-    HEC_HIP(hipMemcpyAsync(dt, tw.data(), tw.size() * sizeof(double), hipMemcpyHostToDevice, c.stream));
-    HEC_HIP(hipMemcpyAsync(dz, twist.data(), twist.size() * sizeof(double), hipMemcpyHostToDevice, c.stream));
+    HEC_HIP(hipMemcpyAsync(dt, inv.data(), inv.size() * sizeof(double), hipMemcpyHostToDevice, c.stream));
     HEC_HIP(hipStreamSynchronize(c.stream));  // the host tables go out of scope
     c.enc_map = dm;
     c.enc_tw = dt;
-    c.enc_twist = dz;
 }
 }  // namespace
 
@@ -1751,10 +1768,11 @@ int hec_encode(hec_context *ctx, const double *re, const double *im, uint64_t n_
             for (u64 v = 0; v < cnt; ++v) {
                 double maxabs;
                 std::memcpy(&maxabs, &mx[v], sizeof(double));
-                // ceil(log2(max(max |coeff|, 1))) + 1 >= total coeff-modulus bits -> throw (SEAL encode_internal)
+                // ceil(log2(max(max |Re|, 1))) + 1 >= total coeff-modulus bits -> throw (SEAL encode_internal; the
+                // maximum is over the unrounded real parts); a non-finite value is rejected the same way
+                if (!std::isfinite(maxabs)) throw std::invalid_argument("encoded values are too large");
                 const int max_bits = (int)std::ceil(std::log2(std::max(maxabs, 1.0))) + 1;
-                if (max_bits >= c.total_bits(level) || maxabs >= 0x1.0p62)
-                    throw std::invalid_argument("encoded values are too large");
+                if (max_bits >= c.total_bits(level)) throw std::invalid_argument("encoded values are too large");
             }
             for (u64 v = 0; v < cnt; ++v) {
                 hec_plaintext *pt = out[v0 + v];

@@ -76,10 +76,10 @@ struct Ctx {
     u64 *cji = nullptr;
     int *zflag = nullptr;
     int logR = 0;                   // pass split N = R x C, R = 2^ceil(logN/2)
-    // CKKS encoder tables (hec_encode.hip), built on first encode: slot -> bit-reversed FFT position
-    // (u32[N]), FFT stage twiddles (complex[N - 1], stage len at len/2 - 1) and the twist polar(1, -pi k/N)
+    // CKKS encoder tables (hec_encode.hip), built on first encode: SEAL's matrix_reps_index_map_ (u32[N]) and
+    // inv_root_powers_ (complex[N], entry 0 unused)
     u32 *enc_map = nullptr;
-    double *enc_tw = nullptr, *enc_twist = nullptr;
+    double *enc_tw = nullptr;
     Workspace ws;
     // host-side constants
     std::vector<u64> p_inv, p_inv_q, p_half_mod;            // key switch mod-down (per data prime)

@@ -416,43 +416,162 @@ static void fft(std::vector<cd> &a, int sign)  // a_t <- sum_k a_k exp(sign * 2 
     }
 }
 
+// ---- SEAL 4.1 CKKSEncoder::encode_internal, restated operation for operation.  Each step below was checked
+// against the reference's own build/demo (SEAL statically linked), read as data, never run:
+//   * CKKSEncoder::CKKSEncoder (0x6b570): matrix_reps_index_map_[i] = bitrev((3^i mod 2N - 1) / 2, logN),
+//     [N/2 + i] = bitrev((2N - 3^i mod 2N - 1) / 2, logN); inv_root_powers_[i] = conj(get_root(bitrev(i - 1, logN)
+//     + 1)), i = 1 .. N - 1 (the pxor on the imaginary part at 0x6bf63);
+//   * ComplexRoots::ComplexRoots(2N) (0xad280): roots_[i] = (cos t, sin t), t = (i * 6.283185307179586) / 2N, for
+//     i <= 2N / 8, with glibc cos and sin called separately (0xad438, 0xad448);
+//   * ComplexRoots::get_root (0xad500): the 8-fold symmetry below;
+//   * encode_internal<double> (0x513b0) is instantiated in the reference's own translation units, built without -O
+//     and without FMA (no vfmadd anywhere in build/demo): scatter, DWTHandler::transform_from_rev (0x13a6a) with
+//     fix = scale / N, then round / signbit / barrett_reduce_64 or _128 / negate_uint_mod per prime, then the NTT;
+//   * complex * complex there is a call to libgcc's __muldc3 (0x1134f): (ac - bd, ad + bc), each product rounded;
+//     complex * double multiplies both parts (0xf2c1).
+static cd seal_complex_root(std::size_t m, const std::vector<cd> &roots, std::size_t index)
+{
+    index &= m - 1;
+    if (index <= m / 8) return roots[index];
+    if (index <= m / 4) {  // mirror: swap the parts
+        const cd a = roots[m / 4 - index];
+        return cd(a.imag(), a.real());
+    }
+    if (index <= m / 2) {  // -conj(x) = (-re, im)
+        const cd a = seal_complex_root(m, roots, m / 2 - index);
+        return cd(-a.real(), a.imag());
+    }
+    if (index <= 3 * m / 4) {
+        const cd a = seal_complex_root(m, roots, index - m / 2);
+        return cd(-a.real(), -a.imag());
+    }
+    const cd a = seal_complex_root(m, roots, m - index);
+    return cd(a.real(), -a.imag());
+}
+
+void ckks_encoder_tables(std::size_t N, std::vector<u32> &map, std::vector<cd> &inv_roots)
+{
+    const int logn = __builtin_ctzll(N);
+    const u64 m = 2 * N, slots = N / 2;
+    map.assign(N, 0);
+    u64 pos = 1;
+    for (u64 i = 0; i < slots; ++i) {
+        map[i] = reverse_bits((u32)((pos - 1) >> 1), logn);
+        map[slots | i] = reverse_bits((u32)((m - pos - 1) >> 1), logn);
+        pos = (pos * 3) & (m - 1);
+    }
+    // cos and sin as two separate glibc calls (never fused into sincos), as the reference binary calls them
+    double (*volatile vcos)(double) = std::cos;
+    double (*volatile vsin)(double) = std::sin;
+    std::vector<cd> roots(m / 8 + 1);
+    for (u64 i = 0; i <= m / 8; ++i) {
+        const double t = ((double)i * 6.283185307179586) / (double)m;
+        roots[i] = cd(vcos(t), vsin(t));
+    }
+    inv_roots.assign(N, cd(0, 0));
+    for (u64 i = 1; i < N; ++i) {
+        const cd r = seal_complex_root(m, roots, (std::size_t)reverse_bits((u32)(i - 1), logn) + 1);
+        inv_roots[i] = cd(r.real(), -r.imag());
+    }
+}
+
+// libgcc __muldc3 for finite operands: (a + bi)(c + di) = (ac - bd) + (ad + bc) i, every product rounded
+static inline cd cmul(const cd &x, const cd &w)
+{
+    const double ac = x.real() * w.real(), bd = x.imag() * w.imag();
+    const double ad = x.real() * w.imag(), bc = x.imag() * w.real();
+    return cd(ac - bd, ad + bc);
+}
+
+// DWTHandler<complex<double>, complex<double>, double>::transform_from_rev(values, log_n, roots, scalar)
+static void seal_transform_from_rev(cd *values, int log_n, const cd *roots, const double *scalar)
+{
+    const std::size_t n = std::size_t(1) << log_n;
+    std::size_t gap = 1, m = n >> 1;
+    const cd *r = roots;
+    for (; m > 1; m >>= 1) {
+        std::size_t offset = 0;
+        for (std::size_t i = 0; i < m; i++) {
+            const cd w = *++r;
+            cd *x = values + offset, *y = x + gap;
+            for (std::size_t j = 0; j < gap; j++) {
+                const cd u = *x, v = *y;
+                *x++ = cd(u.real() + v.real(), u.imag() + v.imag());
+                *y++ = cmul(cd(u.real() - v.real(), u.imag() - v.imag()), w);
+            }
+            offset += gap << 1;
+        }
+        gap <<= 1;
+    }
+    const cd w = *++r;
+    cd *x = values, *y = x + gap;
+    if (scalar) {
+        const double s = *scalar;
+        const cd sw(w.real() * s, w.imag() * s);  // mul_root_scalar
+        for (std::size_t j = 0; j < gap; j++) {
+            const cd u = *x, v = *y;
+            *x++ = cd((u.real() + v.real()) * s, (u.imag() + v.imag()) * s);  // mul_scalar(add(u, v), s)
+            *y++ = cmul(cd(u.real() - v.real(), u.imag() - v.imag()), sw);
+        }
+    } else {
+        for (std::size_t j = 0; j < gap; j++) {
+            const cd u = *x, v = *y;
+            *x++ = cd(u.real() + v.real(), u.imag() + v.imag());
+            *y++ = cmul(cd(u.real() - v.real(), u.imag() - v.imag()), w);
+        }
+    }
+}
+
+// |round(v)| mod q for any finite integer-valued double a >= 0, exactly: SEAL's three decompositions (64-bit,
+// 128-bit fmod / divide split, the multi-word loop) all give the exact integer, so its residue is all that matters
+u64 encode_residue(double a, u64 q)
+{
+    if (a < 0x1.0p64) return (u64)a % q;
+    int e = 0;
+    const double f = std::frexp(a, &e);           // a = f 2^e, 0.5 <= f < 1
+    const u64 mant = (u64)std::ldexp(f, 53);      // a = mant 2^(e - 53), e - 53 > 0 here
+    u64 r = mant % q, pw = 2 % q;
+    for (int k = e - 53; k > 0; k >>= 1) {        // r *= 2^(e - 53) mod q
+        if (k & 1) r = (u64)((u128)r * pw % q);
+        pw = (u64)((u128)pw * pw % q);
+    }
+    return r;
+}
+
 Plaintext encode(const Context &ctx, const std::vector<cd> &values, double scale, std::size_t level)
 {
     const std::size_t N = ctx.N(), slots = N / 2;
-    const u64 m = 2 * N;
     if (values.size() > slots) throw std::invalid_argument("values has invalid size");
     if (level < 1 || level > ctx.L()) throw std::invalid_argument("parms_id is not valid for encryption parameters");
     if (scale <= 0 || (int)std::log2(scale) >= ctx.total_bits(level)) throw std::invalid_argument("scale out of bounds");
+    std::vector<u32> map;
+    std::vector<cd> inv_roots;
+    ckks_encoder_tables(N, map, inv_roots);
     std::vector<cd> v(N, cd(0, 0));
-    u64 pos = 1;
-    for (std::size_t i = 0; i < slots; ++i) {  // SEAL CKKSEncoder::matrix_reps_index_map_ (natural order)
-        const cd z = i < values.size() ? values[i] : cd(0, 0);
-        v[(pos - 1) >> 1] = z;
-        v[(m - pos - 1) >> 1] = std::conj(z);
-        pos = (pos * 3) & (m - 1);
+    for (std::size_t i = 0; i < values.size(); ++i) {
+        v[map[i]] = values[i];
+        v[map[i + slots]] = cd(values[i].real(), -values[i].imag());  // std::conj
     }
-    fft(v, -1);
-    std::vector<long> coeff(N);
-    double maxabs = 0;
-    for (std::size_t k = 0; k < N; ++k) {
-        const cd zk = std::polar(1.0, -kPi * (double)k / (double)N);
-        const double c = std::round((v[k] * zk).real() / (double)N * scale);
-        maxabs = std::max(maxabs, std::fabs(c));
-        coeff[k] = (long)c;
-    }
-    // SEAL CKKSEncoder::encode_internal: ceil(log2(max(max_coeff, 1))) + 1 >= total bits -> throw
-    const int max_bits = (int)std::ceil(std::log2(std::max(maxabs, 1.0))) + 1;
+    const double fix = scale / (double)N;
+    seal_transform_from_rev(v.data(), __builtin_ctzll(N), inv_roots.data(), &fix);
+    double max_coeff = 0;  // over the unrounded real parts, as SEAL
+    for (std::size_t k = 0; k < N; ++k) max_coeff = std::max(max_coeff, std::fabs(v[k].real()));
+    const int max_bits = (int)std::ceil(std::log2(std::max(max_coeff, 1.0))) + 1;
     if (max_bits >= ctx.total_bits(level)) throw std::invalid_argument("encoded values are too large");
-    if (maxabs >= 0x1.0p62) throw std::invalid_argument("encoded values are too large for the oracle");
     Plaintext pt;
     pt.level = level;
     pt.scale = scale;
     pt.data.assign(level * N, 0);
-    for (std::size_t i = 0; i < level; ++i) {
-        u64 *limb = pt.data.data() + i * N;
-        for (std::size_t k = 0; k < N; ++k) limb[k] = signed_mod(coeff[k], ctx.mod(i).value);
-        ntt_forward(limb, ctx.ntt(i));
+    for (std::size_t k = 0; k < N; ++k) {
+        const double c = std::round(v[k].real());
+        const bool neg = std::signbit(c);
+        const double a = std::fabs(c);
+        for (std::size_t i = 0; i < level; ++i) {
+            const u64 q = ctx.mod(i).value, r = encode_residue(a, q);
+            pt.data[i * N + k] = neg && r ? q - r : r;  // negate_uint_mod
+        }
     }
+    for (std::size_t i = 0; i < level; ++i) ntt_forward(pt.data.data() + i * N, ctx.ntt(i));
     return pt;
 }
 

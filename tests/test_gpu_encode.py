@@ -1,9 +1,9 @@
-"""GPU CKKS encoder (hec_encode) vs the oracle's encode() on the same values,
-bit-exact: both run the same IEEE double sequence without contraction (slot map, radix-2 FFT, twist,
-round), then the integer residues and NTT.  The oracle's encoder restates SEAL's CKKSEncoder::encode
-(scatter by matrix_reps_index_map_, inverse DWT, round, residues, NTT); its FFT association differs
-from SEAL's DWTHandler, so the coefficients match SEAL's except where Re(...) lands within float error
-of a rounding tie: the encoder is parity-unpinned against SEAL itself (no SEAL vectors exist here)."""
+"""GPU CKKS encoder (hec_encode) vs the oracle's encode() on the same values, bit-exact.
+Both restate SEAL 4.1's CKKSEncoder::encode_internal operation for operation (matrix_reps_index_map_ scatter,
+DWTHandler::transform_from_rev over inv_root_powers_ with fix = scale / N in the last layer, std::round, residues,
+NTT); the oracle's restatement is pinned to an independent pure-Python one and to the reference binary's code read
+as data (tests/test_oracle_encode.py), so these plaintexts are SEAL's to the extent that reading pins them (no SEAL
+vectors exist here)."""
 import numpy as np
 import pytest
 
@@ -32,6 +32,7 @@ def test_encode_bitexact_small(orc, hecdna, N, bits):
     _check(e, z, 2.0**30, L)                                                   # complex
     _check(e, rng.uniform(-100, 100, (2, 37)), 2.0**25, L - 1)                 # few slots, lower level
     _check(e, np.zeros((1, 4)), 2.0**40, L)                                    # all zero
+    _check(e, rng.uniform(-1e3, 1e3, (2, N // 2)), 2.0**62, L)                 # coefficients beyond 2^64
 
 
 def test_encode_reference_data_cfg1(orc, hecdna):
