@@ -105,6 +105,8 @@ struct Ctx {
     int fan_split = 1;             // HEC_FANSPLIT=0: Barrett (not the FP64 split) for the mod-down rounding limbs
                                    // at FP64 targets (FanDivRound::xf16)
     int fan2 = 1;                  // HEC_FAN2=0: the LDS-round k_fan instead of the register-direct k_fan2
+    int hfuse = 1;                 // HEC_HFUSE=0: hoisted node = ks_modup pass B, then k_hmacm per sibling pair
+    int hfuse_bg = 2;              // HEC_HFUSE_BG: batch entries per k_hfuse block at N = 2^15 (1, 2 or 4)
     bool fan_out = true;           // HEC_FAN=0: separate INTT pass A (fan-out fuses it into the forward passes A)
     int lanes = 3;                 // HEC_LANES: concurrent batch lanes of a matvec (hec_engine.hip matvec_lanes)
     int lane_min_batch = 16;       // input vectors per lane at least
@@ -180,6 +182,10 @@ void hoisted_mac_multi(Ctx &c, PolyArr X1, const u64 *E, const int *zl, const HC
 // three children in one sibling-fused launch (3 x 4 FP64 / 3 x 2 integer batch entries per thread)
 void hoisted_mac_3(Ctx &c, PolyArr X1, const u64 *E, const int *zl, const HChildSpec *kids, int B, int l);
 int hoisted_group(const Ctx &c);  // children per hoisted_mac_multi call for c.hmac_cfg
+// fused hoisted MAC (k_hfuse): the node's pass-A-domain digits E -> pass B in LDS -> the key MACs of up to
+// HFUSE_MAXK sibling rotations (HEC_HFUSE=0: ks_modup pass B + k_hmacm per sibling pair)
+constexpr int HFUSE_MAXK = 12;
+void hoisted_mac_fused(Ctx &c, PolyArr X1, const u64 *E, const int *zl, const HChildSpec *kids, int nkids, int B, int l);
 void fan_divide_round(Ctx &c, const u64 *Y, u64 ysb, u64 ysk, u64 *Z, int B, int nk, int nl, int last_idx);
 void galois_permute(Ctx &c, PolyArr in, PolyArr out, int B, int nk, int nl, u32 elt);
 void tensor_acc(Ctx &c, PolyArr R, const u64 *A, u64 a_sk, PolyArr ACC, int B, int l, bool assign);

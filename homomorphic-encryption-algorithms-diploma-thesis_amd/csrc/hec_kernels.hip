@@ -1490,6 +1490,277 @@ void hoisted_mac_3(Ctx &c, PolyArr X1, const u64 *E, const int *zl, const HChild
     launch_hmacm<4, 2, 3>(c, X1, E, zl, kids, 3, B, l);
 }
 
+// ======================================================= fused hoisted MAC: pass B of the digits + siblings ==
+// k_hfuse finishes the node's mod-up NTTs AND runs the key MAC of up to HFUSE_MAXK sibling rotations in one kernel,
+// so the node's digits go to HBM once, in the pass-A domain (k_fan2's output E), and are read once per launch
+// instead of: written in NTT form by a separate pass B, re-read and re-written by it, then re-read by every
+// sibling-pair MAC launch (those round trips were about half of a step's bytes).
+// A block owns one pass-B chunk (P = 2^LOGP contiguous coefficients) of one target prime I for BG batch entries:
+//   1. it stages every digit tile of its chunk into LDS: E[b][I][J] (pass-A domain) for J != I, and for J == I the
+//      node's own NTT-form c1 (X1), SEAL's reuse of the NTT-form input;
+//   2. it runs pass B (the last LOGP stages of NTT_I) on every J != I tile in LDS, 8 elements per thread, the
+//      chunk's twiddles staged once;
+//   3. for every child c (elt, its inverse einv) a thread owns two adjacent SOURCE positions s, s + 1 of BT batch
+//      entries and accumulates, at the child's output position t = gal_c^-1(s) (pairs stay pairs),
+//        ACC_c[b][k][I][t] = sum_J key_c[J][k][I][t] e_J[s] + W_c[I][t] KW_c[k][I][t]
+//      (the sign-mask term factored out of the digit loop, see k_hmacm; rare zero corrections as there), exact:
+//      FP64 targets as integer-valued double sums of fp_mulmod products, 60-bit targets in 128-bit sums, one
+//      reduction at the end.  Every term is SEAL's, so each child's key-switch input is bit-identical.
+// Grid: two segments (integer targets first, then FP64), each XCD-aware like k_hmacm: the batch groups of one
+// (chunk, I) get ids = mod 8, so they share an XCD and its L2 copy of the children's key chunk.
+struct HFuseKids {
+    HChild c[HFUSE_MAXK];
+    int n;
+};
+constexpr int hfuse_ld(int logp) { return (1 << logp) + (1 << logp) / 8 + 8; }  // tile stride (k_bmac's padding)
+
+template <int LOGP, int BG, int BS, bool FP>
+__device__ __forceinline__ void hfuse_body(u64 *lds, u64 *ltw, PolyArr X1, const u64 *__restrict__ E,
+                                           const int *__restrict__ zl, const HFuseKids &ch, int B, int l, int K,
+                                           int logN, const DevPrime &pr, const TwTables &tt, int I, int kI, int chunk,
+                                           int b0, const u64 *__restrict__ cji, const u64 *__restrict__ psipow)
+{
+    constexpr int P = 1 << LOGP, EPT = 8, TPT = P / EPT, PAIRS = P / 2, THREADS = PAIRS * BS, BT = BG / BS;
+    constexpr int LD = hfuse_ld(LOGP), CONC = THREADS / TPT;
+    static_assert(THREADS % TPT == 0 && BG % BS == 0, "thread layout");
+    const u64 N = 1ull << logN, base = (u64)chunk << LOGP;
+    const int nb = min(BG, B - b0);
+    auto addr_of = [](int tl, int x) { return tl * LD + x + (x >> 3); };
+    {  // the chunk's pass-B twiddles (entry k = 2^s - 1 + i of stage s), independent of the digit
+        const u64 R = 1ull << (logN - LOGP);
+        const ulonglong2 *tw = tt.b + ((u64)kI << logN);
+        const double *twf = tt.fb + ((u64)kI << logN);
+        for (int k = threadIdx.x; k < P - 1; k += THREADS) {
+            const int st = 31 - __clz(k + 1), i = k + 1 - (1 << st);
+            const u64 gi = R * ((1ull << st) - 1) + (u64)i * R + (u64)chunk;
+            if constexpr (FP) ltw[k] = (u64)__double_as_longlong(twf[gi]);
+            else {
+                const ulonglong2 w = tw[gi];
+                ltw[2 * k] = w.x;
+                ltw[2 * k + 1] = w.y;
+            }
+        }
+    }
+    // 1. every (J, batch entry) tile of the chunk, 16-B loads
+    for (int w = threadIdx.x; w < l * BG * PAIRS; w += THREADS) {
+        const int tl = w / PAIRS, pp = w % PAIRS, J = tl / BG, bb = tl % BG;
+        if (bb >= nb) continue;
+        const int b = b0 + bb;
+        const u64 *src = J == I ? X1.p + (u64)b * X1.sb + ((u64)J << logN)
+                                : E + (((u64)((b * (l + 1) + I) * l + J)) << logN);
+        ulonglong2 v = *(const ulonglong2 *)(src + base + 2 * pp);
+        if constexpr (FP) {
+            if (J == I) v = ulonglong2{(u64)__double_as_longlong(u2d(v.x)), (u64)__double_as_longlong(u2d(v.y))};
+        }
+        lds[addr_of(tl, 2 * pp)] = v.x;
+        lds[addr_of(tl, 2 * pp + 1)] = v.y;
+    }
+    __syncthreads();
+    // 2. pass B on the J != I tiles, CONC transforms at a time (rounds of 3 stages, 8 elements per thread)
+    const LdsTw twg{ltw};
+    const int ntf = l * BG;
+    for (int t0 = 0; t0 < ntf; t0 += CONC) {
+        const int tl = t0 + (int)threadIdx.x / TPT, ts = (int)threadIdx.x % TPT;
+        const bool act = tl < ntf && tl / BG != I && tl % BG < nb;
+        auto addr = [tl](int x) { return tl * LD + x + (x >> 3); };
+        if constexpr (LOGP <= 6) {
+            if (act) ntt_round_g<LOGP, 0, 3, EPT, false, FP, false>(lds, addr, ts, twg, pr, nullptr);
+            __syncthreads();
+            if (act) ntt_round_g<LOGP, 3, LOGP, EPT, false, FP, false>(lds, addr, ts, twg, pr, nullptr);
+        } else {
+            if (act) ntt_round_g<LOGP, 0, 3, EPT, false, FP, false>(lds, addr, ts, twg, pr, nullptr);
+            __syncthreads();
+            if (act) ntt_round_g<LOGP, 3, 6, EPT, false, FP, false>(lds, addr, ts, twg, pr, nullptr);
+            __syncthreads();
+            if (act) ntt_round_g<LOGP, 6, LOGP, EPT, false, FP, false>(lds, addr, ts, twg, pr, nullptr);
+        }
+        __syncthreads();
+    }
+    // 3. the children's MACs from the LDS tiles
+    const int pp = (int)threadIdx.x % PAIRS, bs = (int)threadIdx.x / PAIRS;
+    const u64 s0 = base + 2 * pp;
+    const bool zeros = zl[0] != 0;
+    const u64 *pp_pow = psipow + ((u64)kI << (logN + 1));
+    const u64 q = pr.q, two_q = 2 * q;
+    for (int qi = 0; qi < ch.n; ++qi) {
+        const HChild &cc = ch.c[qi];
+        const u32 t = galois_src((u32)s0, cc.einv, logN);
+        const u64 kc = t & ~1u;
+        const bool sw = t & 1;
+        u64 wk[4];
+        {
+            const ulonglong2 w = *(const ulonglong2 *)(cc.W + ((u64)kI << logN) + kc);
+            const ulonglong2 m0 = *(const ulonglong2 *)(cc.KW + ((u64)I << logN) + kc);
+            const ulonglong2 m1 = *(const ulonglong2 *)(cc.KW + ((u64)(l + 1 + I) << logN) + kc);
+            wk[0] = mulmod(w.x, m0.x, pr);
+            wk[1] = mulmod(w.y, m0.y, pr);
+            wk[2] = mulmod(w.x, m1.x, pr);
+            wk[3] = mulmod(w.y, m1.y, pr);
+            if (sw) {
+                u64 x = wk[0]; wk[0] = wk[1]; wk[1] = x;
+                x = wk[2]; wk[2] = wk[3]; wk[3] = x;
+            }
+        }
+        double f[FP ? BT : 1][4];
+        U128 a[FP ? 1 : BT][4];
+#pragma unroll
+        for (int tb = 0; tb < BT; ++tb)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                if constexpr (FP) f[tb][r] = u2d(wk[r]);
+                else a[tb][r] = U128{wk[r], 0};
+            }
+        const u64 *kp = cc.key + ((u64)kI << logN) + kc;
+        ulonglong2 k0 = *(const ulonglong2 *)kp, k1 = *(const ulonglong2 *)(kp + ((u64)K << logN));
+        for (int J = 0; J < l; ++J) {
+            ulonglong2 n0{0, 0}, n1{0, 0};
+            if (J + 1 < l) {  // the next digit's key words, issued before this digit's products
+                const u64 *np = kp + ((u64)((J + 1) * 2) * K << logN);
+                n0 = *(const ulonglong2 *)np;
+                n1 = *(const ulonglong2 *)(np + ((u64)K << logN));
+            }
+            if (sw) {
+                k0 = ulonglong2{k0.y, k0.x};
+                k1 = ulonglong2{k1.y, k1.x};
+            }
+            const u64 cj = cji[J * K + kI];
+#pragma unroll
+            for (int tb = 0; tb < BT; ++tb) {
+                const int bb = bs * BT + tb;
+                if (bb >= nb) break;
+                const int tl = J * BG + bb;
+                u64 e0 = lds[addr_of(tl, 2 * pp)], e1 = lds[addr_of(tl, 2 * pp + 1)];
+                if (J != I && zeros) {  // output slots (in source order) of this child: kc ^ sw, kc ^ !sw
+                    const int *z = zl + 1 + ((b0 + bb) * l + J) * (HEC_ZCAP + 1);
+                    const int nz = min(z[0], HEC_ZCAP);
+                    if (nz > 0) {
+                        if constexpr (FP) {
+                            e0 = fp_canon(__longlong_as_double((long long)e0), pr.qd, pr.qinv);
+                            e1 = fp_canon(__longlong_as_double((long long)e1), pr.qd, pr.qinv);
+                        } else {
+                            e0 = csub(csub(e0, two_q), q);
+                            e1 = csub(csub(e1, two_q), q);
+                        }
+                        const u64 ko0 = kc | (u64)sw, ko1 = kc | (u64)!sw;
+                        for (int zi = 0; zi < nz; ++zi) {
+                            u64 tt2 = ((u64)z[1 + zi] * cc.elt) & (2 * N - 1);
+                            if (tt2 < N) continue;
+                            tt2 -= N;
+                            const u64 ex0 = ((2 * (u64)bitrev((u32)ko0, logN) + 1) * tt2) & (2 * N - 1);
+                            const u64 ex1 = ((2 * (u64)bitrev((u32)ko1, logN) + 1) * tt2) & (2 * N - 1);
+                            e0 = submod(e0, mulmod(cj, pp_pow[ex0], pr), q);
+                            e1 = submod(e1, mulmod(cj, pp_pow[ex1], pr), q);
+                        }
+                        if constexpr (FP) {
+                            e0 = (u64)__double_as_longlong(u2d(e0));
+                            e1 = (u64)__double_as_longlong(u2d(e1));
+                        }
+                    }
+                }
+                if constexpr (FP) {  // |e| < 10 q: the forward NTT's output before canonicalisation
+                    const double d0 = __longlong_as_double((long long)e0), d1 = __longlong_as_double((long long)e1);
+                    f[tb][0] += fp_mulmod(d0, u2d(k0.x), pr.qd, pr.qinv);
+                    f[tb][1] += fp_mulmod(d1, u2d(k0.y), pr.qd, pr.qinv);
+                    f[tb][2] += fp_mulmod(d0, u2d(k1.x), pr.qd, pr.qinv);
+                    f[tb][3] += fp_mulmod(d1, u2d(k1.y), pr.qd, pr.qinv);
+                } else {
+                    if (J != I) {  // lazy [0, 4q) -> canonical
+                        e0 = csub(csub(e0, two_q), q);
+                        e1 = csub(csub(e1, two_q), q);
+                    }
+                    mac128(a[tb][0], e0, k0.x);
+                    mac128(a[tb][1], e1, k0.y);
+                    mac128(a[tb][2], e0, k1.x);
+                    mac128(a[tb][3], e1, k1.y);
+                }
+            }
+            k0 = n0;
+            k1 = n1;
+        }
+#pragma unroll
+        for (int tb = 0; tb < BT; ++tb) {
+            const int bb = bs * BT + tb;
+            if (bb >= nb) break;
+            const int b = b0 + bb;
+            u64 r[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                if constexpr (FP) r[i] = fp_canon(f[tb][i], pr.qd, pr.qinv);
+                else r[i] = barrett128(a[tb][i].lo, a[tb][i].hi, q, pr.r0, pr.r1);
+            }
+            u64 *o0 = cc.ACC + (((u64)((b * 2 + 0) * (l + 1) + I)) << logN) + kc;
+            u64 *o1 = cc.ACC + (((u64)((b * 2 + 1) * (l + 1) + I)) << logN) + kc;
+            *(ulonglong2 *)o0 = sw ? ulonglong2{r[1], r[0]} : ulonglong2{r[0], r[1]};
+            *(ulonglong2 *)o1 = sw ? ulonglong2{r[3], r[2]} : ulonglong2{r[2], r[3]};
+        }
+    }
+}
+
+template <int LOGP, int BG, int BS>
+__global__ void __launch_bounds__((1 << LOGP) / 2 * BS)
+    k_hfuse(PolyArr X1, const u64 *__restrict__ E, const int *__restrict__ zl, const HFuseKids ch, int B, int l, int K,
+            int logN, const DevPrime *__restrict__ primes, TwTables tt, const int *__restrict__ Imap, int nI, int nint,
+            const u64 *__restrict__ cji, const u64 *__restrict__ psipow, int wsplit)
+{
+    constexpr int P = 1 << LOGP;
+    extern __shared__ u64 hfuse_lds[];  // [2 P] twiddles, then l BG tiles of hfuse_ld(LOGP) words
+    u64 *ltw = hfuse_lds, *lds = hfuse_lds + 2 * P;
+    const int X = 1 << (logN - LOGP);  // chunks
+    const int nbg = (B + BG - 1) / BG;
+    const bool integer = (int)blockIdx.x < wsplit;
+    const int w = integer ? blockIdx.x : blockIdx.x - wsplit;
+    const int g8 = w & 7, rest = w >> 3, bg = rest % nbg, G = (rest / nbg) * 8 + g8;
+    if (G >= X * (integer ? nint : nI - nint)) return;
+    const int yi = G / X + (integer ? 0 : nint), chunk = G % X;
+    const int I = Imap[yi];
+    const int kI = I == l ? K - 1 : I;
+    const DevPrime pr = primes[kI];
+    if (integer)
+        hfuse_body<LOGP, BG, BS, false>(lds, ltw, X1, E, zl, ch, B, l, K, logN, pr, tt, I, kI, chunk, bg * BG, cji, psipow);
+    else
+        hfuse_body<LOGP, BG, BS, true>(lds, ltw, X1, E, zl, ch, B, l, K, logN, pr, tt, I, kI, chunk, bg * BG, cji, psipow);
+}
+
+template <int LOGP, int BG, int BS>
+static void launch_hfuse(Ctx &c, PolyArr X1, const u64 *E, const int *zl, const HChildSpec *kids, int nkids, int B,
+                         int l)
+{
+    HFuseKids ch{};
+    ch.n = nkids;
+    for (int q = 0; q < nkids; ++q)
+        ch.c[q] = HChild{kids[q].elt, kids[q].einv, kids[q].key, kids[q].W, kids[q].ACC, kids[q].KW};
+    const int nint = c.imap_nint[l], X = (int)(c.N >> LOGP), nbg = (B + BG - 1) / BG;
+    const int gI = (X * nint + 7) / 8 * 8, gF = (X * (l + 1 - nint) + 7) / 8 * 8;
+    const int wsplit = gI * nbg, total = wsplit + gF * nbg;
+    const TwTables fwd{c.tw, c.twb, c.twf, c.twbf};
+    const std::size_t shm = (std::size_t)(2 * (1 << LOGP) + l * BG * hfuse_ld(LOGP)) * sizeof(u64);
+    k_hfuse<LOGP, BG, BS><<<dim3((unsigned)total), (1 << LOGP) / 2 * BS, shm, c.stream>>>(
+        X1, E, zl, ch, B, l, (int)c.K, c.logN, c.primes, fwd, c.imap_at(l), l + 1, nint, c.cji, c.psipow, wsplit);
+    HEC_HIP(hipGetLastError());
+}
+
+void hoisted_mac_fused(Ctx &c, PolyArr X1, const u64 *E, const int *zl, const HChildSpec *kids, int nkids, int B, int l)
+{
+    if (nkids < 1 || nkids > HFUSE_MAXK) throw std::invalid_argument("hoisted_mac_fused: children per launch");
+    if (l > HEC_MAXL) throw std::invalid_argument("too many limbs");
+    // <LOGP, batch entries per block, batch sets per block>: LDS = l BG hfuse_ld(LOGP) words (the largest static
+    // shape is HEC_MAXL digits), blocks of P / 2 x BS threads
+    switch (c.logN) {
+    case 10: launch_hfuse<5, 4, 4>(c, X1, E, zl, kids, nkids, B, l); break;
+    case 11: launch_hfuse<5, 4, 4>(c, X1, E, zl, kids, nkids, B, l); break;
+    case 12: launch_hfuse<6, 4, 2>(c, X1, E, zl, kids, nkids, B, l); break;
+    case 13: launch_hfuse<6, 4, 2>(c, X1, E, zl, kids, nkids, B, l); break;
+    case 14: launch_hfuse<7, 2, 2>(c, X1, E, zl, kids, nkids, B, l); break;
+    case 15:
+        if (c.hfuse_bg == 4) launch_hfuse<7, 4, 2>(c, X1, E, zl, kids, nkids, B, l);
+        else if (c.hfuse_bg == 1) launch_hfuse<7, 1, 1>(c, X1, E, zl, kids, nkids, B, l);
+        else launch_hfuse<7, 2, 2>(c, X1, E, zl, kids, nkids, B, l);
+        break;
+    case 16: launch_hfuse<8, 1, 1>(c, X1, E, zl, kids, nkids, B, l); break;
+    default: throw std::invalid_argument("poly_modulus_degree must be 2^10 .. 2^16");
+    }
+}
+
 void fan_divide_round(Ctx &c, const u64 *Y, u64 ysb, u64 ysk, u64 *Z, int B, int nk, int nl, int last_idx)
 {
     if (nl > HEC_MAXL) throw std::invalid_argument("too many limbs");
