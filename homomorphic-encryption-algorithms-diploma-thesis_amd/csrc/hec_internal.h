@@ -107,6 +107,7 @@ struct Ctx {
     int fan2 = 1;                  // HEC_FAN2=0: the LDS-round k_fan instead of the register-direct k_fan2
     int hfuse = 1;                 // HEC_HFUSE=0: hoisted node = ks_modup pass B, then k_hmacm per sibling pair
     int hfuse_bg = 2;              // HEC_HFUSE_BG: batch entries per k_hfuse block at N = 2^15 (1, 2 or 4)
+    int hfuse_cg = 4;              // HEC_HFUSE_CG: children per k_hfuse2 launch at N = 2^14, 2^15 (2, 4 or 6)
     bool fan_out = true;           // HEC_FAN=0: separate INTT pass A (fan-out fuses it into the forward passes A)
     int lanes = 3;                 // HEC_LANES: concurrent batch lanes of a matvec (hec_engine.hip matvec_lanes)
     int lane_min_batch = 16;       // input vectors per lane at least

@@ -1576,122 +1576,152 @@ __device__ __forceinline__ void hfuse_body(u64 *lds, u64 *ltw, PolyArr X1, const
         }
         __syncthreads();
     }
-    // 3. the children's MACs from the LDS tiles
+    // 3. the children's MACs from the LDS tiles, two children per pass (independent key streams), each child's key
+    //    words for KCH digits issued together before their products
     const int pp = (int)threadIdx.x % PAIRS, bs = (int)threadIdx.x / PAIRS;
     const u64 s0 = base + 2 * pp;
     const bool zeros = zl[0] != 0;
     const u64 *pp_pow = psipow + ((u64)kI << (logN + 1));
     const u64 q = pr.q, two_q = 2 * q;
-    for (int qi = 0; qi < ch.n; ++qi) {
-        const HChild &cc = ch.c[qi];
-        const u32 t = galois_src((u32)s0, cc.einv, logN);
-        const u64 kc = t & ~1u;
-        const bool sw = t & 1;
-        u64 wk[4];
-        {
-            const ulonglong2 w = *(const ulonglong2 *)(cc.W + ((u64)kI << logN) + kc);
-            const ulonglong2 m0 = *(const ulonglong2 *)(cc.KW + ((u64)I << logN) + kc);
-            const ulonglong2 m1 = *(const ulonglong2 *)(cc.KW + ((u64)(l + 1 + I) << logN) + kc);
-            wk[0] = mulmod(w.x, m0.x, pr);
-            wk[1] = mulmod(w.y, m0.y, pr);
-            wk[2] = mulmod(w.x, m1.x, pr);
-            wk[3] = mulmod(w.y, m1.y, pr);
-            if (sw) {
-                u64 x = wk[0]; wk[0] = wk[1]; wk[1] = x;
-                x = wk[2]; wk[2] = wk[3]; wk[3] = x;
+    constexpr int CGP = 2, KCH = 2;
+    for (int q0 = 0; q0 < ch.n; q0 += CGP) {
+        const int nq = min(CGP, ch.n - q0);
+        u64 kc[CGP];
+        bool sw[CGP];
+        double f[FP ? CGP : 1][FP ? BT : 1][4];
+        U128 a[FP ? 1 : CGP][FP ? 1 : BT][4];
+#pragma unroll
+        for (int c2 = 0; c2 < CGP; ++c2) {
+            const HChild &cc = ch.c[q0 + (c2 < nq ? c2 : 0)];
+            const u32 t = galois_src((u32)s0, cc.einv, logN);
+            kc[c2] = t & ~1u;
+            sw[c2] = t & 1;
+            // the sign-mask term W KW at the output pair, in source order
+            const ulonglong2 w = *(const ulonglong2 *)(cc.W + ((u64)kI << logN) + kc[c2]);
+            const ulonglong2 m0 = *(const ulonglong2 *)(cc.KW + ((u64)I << logN) + kc[c2]);
+            const ulonglong2 m1 = *(const ulonglong2 *)(cc.KW + ((u64)(l + 1 + I) << logN) + kc[c2]);
+            if constexpr (FP) {  // canonical operands < q < 2^42: fp_mulmod is exact
+                double wk[4] = {fp_mulmod(u2d(w.x), u2d(m0.x), pr.qd, pr.qinv), fp_mulmod(u2d(w.y), u2d(m0.y), pr.qd, pr.qinv),
+                                fp_mulmod(u2d(w.x), u2d(m1.x), pr.qd, pr.qinv), fp_mulmod(u2d(w.y), u2d(m1.y), pr.qd, pr.qinv)};
+                if (sw[c2]) {
+                    double x = wk[0]; wk[0] = wk[1]; wk[1] = x;
+                    x = wk[2]; wk[2] = wk[3]; wk[3] = x;
+                }
+#pragma unroll
+                for (int tb = 0; tb < BT; ++tb)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) f[c2][tb][r] = wk[r];
+            } else {
+                u64 wk[4] = {mulmod(w.x, m0.x, pr), mulmod(w.y, m0.y, pr), mulmod(w.x, m1.x, pr), mulmod(w.y, m1.y, pr)};
+                if (sw[c2]) {
+                    u64 x = wk[0]; wk[0] = wk[1]; wk[1] = x;
+                    x = wk[2]; wk[2] = wk[3]; wk[3] = x;
+                }
+#pragma unroll
+                for (int tb = 0; tb < BT; ++tb)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) a[c2][tb][r] = U128{wk[r], 0};
             }
         }
-        double f[FP ? BT : 1][4];
-        U128 a[FP ? 1 : BT][4];
+        for (int J0 = 0; J0 < l; J0 += KCH) {
+            ulonglong2 kk[CGP][KCH][2];  // key words of digits J0 .. J0 + KCH - 1, both polys, in source order
 #pragma unroll
-        for (int tb = 0; tb < BT; ++tb)
+            for (int c2 = 0; c2 < CGP; ++c2)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                if constexpr (FP) f[tb][r] = u2d(wk[r]);
-                else a[tb][r] = U128{wk[r], 0};
+                for (int j = 0; j < KCH; ++j) {
+                    if (J0 + j < l && c2 < nq) {
+                        const u64 *kp = ch.c[q0 + c2].key + (((u64)((J0 + j) * 2) * K + kI) << logN) + kc[c2];
+                        kk[c2][j][0] = *(const ulonglong2 *)kp;
+                        kk[c2][j][1] = *(const ulonglong2 *)(kp + ((u64)K << logN));
+                    } else {
+                        kk[c2][j][0] = kk[c2][j][1] = ulonglong2{0, 0};
+                    }
+                }
+#pragma unroll
+            for (int j = 0; j < KCH; ++j) {
+                const int J = J0 + j;
+                if (J >= l) break;
+                const u64 cj = cji[J * K + kI];
+#pragma unroll
+                for (int tb = 0; tb < BT; ++tb) {
+                    const int bb = bs * BT + tb;
+                    if (bb >= nb) break;
+                    const int tl = J * BG + bb;
+                    const u64 r0 = lds[addr_of(tl, 2 * pp)], r1 = lds[addr_of(tl, 2 * pp + 1)];
+#pragma unroll
+                    for (int c2 = 0; c2 < CGP; ++c2) {
+                        if (c2 >= nq) break;
+                        u64 e0 = r0, e1 = r1;
+                        if (J != I && zeros) {  // output slots (in source order) of this child: kc ^ sw, kc ^ !sw
+                            const int *z = zl + 1 + ((b0 + bb) * l + J) * (HEC_ZCAP + 1);
+                            const int nz = min(z[0], HEC_ZCAP);
+                            if (nz > 0) {
+                                if constexpr (FP) {
+                                    e0 = fp_canon(__longlong_as_double((long long)e0), pr.qd, pr.qinv);
+                                    e1 = fp_canon(__longlong_as_double((long long)e1), pr.qd, pr.qinv);
+                                } else {
+                                    e0 = csub(csub(e0, two_q), q);
+                                    e1 = csub(csub(e1, two_q), q);
+                                }
+                                const u64 ko0 = kc[c2] | (u64)sw[c2], ko1 = kc[c2] | (u64)!sw[c2];
+                                const u32 elt = ch.c[q0 + c2].elt;
+                                for (int zi = 0; zi < nz; ++zi) {
+                                    u64 tt2 = ((u64)z[1 + zi] * elt) & (2 * N - 1);
+                                    if (tt2 < N) continue;
+                                    tt2 -= N;
+                                    const u64 ex0 = ((2 * (u64)bitrev((u32)ko0, logN) + 1) * tt2) & (2 * N - 1);
+                                    const u64 ex1 = ((2 * (u64)bitrev((u32)ko1, logN) + 1) * tt2) & (2 * N - 1);
+                                    e0 = submod(e0, mulmod(cj, pp_pow[ex0], pr), q);
+                                    e1 = submod(e1, mulmod(cj, pp_pow[ex1], pr), q);
+                                }
+                                if constexpr (FP) {
+                                    e0 = (u64)__double_as_longlong(u2d(e0));
+                                    e1 = (u64)__double_as_longlong(u2d(e1));
+                                }
+                            }
+                        }
+                        const ulonglong2 k0 = sw[c2] ? ulonglong2{kk[c2][j][0].y, kk[c2][j][0].x} : kk[c2][j][0];
+                        const ulonglong2 k1 = sw[c2] ? ulonglong2{kk[c2][j][1].y, kk[c2][j][1].x} : kk[c2][j][1];
+                        if constexpr (FP) {  // |e| < 10 q: the forward NTT's output before canonicalisation
+                            const double d0 = __longlong_as_double((long long)e0), d1 = __longlong_as_double((long long)e1);
+                            f[c2][tb][0] += fp_mulmod(d0, u2d(k0.x), pr.qd, pr.qinv);
+                            f[c2][tb][1] += fp_mulmod(d1, u2d(k0.y), pr.qd, pr.qinv);
+                            f[c2][tb][2] += fp_mulmod(d0, u2d(k1.x), pr.qd, pr.qinv);
+                            f[c2][tb][3] += fp_mulmod(d1, u2d(k1.y), pr.qd, pr.qinv);
+                        } else {
+                            if (J != I) {  // lazy [0, 4q) -> canonical
+                                e0 = csub(csub(e0, two_q), q);
+                                e1 = csub(csub(e1, two_q), q);
+                            }
+                            mac128(a[c2][tb][0], e0, k0.x);
+                            mac128(a[c2][tb][1], e1, k0.y);
+                            mac128(a[c2][tb][2], e0, k1.x);
+                            mac128(a[c2][tb][3], e1, k1.y);
+                        }
+                    }
+                }
             }
-        const u64 *kp = cc.key + ((u64)kI << logN) + kc;
-        ulonglong2 k0 = *(const ulonglong2 *)kp, k1 = *(const ulonglong2 *)(kp + ((u64)K << logN));
-        for (int J = 0; J < l; ++J) {
-            ulonglong2 n0{0, 0}, n1{0, 0};
-            if (J + 1 < l) {  // the next digit's key words, issued before this digit's products
-                const u64 *np = kp + ((u64)((J + 1) * 2) * K << logN);
-                n0 = *(const ulonglong2 *)np;
-                n1 = *(const ulonglong2 *)(np + ((u64)K << logN));
-            }
-            if (sw) {
-                k0 = ulonglong2{k0.y, k0.x};
-                k1 = ulonglong2{k1.y, k1.x};
-            }
-            const u64 cj = cji[J * K + kI];
+        }
+#pragma unroll
+        for (int c2 = 0; c2 < CGP; ++c2) {
+            if (c2 >= nq) break;
+            const HChild &cc = ch.c[q0 + c2];
 #pragma unroll
             for (int tb = 0; tb < BT; ++tb) {
                 const int bb = bs * BT + tb;
                 if (bb >= nb) break;
-                const int tl = J * BG + bb;
-                u64 e0 = lds[addr_of(tl, 2 * pp)], e1 = lds[addr_of(tl, 2 * pp + 1)];
-                if (J != I && zeros) {  // output slots (in source order) of this child: kc ^ sw, kc ^ !sw
-                    const int *z = zl + 1 + ((b0 + bb) * l + J) * (HEC_ZCAP + 1);
-                    const int nz = min(z[0], HEC_ZCAP);
-                    if (nz > 0) {
-                        if constexpr (FP) {
-                            e0 = fp_canon(__longlong_as_double((long long)e0), pr.qd, pr.qinv);
-                            e1 = fp_canon(__longlong_as_double((long long)e1), pr.qd, pr.qinv);
-                        } else {
-                            e0 = csub(csub(e0, two_q), q);
-                            e1 = csub(csub(e1, two_q), q);
-                        }
-                        const u64 ko0 = kc | (u64)sw, ko1 = kc | (u64)!sw;
-                        for (int zi = 0; zi < nz; ++zi) {
-                            u64 tt2 = ((u64)z[1 + zi] * cc.elt) & (2 * N - 1);
-                            if (tt2 < N) continue;
-                            tt2 -= N;
-                            const u64 ex0 = ((2 * (u64)bitrev((u32)ko0, logN) + 1) * tt2) & (2 * N - 1);
-                            const u64 ex1 = ((2 * (u64)bitrev((u32)ko1, logN) + 1) * tt2) & (2 * N - 1);
-                            e0 = submod(e0, mulmod(cj, pp_pow[ex0], pr), q);
-                            e1 = submod(e1, mulmod(cj, pp_pow[ex1], pr), q);
-                        }
-                        if constexpr (FP) {
-                            e0 = (u64)__double_as_longlong(u2d(e0));
-                            e1 = (u64)__double_as_longlong(u2d(e1));
-                        }
-                    }
-                }
-                if constexpr (FP) {  // |e| < 10 q: the forward NTT's output before canonicalisation
-                    const double d0 = __longlong_as_double((long long)e0), d1 = __longlong_as_double((long long)e1);
-                    f[tb][0] += fp_mulmod(d0, u2d(k0.x), pr.qd, pr.qinv);
-                    f[tb][1] += fp_mulmod(d1, u2d(k0.y), pr.qd, pr.qinv);
-                    f[tb][2] += fp_mulmod(d0, u2d(k1.x), pr.qd, pr.qinv);
-                    f[tb][3] += fp_mulmod(d1, u2d(k1.y), pr.qd, pr.qinv);
-                } else {
-                    if (J != I) {  // lazy [0, 4q) -> canonical
-                        e0 = csub(csub(e0, two_q), q);
-                        e1 = csub(csub(e1, two_q), q);
-                    }
-                    mac128(a[tb][0], e0, k0.x);
-                    mac128(a[tb][1], e1, k0.y);
-                    mac128(a[tb][2], e0, k1.x);
-                    mac128(a[tb][3], e1, k1.y);
-                }
-            }
-            k0 = n0;
-            k1 = n1;
-        }
+                const int b = b0 + bb;
+                u64 r[4];
 #pragma unroll
-        for (int tb = 0; tb < BT; ++tb) {
-            const int bb = bs * BT + tb;
-            if (bb >= nb) break;
-            const int b = b0 + bb;
-            u64 r[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                if constexpr (FP) r[i] = fp_canon(f[tb][i], pr.qd, pr.qinv);
-                else r[i] = barrett128(a[tb][i].lo, a[tb][i].hi, q, pr.r0, pr.r1);
+                for (int i = 0; i < 4; ++i) {
+                    if constexpr (FP) r[i] = fp_canon(f[c2][tb][i], pr.qd, pr.qinv);
+                    else r[i] = barrett128(a[c2][tb][i].lo, a[c2][tb][i].hi, q, pr.r0, pr.r1);
+                }
+                u64 *o0 = cc.ACC + (((u64)((b * 2 + 0) * (l + 1) + I)) << logN) + kc[c2];
+                u64 *o1 = cc.ACC + (((u64)((b * 2 + 1) * (l + 1) + I)) << logN) + kc[c2];
+                *(ulonglong2 *)o0 = sw[c2] ? ulonglong2{r[1], r[0]} : ulonglong2{r[0], r[1]};
+                *(ulonglong2 *)o1 = sw[c2] ? ulonglong2{r[3], r[2]} : ulonglong2{r[2], r[3]};
             }
-            u64 *o0 = cc.ACC + (((u64)((b * 2 + 0) * (l + 1) + I)) << logN) + kc;
-            u64 *o1 = cc.ACC + (((u64)((b * 2 + 1) * (l + 1) + I)) << logN) + kc;
-            *(ulonglong2 *)o0 = sw ? ulonglong2{r[1], r[0]} : ulonglong2{r[0], r[1]};
-            *(ulonglong2 *)o1 = sw ? ulonglong2{r[3], r[2]} : ulonglong2{r[2], r[3]};
         }
     }
 }
@@ -1739,10 +1769,287 @@ static void launch_hfuse(Ctx &c, PolyArr X1, const u64 *E, const int *zl, const 
     HEC_HIP(hipGetLastError());
 }
 
+// k_hfuse2: the same fused computation with the digit loop outside the children.  A block (one pass-B chunk of one
+// target prime I, BG batch entries) stages D digits at a time (D BG tiles = one pass-B transform per 16 threads),
+// runs their pass B in LDS, then every thread multiply-accumulates its position pair x BT batch entries into the
+// accumulators of all CG children of the launch: per digit the CG children's key words are independent loads
+// (memory-level parallelism), and the LDS holds only D BG tiles.  Integer (60-bit) and FP64 targets are separate
+// grid segments with their own batch tile (BGI, BGF), as in k_hmacm.
+template <int LOGP, int BG, int BS, int CG, bool FP>
+__device__ __forceinline__ void hfuse2_body(u64 *lds, u64 *ltw, PolyArr X1, const u64 *__restrict__ E,
+                                            const int *__restrict__ zl, const HFuseKids &ch, int B, int l, int K,
+                                            int logN, const DevPrime &pr, const TwTables &tt, int I, int kI, int chunk,
+                                            int b0, const u64 *__restrict__ cji, const u64 *__restrict__ psipow)
+{
+    constexpr int P = 1 << LOGP, EPT = 8, TPT = P / EPT, PAIRS = P / 2, THREADS = PAIRS * BS, BT = BG / BS;
+    constexpr int LD = hfuse_ld(LOGP), CONC = THREADS / TPT, D = CONC / BG > 0 ? CONC / BG : 1;
+    static_assert(THREADS % TPT == 0 && BG % BS == 0, "thread layout");
+    const u64 N = 1ull << logN, base = (u64)chunk << LOGP;
+    const int nb = min(BG, B - b0);
+    const int nk = ch.n;
+    auto addr_of = [](int tl, int x) { return tl * LD + x + (x >> 3); };
+    {  // the chunk's pass-B twiddles
+        const u64 R = 1ull << (logN - LOGP);
+        const ulonglong2 *tw = tt.b + ((u64)kI << logN);
+        const double *twf = tt.fb + ((u64)kI << logN);
+        for (int k = threadIdx.x; k < P - 1; k += THREADS) {
+            const int st = 31 - __clz(k + 1), i = k + 1 - (1 << st);
+            const u64 gi = R * ((1ull << st) - 1) + (u64)i * R + (u64)chunk;
+            if constexpr (FP) ltw[k] = (u64)__double_as_longlong(twf[gi]);
+            else {
+                const ulonglong2 w = tw[gi];
+                ltw[2 * k] = w.x;
+                ltw[2 * k + 1] = w.y;
+            }
+        }
+    }
+    const int pp = (int)threadIdx.x % PAIRS, bs = (int)threadIdx.x / PAIRS;
+    const u64 s0 = base + 2 * pp;
+    const bool zeros = zl[0] != 0;
+    const u64 *pp_pow = psipow + ((u64)kI << (logN + 1));
+    const u64 q = pr.q, two_q = 2 * q;
+    u64 kc[CG];
+    bool sw[CG];
+    double f[FP ? CG : 1][FP ? BT : 1][4];
+    U128 a[FP ? 1 : CG][FP ? 1 : BT][4];
+#pragma unroll
+    for (int c2 = 0; c2 < CG; ++c2) {  // output pairs and the sign-mask terms W KW (source order)
+        const HChild &cc = ch.c[c2 < nk ? c2 : 0];
+        const u32 t = galois_src((u32)s0, cc.einv, logN);
+        kc[c2] = t & ~1u;
+        sw[c2] = t & 1;
+        const ulonglong2 w = *(const ulonglong2 *)(cc.W + ((u64)kI << logN) + kc[c2]);
+        const ulonglong2 m0 = *(const ulonglong2 *)(cc.KW + ((u64)I << logN) + kc[c2]);
+        const ulonglong2 m1 = *(const ulonglong2 *)(cc.KW + ((u64)(l + 1 + I) << logN) + kc[c2]);
+        if constexpr (FP) {
+            double wk[4] = {fp_mulmod(u2d(w.x), u2d(m0.x), pr.qd, pr.qinv), fp_mulmod(u2d(w.y), u2d(m0.y), pr.qd, pr.qinv),
+                            fp_mulmod(u2d(w.x), u2d(m1.x), pr.qd, pr.qinv), fp_mulmod(u2d(w.y), u2d(m1.y), pr.qd, pr.qinv)};
+            if (sw[c2]) {
+                double x = wk[0]; wk[0] = wk[1]; wk[1] = x;
+                x = wk[2]; wk[2] = wk[3]; wk[3] = x;
+            }
+#pragma unroll
+            for (int tb = 0; tb < BT; ++tb)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) f[c2][tb][r] = wk[r];
+        } else {
+            u64 wk[4] = {mulmod(w.x, m0.x, pr), mulmod(w.y, m0.y, pr), mulmod(w.x, m1.x, pr), mulmod(w.y, m1.y, pr)};
+            if (sw[c2]) {
+                u64 x = wk[0]; wk[0] = wk[1]; wk[1] = x;
+                x = wk[2]; wk[2] = wk[3]; wk[3] = x;
+            }
+#pragma unroll
+            for (int tb = 0; tb < BT; ++tb)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) a[c2][tb][r] = U128{wk[r], 0};
+        }
+    }
+    const LdsTw twg{ltw};
+    for (int J0 = 0; J0 < l; J0 += D) {
+        // stage the D BG tiles of digits J0 .. J0 + D - 1 (16-B loads), J == I from the node's NTT-form c1
+        for (int w = threadIdx.x; w < D * BG * PAIRS; w += THREADS) {
+            const int tl = w / PAIRS, p2 = w % PAIRS, J = J0 + tl / BG, bb = tl % BG;
+            if (J >= l || bb >= nb) continue;
+            const int b = b0 + bb;
+            const u64 *src = J == I ? X1.p + (u64)b * X1.sb + ((u64)J << logN)
+                                    : E + (((u64)((b * (l + 1) + I) * l + J)) << logN);
+            ulonglong2 v = *(const ulonglong2 *)(src + base + 2 * p2);
+            if constexpr (FP) {
+                if (J == I) v = ulonglong2{(u64)__double_as_longlong(u2d(v.x)), (u64)__double_as_longlong(u2d(v.y))};
+            }
+            lds[addr_of(tl, 2 * p2)] = v.x;
+            lds[addr_of(tl, 2 * p2 + 1)] = v.y;
+        }
+        __syncthreads();
+        {  // their pass B, one transform per TPT threads
+            const int tl = (int)threadIdx.x / TPT, ts = (int)threadIdx.x % TPT;
+            const int J = J0 + tl / BG;
+            const bool act = tl < D * BG && J < l && J != I && tl % BG < nb;
+            auto addr = [tl](int x) { return tl * LD + x + (x >> 3); };
+            if constexpr (LOGP <= 6) {
+                if (act) ntt_round_g<LOGP, 0, 3, EPT, false, FP, false>(lds, addr, ts, twg, pr, nullptr);
+                __syncthreads();
+                if (act) ntt_round_g<LOGP, 3, LOGP, EPT, false, FP, false>(lds, addr, ts, twg, pr, nullptr);
+            } else {
+                if (act) ntt_round_g<LOGP, 0, 3, EPT, false, FP, false>(lds, addr, ts, twg, pr, nullptr);
+                __syncthreads();
+                if (act) ntt_round_g<LOGP, 3, 6, EPT, false, FP, false>(lds, addr, ts, twg, pr, nullptr);
+                __syncthreads();
+                if (act) ntt_round_g<LOGP, 6, LOGP, EPT, false, FP, false>(lds, addr, ts, twg, pr, nullptr);
+            }
+            __syncthreads();
+        }
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            const int J = J0 + j;
+            if (J >= l) break;
+            ulonglong2 kk[CG][2];  // the CG children's key words of digit J, both polys: independent loads
+#pragma unroll
+            for (int c2 = 0; c2 < CG; ++c2) {
+                if (c2 < nk) {
+                    const u64 *kp = ch.c[c2].key + (((u64)(J * 2) * K + kI) << logN) + kc[c2];
+                    kk[c2][0] = *(const ulonglong2 *)kp;
+                    kk[c2][1] = *(const ulonglong2 *)(kp + ((u64)K << logN));
+                } else {
+                    kk[c2][0] = kk[c2][1] = ulonglong2{0, 0};
+                }
+            }
+            const u64 cj = cji[J * K + kI];
+#pragma unroll
+            for (int tb = 0; tb < BT; ++tb) {
+                const int bb = bs * BT + tb;
+                if (bb >= nb) break;
+                const int tl = j * BG + bb;
+                u64 r0 = lds[addr_of(tl, 2 * pp)], r1 = lds[addr_of(tl, 2 * pp + 1)];
+                if constexpr (!FP) {
+                    if (J != I) {  // lazy [0, 4q) -> canonical
+                        r0 = csub(csub(r0, two_q), q);
+                        r1 = csub(csub(r1, two_q), q);
+                    }
+                }
+                int nz = 0;
+                const int *z = nullptr;
+                if (J != I && zeros) {
+                    z = zl + 1 + ((b0 + bb) * l + J) * (HEC_ZCAP + 1);
+                    nz = min(z[0], HEC_ZCAP);
+                }
+#pragma unroll
+                for (int c2 = 0; c2 < CG; ++c2) {
+                    if (c2 >= nk) break;
+                    u64 e0 = r0, e1 = r1;
+                    if (nz > 0) {  // the rare zero corrections of this child (output slots kc ^ sw, kc ^ !sw)
+                        if constexpr (FP) {
+                            e0 = fp_canon(__longlong_as_double((long long)e0), pr.qd, pr.qinv);
+                            e1 = fp_canon(__longlong_as_double((long long)e1), pr.qd, pr.qinv);
+                        }
+                        const u64 ko0 = kc[c2] | (u64)sw[c2], ko1 = kc[c2] | (u64)!sw[c2];
+                        const u32 elt = ch.c[c2].elt;
+                        for (int zi = 0; zi < nz; ++zi) {
+                            u64 tt2 = ((u64)z[1 + zi] * elt) & (2 * N - 1);
+                            if (tt2 < N) continue;
+                            tt2 -= N;
+                            const u64 ex0 = ((2 * (u64)bitrev((u32)ko0, logN) + 1) * tt2) & (2 * N - 1);
+                            const u64 ex1 = ((2 * (u64)bitrev((u32)ko1, logN) + 1) * tt2) & (2 * N - 1);
+                            e0 = submod(e0, mulmod(cj, pp_pow[ex0], pr), q);
+                            e1 = submod(e1, mulmod(cj, pp_pow[ex1], pr), q);
+                        }
+                        if constexpr (FP) {
+                            e0 = (u64)__double_as_longlong(u2d(e0));
+                            e1 = (u64)__double_as_longlong(u2d(e1));
+                        }
+                    }
+                    const ulonglong2 k0 = sw[c2] ? ulonglong2{kk[c2][0].y, kk[c2][0].x} : kk[c2][0];
+                    const ulonglong2 k1 = sw[c2] ? ulonglong2{kk[c2][1].y, kk[c2][1].x} : kk[c2][1];
+                    if constexpr (FP) {  // |e| < 10 q: the forward NTT's output before canonicalisation
+                        const double d0 = __longlong_as_double((long long)e0), d1 = __longlong_as_double((long long)e1);
+                        f[c2][tb][0] += fp_mulmod(d0, u2d(k0.x), pr.qd, pr.qinv);
+                        f[c2][tb][1] += fp_mulmod(d1, u2d(k0.y), pr.qd, pr.qinv);
+                        f[c2][tb][2] += fp_mulmod(d0, u2d(k1.x), pr.qd, pr.qinv);
+                        f[c2][tb][3] += fp_mulmod(d1, u2d(k1.y), pr.qd, pr.qinv);
+                    } else {
+                        mac128(a[c2][tb][0], e0, k0.x);
+                        mac128(a[c2][tb][1], e1, k0.y);
+                        mac128(a[c2][tb][2], e0, k1.x);
+                        mac128(a[c2][tb][3], e1, k1.y);
+                    }
+                }
+            }
+        }
+        __syncthreads();  // the next digits overwrite the tiles
+    }
+#pragma unroll
+    for (int c2 = 0; c2 < CG; ++c2) {
+        if (c2 >= nk) break;
+        const HChild &cc = ch.c[c2];
+#pragma unroll
+        for (int tb = 0; tb < BT; ++tb) {
+            const int bb = bs * BT + tb;
+            if (bb >= nb) break;
+            const int b = b0 + bb;
+            u64 r[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                if constexpr (FP) r[i] = fp_canon(f[c2][tb][i], pr.qd, pr.qinv);
+                else r[i] = barrett128(a[c2][tb][i].lo, a[c2][tb][i].hi, q, pr.r0, pr.r1);
+            }
+            u64 *o0 = cc.ACC + (((u64)((b * 2 + 0) * (l + 1) + I)) << logN) + kc[c2];
+            u64 *o1 = cc.ACC + (((u64)((b * 2 + 1) * (l + 1) + I)) << logN) + kc[c2];
+            *(ulonglong2 *)o0 = sw[c2] ? ulonglong2{r[1], r[0]} : ulonglong2{r[0], r[1]};
+            *(ulonglong2 *)o1 = sw[c2] ? ulonglong2{r[3], r[2]} : ulonglong2{r[2], r[3]};
+        }
+    }
+}
+
+template <int LOGP, int BGF, int BGI, int BS, int CG>
+__global__ void __launch_bounds__((1 << LOGP) / 2 * BS)
+    k_hfuse2(PolyArr X1, const u64 *__restrict__ E, const int *__restrict__ zl, const HFuseKids ch, int B, int l, int K,
+             int logN, const DevPrime *__restrict__ primes, TwTables tt, const int *__restrict__ Imap, int nI, int nint,
+             const u64 *__restrict__ cji, const u64 *__restrict__ psipow, int wsplit)
+{
+    constexpr int P = 1 << LOGP;
+    extern __shared__ u64 hfuse_lds[];  // [2 P] twiddles, then the staged tiles
+    u64 *ltw = hfuse_lds, *lds = hfuse_lds + 2 * P;
+    const int X = 1 << (logN - LOGP);
+    const bool integer = (int)blockIdx.x < wsplit;
+    const int bg = integer ? BGI : BGF, nbg = (B + bg - 1) / bg;
+    const int w = integer ? blockIdx.x : blockIdx.x - wsplit;
+    const int g8 = w & 7, rest = w >> 3, bgi = rest % nbg, G = (rest / nbg) * 8 + g8;
+    if (G >= X * (integer ? nint : nI - nint)) return;
+    const int yi = G / X + (integer ? 0 : nint), chunk = G % X;
+    const int I = Imap[yi];
+    const int kI = I == l ? K - 1 : I;
+    const DevPrime pr = primes[kI];
+    if (integer)
+        hfuse2_body<LOGP, BGI, BS, CG, false>(lds, ltw, X1, E, zl, ch, B, l, K, logN, pr, tt, I, kI, chunk, bgi * BGI, cji,
+                                              psipow);
+    else
+        hfuse2_body<LOGP, BGF, BS, CG, true>(lds, ltw, X1, E, zl, ch, B, l, K, logN, pr, tt, I, kI, chunk, bgi * BGF, cji,
+                                             psipow);
+}
+
+template <int LOGP, int BGF, int BGI, int BS, int CG>
+static void launch_hfuse2(Ctx &c, PolyArr X1, const u64 *E, const int *zl, const HChildSpec *kids, int nkids, int B,
+                          int l)
+{
+    constexpr int P = 1 << LOGP, THREADS = P / 2 * BS, CONC = THREADS / (P / 8);
+    for (int k0 = 0; k0 < nkids; k0 += CG) {  // CG children per launch
+        HFuseKids ch{};
+        ch.n = std::min(CG, nkids - k0);
+        for (int q = 0; q < ch.n; ++q) {
+            const HChildSpec &k = kids[k0 + q];
+            ch.c[q] = HChild{k.elt, k.einv, k.key, k.W, k.ACC, k.KW};
+        }
+        const int nint = c.imap_nint[l], X = (int)(c.N >> LOGP);
+        const int gI = (X * nint + 7) / 8 * 8, gF = (X * (l + 1 - nint) + 7) / 8 * 8;
+        const int wsplit = gI * ((B + BGI - 1) / BGI), total = wsplit + gF * ((B + BGF - 1) / BGF);
+        const int tiles = std::max(CONC / BGF, 1) * BGF > std::max(CONC / BGI, 1) * BGI ? std::max(CONC / BGF, 1) * BGF
+                                                                                         : std::max(CONC / BGI, 1) * BGI;
+        const std::size_t shm = (std::size_t)(2 * P + tiles * hfuse_ld(LOGP)) * sizeof(u64);
+        const TwTables fwd{c.tw, c.twb, c.twf, c.twbf};
+        k_hfuse2<LOGP, BGF, BGI, BS, CG><<<dim3((unsigned)total), THREADS, shm, c.stream>>>(
+            X1, E, zl, ch, B, l, (int)c.K, c.logN, c.primes, fwd, c.imap_at(l), l + 1, nint, c.cji, c.psipow, wsplit);
+        HEC_HIP(hipGetLastError());
+    }
+}
+
 void hoisted_mac_fused(Ctx &c, PolyArr X1, const u64 *E, const int *zl, const HChildSpec *kids, int nkids, int B, int l)
 {
     if (nkids < 1 || nkids > HFUSE_MAXK) throw std::invalid_argument("hoisted_mac_fused: children per launch");
     if (l > HEC_MAXL) throw std::invalid_argument("too many limbs");
+    if (c.hfuse == 2) {  // digit-outer k_hfuse2: <LOGP, FP64 batch tile, integer batch tile, batch sets, children>
+        switch (c.logN) {
+        case 10: case 11: launch_hfuse2<5, 4, 4, 4, 4>(c, X1, E, zl, kids, nkids, B, l); break;
+        case 12: case 13: launch_hfuse2<6, 4, 2, 2, 4>(c, X1, E, zl, kids, nkids, B, l); break;
+        case 14: case 15:
+            if (c.hfuse_cg == 2) launch_hfuse2<7, 4, 2, 2, 2>(c, X1, E, zl, kids, nkids, B, l);
+            else if (c.hfuse_bg == 2) launch_hfuse2<7, 2, 2, 2, 4>(c, X1, E, zl, kids, nkids, B, l);
+            else launch_hfuse2<7, 4, 2, 2, 4>(c, X1, E, zl, kids, nkids, B, l);
+            break;
+        case 16: launch_hfuse2<8, 2, 2, 2, 4>(c, X1, E, zl, kids, nkids, B, l); break;
+        default: throw std::invalid_argument("poly_modulus_degree must be 2^10 .. 2^16");
+        }
+        return;
+    }
     // <LOGP, batch entries per block, batch sets per block>: LDS = l BG hfuse_ld(LOGP) words (the largest static
     // shape is HEC_MAXL digits), blocks of P / 2 x BS threads
     switch (c.logN) {

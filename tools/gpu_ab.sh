@@ -1,22 +1,15 @@
 #!/bin/bash
-# A/B of engine switches: quick parity (test_gpu_parity.py), then one bench line per setting.
-# usage: bash tools/gpu_ab.sh <tag> "ENV=a ENV2=b" "ENV=c|--batch 128" ...   (text after | = bench.py arguments)
+# quick A/B: a few parity tests of the hoisted path, then the bench under each env setting given.
+# usage: bash tools/gpu_ab.sh <tag> "ENV=1 ENV2=3" "ENV=0" ...
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-TAG=$1; shift
-mkdir -p gpurun_out/$TAG
-timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread > gpurun_out/$TAG/parity.log 2>&1 || { tail -30 gpurun_out/$TAG/parity.log; exit 1; }
-tail -1 gpurun_out/$TAG/parity.log
+T=$1; shift
+mkdir -p gpurun_out/$T
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread -k "keyswitch_variants or hoisted or lane or cfg3_matvec or cfg5_params" > gpurun_out/$T/tests.log 2>&1 || { tail -30 gpurun_out/$T/tests.log; exit 1; }
+tail -2 gpurun_out/$T/tests.log
 i=0
-for cfg in "$@"; do
-  envs=${cfg%%|*}
-  args=""
-  [[ "$cfg" == *"|"* ]] && args=${cfg#*|}
-  env $envs timeout -k 10 300 python bench.py --no-cpu-baseline $args > gpurun_out/$TAG/b_$i.json 2> gpurun_out/$TAG/b_$i.err || { tail -20 gpurun_out/$TAG/b_$i.err; exit 1; }
-  python - "$cfg" gpurun_out/$TAG/b_$i.json <<'PY'
-import json, sys
-d = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1])
-print(sys.argv[1], d["value"], {k: v["ms"] for k, v in d["kernels_one_step"].items()})
-PY
+for e in "$@"; do
   i=$((i+1))
+  env $e timeout -k 10 300 python bench.py --no-cpu-baseline --steps 2 --warmup 1 > gpurun_out/$T/bench_$i.json 2> gpurun_out/$T/bench_$i.err || { tail gpurun_out/$T/bench_$i.err; exit 1; }
+  echo "$e: $(head -c 120 gpurun_out/$T/bench_$i.json)"
 done
