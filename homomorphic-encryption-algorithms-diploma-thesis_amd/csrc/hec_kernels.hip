@@ -2106,16 +2106,22 @@ __device__ __forceinline__ void bmac_body(u64 *lds, u64 *ltw, PolyArr T, const u
                                           u64 *__restrict__ ACC, const TwTables &tt, const DevPrime &pr, int I, int kI,
                                           int b, int xb, int logN, int l, int K, u32 elt)
 {
-    constexpr int P = 1 << LOGP, THREADS = NSEG * P / EPT, LD = bmac_ld(LOGP), TWS = 2 * P + 2;
+    // KEYM 3: keys as 1, with the segment-major lane layout below (lanes = consecutive threads of one chunk,
+    // stride P + P/8, one pad word per 16): the staging writes and the rounds' reads and writes at about half the
+    // bank-conflict cycles of the chunk-interleaved layout (tools/lds_banks.py)
+    constexpr bool LAY = KEYM == 3;
+    constexpr int KM = LAY ? 1 : KEYM;
+    constexpr int P = 1 << LOGP, THREADS = NSEG * P / EPT, LD = LAY ? P + P / 8 : bmac_ld(LOGP), TWS = 2 * P + 2;
     const u64 N = 1ull << logN;
     const int seg0 = xb * NSEG;
     const u64 base = (u64)seg0 << LOGP;
     const ulonglong2 *tw = tt.b + ((u64)kI << logN);
     const double *twf = tt.fb + ((u64)kI << logN);
-    const int ts = threadIdx.x / NSEG, sg = threadIdx.x % NSEG;
+    const int ts = LAY ? (int)threadIdx.x % (P / EPT) : (int)threadIdx.x / NSEG;
+    const int sg = LAY ? (int)threadIdx.x / (P / EPT) : (int)threadIdx.x % NSEG;
     // one pad word per 8 elements plus a segment stride of P + P/8 + 8: the three round access patterns
     // and the staging writes go from 4-way to <= 2-way LDS bank conflicts (64 banks, 32-lane halves)
-    auto addr = [sg](int x) { return sg * LD + x + (x >> 3); };
+    auto addr = [sg](int x) { return sg * LD + x + (LAY ? (x >> 4) : (x >> 3)); };
     const u64 R = 1ull << (logN - LOGP);
     // the pass-B twiddles of a chunk do not depend on the digit J: stage the block's (NSEG chunks x
     // (P - 1) entries) once into LDS, rows padded to TWS words (bank spread), lanes = consecutive chunks
@@ -2153,8 +2159,8 @@ __device__ __forceinline__ void bmac_body(u64 *lds, u64 *ltw, PolyArr T, const u
             k0[e] = a.x; k0[e + 1] = a.y; k1[e] = c.x; k1[e + 1] = c.y;
         }
     };
-    u64 kc0[KEYM == 2 ? EPT : 1], kc1[KEYM == 2 ? EPT : 1];
-    if constexpr (KEYM == 2) load_keys(0, kc0, kc1);
+    u64 kc0[KM == 2 ? EPT : 1], kc1[KM == 2 ? EPT : 1];
+    if constexpr (KM == 2) load_keys(0, kc0, kc1);
     // digit tiles move as 16-B pairs: pair w = threadIdx.x + e THREADS holds block elements 2w, 2w + 1
     u64 nx[EPT];
     auto load_tile = [&](int J) {
@@ -2187,16 +2193,16 @@ __device__ __forceinline__ void bmac_body(u64 *lds, u64 *ltw, PolyArr T, const u
             if constexpr (FP) {
                 if (!ntt) v = (u64)__double_as_longlong(u2d(v));  // canonical integer target
             }
-            lds[(li / P) * LD + (li % P) + ((li % P) >> 3)] = v;
+            lds[(li / P) * LD + (li % P) + (LAY ? ((li % P) >> 4) : ((li % P) >> 3))] = v;
         }
         if (J + 1 < l) load_tile(J + 1);
         u64 k0[EPT], k1[EPT];
-        if constexpr (KEYM == 2) {  // keys of digit J were loaded one iteration ago; issue J + 1's now
+        if constexpr (KM == 2) {  // keys of digit J were loaded one iteration ago; issue J + 1's now
 #pragma unroll
             for (int e = 0; e < EPT; ++e) { k0[e] = kc0[e]; k1[e] = kc1[e]; }
             if (J + 1 < l) load_keys(J + 1, kc0, kc1);
         }
-        if constexpr (KEYM == 1) load_keys(J, k0, k1);
+        if constexpr (KM == 1) load_keys(J, k0, k1);
         __syncthreads();
         u64 v[EPT];
         if (ntt) {
@@ -2216,7 +2222,7 @@ __device__ __forceinline__ void bmac_body(u64 *lds, u64 *ltw, PolyArr T, const u
 #pragma unroll
             for (int e = 0; e < EPT; ++e) v[e] = lds[addr(ts * EPT + e)];
         }
-        if constexpr (KEYM == 0) load_keys(J, k0, k1);
+        if constexpr (KM == 0) load_keys(J, k0, k1);
 #pragma unroll
         for (int e = 0; e < EPT; ++e) {
             if constexpr (FP) {
@@ -2339,9 +2345,10 @@ static void run_modup_fused(Ctx &c, const u64 *D, u64 *E, PolyArr T, const u64 *
         constexpr int CL = decltype(cls)::value;
         const int gpad = (X * nI + 7) / 8 * 8;
         const dim3 grid(gpad * B);
-        switch (c.bmac_keys) {  // key loads: 0 after the rounds, 1 before them, 2 one digit ahead
+        switch (c.bmac_keys) {  // key loads: 0 after the rounds, 1 before them, 2 one digit ahead; 3 = 1 + LDS layout
         case 0: k_bmac<LOGC, NB2, EPT, 0, CL><<<grid, TB, 0, st>>>(T, E, key, ACC, fwd, c.primes, Il, nI, c.logN, l, (int)c.K, nint, gpad, elt); break;
         case 1: k_bmac<LOGC, NB2, EPT, 1, CL><<<grid, TB, 0, st>>>(T, E, key, ACC, fwd, c.primes, Il, nI, c.logN, l, (int)c.K, nint, gpad, elt); break;
+        case 3: k_bmac<LOGC, NB2, EPT, 3, CL><<<grid, TB, 0, st>>>(T, E, key, ACC, fwd, c.primes, Il, nI, c.logN, l, (int)c.K, nint, gpad, elt); break;
         default: k_bmac<LOGC, NB2, EPT, 2, CL><<<grid, TB, 0, st>>>(T, E, key, ACC, fwd, c.primes, Il, nI, c.logN, l, (int)c.K, nint, gpad, elt); break;
         }
     };
