@@ -54,13 +54,14 @@ def algorithmic_bytes_per_matvec(N, l, n, B, ks):
 
 def pmc_traffic(kernel, B, logn, level, n):
     """HBM bytes per launch of the roofline kernel from the committed rocprofv3 PMC passes
-    (profiles/r02_pmc_<kernel>_B<B>.json, else r01_; written by tools/pmc_summary.py: FETCH_SIZE and WRITE_SIZE in
+    (profiles/r03_pmc_<kernel>_B<B>.json, else r02_ / r01_; written by tools/pmc_summary.py: FETCH_SIZE and WRITE_SIZE in
     separate passes, gfx950 FETCH x2 correction for 16-B/lane reads) when they were taken on this
     configuration; else None."""
-    path = os.path.join(ROOT, "profiles", f"r02_pmc_{kernel}_B{B}.json")
-    if not os.path.exists(path):
-        path = os.path.join(ROOT, "profiles", f"r01_pmc_{kernel}_B{B}.json")
-    if not os.path.exists(path):
+    for tag in ("r03", "r02", "r01"):  # the newest round's pass for this kernel
+        path = os.path.join(ROOT, "profiles", f"{tag}_pmc_{kernel}_B{B}.json")
+        if os.path.exists(path):
+            break
+    else:
         return None
     p = json.load(open(path))
     if (p["batch"], p["logN"], p["level"], p.get("n")) != (B, logn, level, n):

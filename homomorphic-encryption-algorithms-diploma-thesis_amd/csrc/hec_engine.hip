@@ -431,7 +431,7 @@ void keyswitch(Ctx &c, Scratch &s, PolyArr T, const u64 *key, PolyArr IN, int in
         {  // digits E (B l^2) + the I == J targets (B l) + key (2 l K) -> ACC (2 B K)
             ProfScope ps(c, "ks_bmac");
             ProfScope k(c, "k:k_bmac", (double)B * l * l + (double)B * l + 2.0 * l * K + 2.0 * B * K,
-                        c.split_classes ? 2 : 1);
+                        1);
             ks_modup_mac(c, D, E, T, key, ACC, B, l, 2, elt);
         }
     } else {
@@ -989,7 +989,7 @@ void matvec_core(hec_context *ctx, const hec_ciphertext *const *diags, const hec
 // cycles), so the batch of a matvec is split into up to c.lanes sub-batches of at least
 // c.lane_min_batch vectors that run the same trie walk concurrently, each from its own host thread on its
 // own HIP stream and workspace.  Outputs are independent per input vector, so the bits are unchanged.
-hec_context *make_lane(hec_context *parent, int index)
+hec_context *make_lane(hec_context *parent)
 {
     auto *l = new hec_context();
     Ctx &c = l->c;
@@ -1004,19 +1004,7 @@ hec_context *make_lane(hec_context *parent, int index)
     c.stream = c.side = nullptr;
     c.ev_fork = c.ev_join = nullptr;
     c.zflag = nullptr;
-    if (c.lane_cumask != 0 && c.lanes > 1) {  // the lane's own share of the CUs
-        hipDeviceProp_t prop;
-        HEC_HIP(hipGetDeviceProperties(&prop, c.device));
-        const int ncu = prop.multiProcessorCount, n = c.lanes, i = index % n;
-        std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
-        for (int cu = 0; cu < ncu; ++cu) {
-            const bool mine = c.lane_cumask == 1 ? cu % n == i : (cu % 32) * n / 32 == i;
-            if (mine) mask[cu / 32] |= 1u << (cu % 32);
-        }
-        HEC_HIP(hipExtStreamCreateWithCUMask(&c.stream, (uint32_t)mask.size(), mask.data()));
-    } else {
-        HEC_HIP(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
-    }
+    HEC_HIP(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
     c.own_stream = true;
     HEC_HIP(hipStreamCreateWithFlags(&c.side, hipStreamNonBlocking));
     HEC_HIP(hipEventCreateWithFlags(&c.ev_fork, hipEventDisableTiming));
@@ -1067,7 +1055,7 @@ void matvec_lanes(hec_context *ctx, const hec_ciphertext *const *diags, const he
             ensure(out[i], w);
         }
     }
-    while ((int)ctx->lanes.size() < nl) ctx->lanes.push_back(make_lane(ctx, (int)ctx->lanes.size()));
+    while ((int)ctx->lanes.size() < nl) ctx->lanes.push_back(make_lane(ctx));
     if (!ctx->lanes_start) HEC_HIP(hipEventCreateWithFlags(&ctx->lanes_start, hipEventDisableTiming));
     hipEvent_t start = ctx->lanes_start;
     HEC_HIP(hipEventRecord(start, c.stream));  // the inputs were produced on the context's stream
@@ -1308,14 +1296,12 @@ int hec_context_create(uint64_t N, const uint64_t *mod, uint64_t K, int device, 
         if (const char *f = std::getenv("HEC_DIVROUND_FP")) c.divround_fp = std::atoi(f);
         if (const char *f = std::getenv("HEC_TENSOR_BG")) c.tensor_bg = std::atoi(f);
         if (const char *f = std::getenv("HEC_LANES")) c.lanes = std::max(1, std::atoi(f));
-        if (const char *f = std::getenv("HEC_LANE_CUMASK")) c.lane_cumask = std::atoi(f);
         if (const char *f = std::getenv("HEC_FANG"))
             std::sscanf(f, "%d,%d,%d", &c.fan_groups_moddown, &c.fan_groups_modup, &c.fan_groups_hoist);
         if (const char *f = std::getenv("HEC_HOIST")) c.hoist = f[0] != '0';
         if (const char *f = std::getenv("HEC_HMAC")) c.hmac_cfg = std::atoi(f);
         if (const char *f = std::getenv("HEC_HMAC_ODD3")) c.hmac_odd3 = std::atoi(f);
         if (const char *f = std::getenv("HEC_HOIST_MIN")) c.hoist_min_children = std::max(1, std::atoi(f));
-        if (const char *f = std::getenv("HEC_SPLIT_CLASSES")) c.split_classes = f[0] - '0';
         if (const char *f = std::getenv("HEC_TENSOR_DEFER")) c.tensor_defer_max = std::max(1, std::atoi(f));
         if (const char *f = std::getenv("HEC_TENSOR_BUFS")) c.tensor_defer_bufs = std::max(1, std::atoi(f));
         c.N = N;

@@ -85,15 +85,13 @@ struct Ctx {
     std::vector<u64> p_inv, p_inv_q, p_half_mod;            // key switch mod-down (per data prime)
     std::vector<std::vector<u64>> ql_inv, ql_inv_q, ql_half_mod;  // rescale at level l (drop prime l-1)
     int bmac_keys = 1;             // HEC_BMAC_KEYS: k_bmac key loads 0 late / 1 before the rounds / 2 one digit ahead
-    int split_classes = 0;         // HEC_SPLIT_CLASSES: mod-up A / k_bmac as one mixed launch (0), FP64 and
-                                   // integer launches on one stream (1) or on two streams (2)
     int tensor_defer_max = 12;     // HEC_TENSOR_DEFER: terminals per deferred tensor batch (1 = immediate)
     int tensor_defer_bufs = 8;     // HEC_TENSOR_BUFS: rotation buffers per trie depth
     int tensor_bg = 1;             // HEC_TENSOR_BG=0: k_tensor_multi (one thread per coefficient, whole batch)
     bool hoist = true;             // HEC_HOIST=0: no hoisted mod-up in the rotation trie walk
-    int hoist_min_children = 2;
+    int hoist_min_children = 2;    // HEC_HOIST_MIN: children a trie node needs to be hoisted
     int hmac_cfg = 3;              // HEC_HMAC: 0 one hoisted MAC per child; siblings fused: 1 (4 x 1 batch),
-                                   // 2 (2 x 2), 3 (2 x 4, default), 4 (3 x 2) children x batch entries per thread    // HEC_HOIST_MIN: children a trie node needs to be hoisted
+                                   // 2 (2 x 2), 3 (2 x 4, default), 4 (3 x 2) children x batch entries per thread
     int fan_groups_moddown = 1;    // HEC_FANG="moddown,modup,hoist": target groups per k_fan source (blocks
     int fan_groups_modup = 1;      // per launch x groups; the source's inverse pass is repeated per group)
     int fan_groups_hoist = 1;
@@ -111,9 +109,6 @@ struct Ctx {
     bool fan_out = true;           // HEC_FAN=0: separate INTT pass A (fan-out fuses it into the forward passes A)
     int lanes = 3;                 // HEC_LANES: concurrent batch lanes of a matvec (hec_engine.hip matvec_lanes)
     int lane_min_batch = 16;       // input vectors per lane at least
-    int lane_cumask = 0;           // HEC_LANE_CUMASK: 0 lanes share every CU; 1 lane i of n owns the CUs with
-                                   // index % n == i; 2 a contiguous range of every 32 (hipExtStreamCreateWithCUMask; either
-                                   // way each lane keeps CUs on all 8 XCDs)
     bool fuse_galois = true;       // HEC_FUSE_GALOIS=0: materialise apply_galois before the key switch
     bool fused_modup_mac = true;  // HEC_FUSED_MODUP_MAC=0: separate mod-up pass B and key MAC kernels
     // profiling (ProfScope in hec_engine.hip)

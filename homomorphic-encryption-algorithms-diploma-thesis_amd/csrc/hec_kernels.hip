@@ -2284,25 +2284,6 @@ __global__ void __launch_bounds__(NSEG *(1 << LOGP) / EPT)
         bmac_body<LOGP, NSEG, EPT, true, KEYM>(lds, ltw, T, E, key, ACC, tt, pr, I, kI, b, xb, logN, l, K, elt);
 }
 
-// fork -> (integer-class launch on the side stream) || (FP64-class launch on the main stream) -> join,
-// or both in order on the main stream
-template <class FI, class FF>
-static void dual(Ctx &c, bool two_streams, const FI &launch_int, const FF &launch_fp)
-{
-    if (two_streams) {
-        HEC_HIP(hipEventRecord(c.ev_fork, c.stream));
-        HEC_HIP(hipStreamWaitEvent(c.side, c.ev_fork, 0));
-        launch_int(c.side);
-        HEC_HIP(hipEventRecord(c.ev_join, c.side));
-        launch_fp(c.stream);
-        HEC_HIP(hipStreamWaitEvent(c.stream, c.ev_join, 0));
-    } else {
-        launch_int(c.stream);
-        launch_fp(c.stream);
-    }
-    HEC_HIP(hipGetLastError());
-}
-
 template <int LOGR, int LOGC, int NA, int NB2>
 static void run_modup_fused(Ctx &c, const u64 *D, u64 *E, PolyArr T, const u64 *key, u64 *ACC, int B, int l,
                             int part, u32 elt)
@@ -2310,29 +2291,12 @@ static void run_modup_fused(Ctx &c, const u64 *D, u64 *E, PolyArr T, const u64 *
     constexpr int R = 1 << LOGR, C = 1 << LOGC, EPT = 8;
     const TwTables fwd{c.tw, c.twb, c.twf, c.twbf};
     // (2a) pass A of every mod-up NTT (B * l * l jobs), output E[b][I][J] (lazy, pass-A domain)
-    const int nint = c.imap_nint[l], nfp = l + 1 - nint;
+    const int nint = c.imap_nint[l];
     const int *dm = c.imap_at(l);
-    const bool split = c.split_classes != 0 && nint > 0 && nfp > 0;
     if (part & 1) {
-        if (!split) {
-            ModUpMap m{l, c.logN, (int)c.K - 1};
-            k_ntt<LOGR, NA, false, true, false><<<dim3(C / NA, B * l * l), NA * R / 16, 0, c.stream>>>(
-                ModUpIO_A{m, D, E, c.primes}, fwd, c.primes, c.logN);
-        } else {
-            const ModUpMap mi{l, c.logN, (int)c.K - 1, dm, nint}, mf{l, c.logN, (int)c.K - 1, dm + nint, nfp};
-            dual(
-                c, c.split_classes == 2,
-                [&](hipStream_t st) {
-                    k_ntt<LOGR, NA, false, true, false, ModUpIO_A, 2><<<dim3(C / NA, B * nint * l), NA * R / 16, 0,
-                                                                         st>>>(ModUpIO_A{mi, D, E, c.primes}, fwd,
-                                                                               c.primes, c.logN);
-                },
-                [&](hipStream_t st) {
-                    k_ntt<LOGR, NA, false, true, false, ModUpIO_A, 1><<<dim3(C / NA, B * nfp * l), NA * R / 16, 0,
-                                                                         st>>>(ModUpIO_A{mf, D, E, c.primes}, fwd,
-                                                                               c.primes, c.logN);
-                });
-        }
+        ModUpMap m{l, c.logN, (int)c.K - 1};
+        k_ntt<LOGR, NA, false, true, false><<<dim3(C / NA, B * l * l), NA * R / 16, 0, c.stream>>>(
+            ModUpIO_A{m, D, E, c.primes}, fwd, c.primes, c.logN);
     }
     if (!(part & 2)) {
         HEC_HIP(hipGetLastError());
@@ -2352,11 +2316,7 @@ static void run_modup_fused(Ctx &c, const u64 *D, u64 *E, PolyArr T, const u64 *
         default: k_bmac<LOGC, NB2, EPT, 2, CL><<<grid, TB, 0, st>>>(T, E, key, ACC, fwd, c.primes, Il, nI, c.logN, l, (int)c.K, nint, gpad, elt); break;
         }
     };
-    if (!split) launch(std::integral_constant<int, 0>{}, c.stream, dm, l + 1);
-    else
-        dual(
-            c, c.split_classes == 2, [&](hipStream_t st) { launch(std::integral_constant<int, 2>{}, st, dm, nint); },
-            [&](hipStream_t st) { launch(std::integral_constant<int, 1>{}, st, dm + nint, nfp); });
+    launch(std::integral_constant<int, 0>{}, c.stream, dm, l + 1);
     HEC_HIP(hipGetLastError());
 }
 

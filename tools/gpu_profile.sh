@@ -14,7 +14,7 @@ tail -1 $OUT/bench.json | cut -c1-600
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -T --output-format csv -d $OUT/trace -o run -- python3 $GRAFT_REPO_ROOT/bench.py --no-cpu-baseline > $OUT/trace_bench.json 2> $OUT/trace.log || { tail $OUT/trace.log; exit 1; }
 PMCARGS="--no-cpu-baseline --no-profile --steps 1 --warmup 0"
-KRE="k_fan|k_ntt|k_hmacm|k_bmac|k_tensor_multi"
+KRE="k_fan|k_ntt|k_hmacm|k_hfuse|k_bmac|k_tensor_multi"
 # one lane: each dispatch covers the whole batch, as in bench.py's event-timed profile step
 export HEC_LANES=1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$KRE" --output-format csv -d $OUT/pmc_fetch -o run -- python3 $GRAFT_REPO_ROOT/bench.py $PMCARGS > $OUT/pmc_fetch.log 2>&1 || { tail $OUT/pmc_fetch.log; exit 1; }
@@ -22,5 +22,5 @@ timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$KRE" --out
 cd $GRAFT_REPO_ROOT
 python tools/profile_step.py $OUT/trace/run_kernel_trace.csv $OUT/trace_bench.json $OUT/profile_step.json || exit 1
 cp $OUT/pmc_fetch/run_counter_collection.csv $OUT/pmc_fetch.csv && cp $OUT/pmc_write/run_counter_collection.csv $OUT/pmc_write.csv
-python tools/pmc_summary.py $OUT/pmc_fetch.csv $OUT/pmc_write.csv 96 15 10 4096 $TAG "HEC_LANES=1 rocprofv3 --pmc FETCH_SIZE (then WRITE_SIZE, separate pass) --kernel-include-regex '$KRE' -- python3 bench.py $PMCARGS" k_fan2 k_ntt k_hmacm k_bmac k_tensor_multi2 > /dev/null || exit 1
+python tools/pmc_summary.py $OUT/pmc_fetch.csv $OUT/pmc_write.csv 96 15 10 4096 $TAG "HEC_LANES=1 rocprofv3 --pmc FETCH_SIZE (then WRITE_SIZE, separate pass) --kernel-include-regex '$KRE' -- python3 bench.py $PMCARGS" k_fan2 k_ntt k_hmacm k_hfuse2 k_hfuse k_bmac k_tensor_multi2 > /dev/null || exit 1
 ls $OUT
