@@ -484,7 +484,7 @@ Hoist hoist_alloc(const Ctx &c, Scratch &s, int B, int l, int cap)
 // k_hfuse's LDS for level l fits a block (64 KiB of dynamic LDS): otherwise the per-pair path
 bool hfuse_fits(const Ctx &c, int l)
 {
-    if (c.hfuse == 2) return true;  // k_hfuse2 stages a few digits at a time
+    if (c.hfuse >= 2) return true;  // k_hfuse2 stages a few digits at a time
     const int logp = c.logN - c.logR, bg = c.logN == 15 ? c.hfuse_bg : c.logN <= 13 ? 4 : c.logN == 14 ? 2 : 1;
     const std::size_t words = 2 * ((std::size_t)1 << logp) + (std::size_t)l * bg * (((1 << logp) + (1 << logp) / 8 + 8));
     return c.hfuse && words * sizeof(u64) <= 65536;

@@ -1309,7 +1309,6 @@ __device__ __forceinline__ void hmacm_body(PolyArr X1, const u64 *__restrict__ E
                 dv[t][1] = u2d(v.y);
             }
         }
-        const u64 cj = cji[J * K + kI];
 #pragma unroll
         for (int q = 0; q < CG; ++q) {
             if (q >= ch.n) break;
@@ -1322,30 +1321,11 @@ __device__ __forceinline__ void hmacm_body(PolyArr X1, const u64 *__restrict__ E
 #pragma unroll
             for (int t = 0; t < BT; ++t) {
                 if (b0 + t >= B) break;
-                u64 e0 = ev[t][0], e1 = ev[t][1];
+                const u64 e0 = ev[t][0], e1 = ev[t][1];
                 double d0 = 0, d1 = 0;
                 if constexpr (FP) {
                     d0 = dv[t][0];
                     d1 = dv[t][1];
-                }
-                if (J != I && zeros) {  // output slots (in source order) of this child: kc ^ sw, kc ^ !sw
-                    const u64 ko0 = kc[q] | (u64)sw[q], ko1 = kc[q] | (u64)!sw[q];
-                    const int *z = zl + 1 + ((b0 + t) * l + J) * (HEC_ZCAP + 1);
-                    const int nz = min(z[0], HEC_ZCAP);
-                    const u64 N = 1ull << logN;
-                    for (int zi = 0; zi < nz; ++zi) {
-                        u64 tt = ((u64)z[1 + zi] * ch.c[q].elt) & (2 * N - 1);
-                        if (tt < N) continue;
-                        tt -= N;
-                        const u64 ex0 = ((2 * (u64)bitrev((u32)ko0, logN) + 1) * tt) & (2 * N - 1);
-                        const u64 ex1 = ((2 * (u64)bitrev((u32)ko1, logN) + 1) * tt) & (2 * N - 1);
-                        e0 = submod(e0, mulmod(cj, pp[ex0], pr), pr.q);
-                        e1 = submod(e1, mulmod(cj, pp[ex1], pr), pr.q);
-                    }
-                    if constexpr (FP) {
-                        d0 = u2d(e0);
-                        d1 = u2d(e1);
-                    }
                 }
                 if constexpr (FP) {
                     f[q][t][0] += fp_mulmod(d0, u2d(k0.x), pr.qd, pr.qinv);
@@ -1357,6 +1337,54 @@ __device__ __forceinline__ void hmacm_body(PolyArr X1, const u64 *__restrict__ E
                     mac128(a[q][t][1], e1, k0.y);
                     mac128(a[q][t][2], e0, k1.x);
                     mac128(a[q][t][3], e1, k1.y);
+                }
+            }
+        }
+    }
+    if (zeros) {  // the rare zero corrections (only zeros of D_J that a child negates), after the digit loop as
+                  // + (q - corr) key_J at the child's output slots kc ^ sw, kc ^ !sw: the MAC is linear, every term exact
+        const u64 N = 1ull << logN;
+        for (int J = 0; J < l; ++J) {
+            if (J == I) continue;
+            const u64 cj = cji[J * K + kI];
+#pragma unroll
+            for (int t = 0; t < BT; ++t) {
+                if (b0 + t >= B) break;
+                const int *z = zl + 1 + ((b0 + t) * l + J) * (HEC_ZCAP + 1);
+                const int nz = min(z[0], HEC_ZCAP);
+                if (nz == 0) continue;
+                for (int q = 0; q < CG; ++q) {
+                    if (q >= ch.n) break;
+                    const u64 ko0 = kc[q] | (u64)sw[q], ko1 = kc[q] | (u64)!sw[q];
+                    u64 c0 = 0, c1 = 0;
+                    for (int zi = 0; zi < nz; ++zi) {
+                        u64 tt = ((u64)z[1 + zi] * ch.c[q].elt) & (2 * N - 1);
+                        if (tt < N) continue;
+                        tt -= N;
+                        const u64 ex0 = ((2 * (u64)bitrev((u32)ko0, logN) + 1) * tt) & (2 * N - 1);
+                        const u64 ex1 = ((2 * (u64)bitrev((u32)ko1, logN) + 1) * tt) & (2 * N - 1);
+                        c0 = addmod(c0, mulmod(cj, pp[ex0], pr), pr.q);
+                        c1 = addmod(c1, mulmod(cj, pp[ex1], pr), pr.q);
+                    }
+                    if (c0 == 0 && c1 == 0) continue;
+                    const u64 n0 = c0 ? pr.q - c0 : 0, n1 = c1 ? pr.q - c1 : 0;
+                    const u64 *kp = ch.c[q].key + (((u64)(J * 2) * K + kI) << logN) + kc[q];
+                    ulonglong2 k0 = *(const ulonglong2 *)kp, k1 = *(const ulonglong2 *)(kp + ((u64)K << logN));
+                    if (sw[q]) {
+                        k0 = ulonglong2{k0.y, k0.x};
+                        k1 = ulonglong2{k1.y, k1.x};
+                    }
+                    if constexpr (FP) {
+                        f[q][t][0] += fp_mulmod(u2d(n0), u2d(k0.x), pr.qd, pr.qinv);
+                        f[q][t][1] += fp_mulmod(u2d(n1), u2d(k0.y), pr.qd, pr.qinv);
+                        f[q][t][2] += fp_mulmod(u2d(n0), u2d(k1.x), pr.qd, pr.qinv);
+                        f[q][t][3] += fp_mulmod(u2d(n1), u2d(k1.y), pr.qd, pr.qinv);
+                    } else {
+                        mac128(a[q][t][0], n0, k0.x);
+                        mac128(a[q][t][1], n1, k0.y);
+                        mac128(a[q][t][2], n0, k1.x);
+                        mac128(a[q][t][3], n1, k1.y);
+                    }
                 }
             }
         }
@@ -1894,7 +1922,6 @@ __device__ __forceinline__ void hfuse2_body(u64 *lds, u64 *ltw, PolyArr X1, cons
                     kk[c2][0] = kk[c2][1] = ulonglong2{0, 0};
                 }
             }
-            const u64 cj = cji[J * K + kI];
 #pragma unroll
             for (int tb = 0; tb < BT; ++tb) {
                 const int bb = bs * BT + tb;
@@ -1907,37 +1934,10 @@ __device__ __forceinline__ void hfuse2_body(u64 *lds, u64 *ltw, PolyArr X1, cons
                         r1 = csub(csub(r1, two_q), q);
                     }
                 }
-                int nz = 0;
-                const int *z = nullptr;
-                if (J != I && zeros) {
-                    z = zl + 1 + ((b0 + bb) * l + J) * (HEC_ZCAP + 1);
-                    nz = min(z[0], HEC_ZCAP);
-                }
 #pragma unroll
                 for (int c2 = 0; c2 < CG; ++c2) {
                     if (c2 >= nk) break;
-                    u64 e0 = r0, e1 = r1;
-                    if (nz > 0) {  // the rare zero corrections of this child (output slots kc ^ sw, kc ^ !sw)
-                        if constexpr (FP) {
-                            e0 = fp_canon(__longlong_as_double((long long)e0), pr.qd, pr.qinv);
-                            e1 = fp_canon(__longlong_as_double((long long)e1), pr.qd, pr.qinv);
-                        }
-                        const u64 ko0 = kc[c2] | (u64)sw[c2], ko1 = kc[c2] | (u64)!sw[c2];
-                        const u32 elt = ch.c[c2].elt;
-                        for (int zi = 0; zi < nz; ++zi) {
-                            u64 tt2 = ((u64)z[1 + zi] * elt) & (2 * N - 1);
-                            if (tt2 < N) continue;
-                            tt2 -= N;
-                            const u64 ex0 = ((2 * (u64)bitrev((u32)ko0, logN) + 1) * tt2) & (2 * N - 1);
-                            const u64 ex1 = ((2 * (u64)bitrev((u32)ko1, logN) + 1) * tt2) & (2 * N - 1);
-                            e0 = submod(e0, mulmod(cj, pp_pow[ex0], pr), q);
-                            e1 = submod(e1, mulmod(cj, pp_pow[ex1], pr), q);
-                        }
-                        if constexpr (FP) {
-                            e0 = (u64)__double_as_longlong(u2d(e0));
-                            e1 = (u64)__double_as_longlong(u2d(e1));
-                        }
-                    }
+                    const u64 e0 = r0, e1 = r1;
                     const ulonglong2 k0 = sw[c2] ? ulonglong2{kk[c2][0].y, kk[c2][0].x} : kk[c2][0];
                     const ulonglong2 k1 = sw[c2] ? ulonglong2{kk[c2][1].y, kk[c2][1].x} : kk[c2][1];
                     if constexpr (FP) {  // |e| < 10 q: the forward NTT's output before canonicalisation
@@ -1956,6 +1956,55 @@ __device__ __forceinline__ void hfuse2_body(u64 *lds, u64 *ltw, PolyArr X1, cons
             }
         }
         __syncthreads();  // the next digits overwrite the tiles
+    }
+    if (zeros) {  // the rare zero corrections: e_J - corr at the child's output slots (kc ^ sw, kc ^ !sw), applied
+                  // after the digit loop as + (q - corr) key_J (the MAC is linear, every term exact mod q)
+        for (int J = 0; J < l; ++J) {
+            if (J == I) continue;
+            const u64 cj = cji[J * K + kI];
+#pragma unroll
+            for (int tb = 0; tb < BT; ++tb) {
+                const int bb = bs * BT + tb;
+                if (bb >= nb) break;
+                const int *z = zl + 1 + ((b0 + bb) * l + J) * (HEC_ZCAP + 1);
+                const int nz = min(z[0], HEC_ZCAP);
+                if (nz == 0) continue;
+                for (int c2 = 0; c2 < CG; ++c2) {
+                    if (c2 >= nk) break;
+                    const u64 ko0 = kc[c2] | (u64)sw[c2], ko1 = kc[c2] | (u64)!sw[c2];
+                    const u32 elt = ch.c[c2].elt;
+                    u64 c0 = 0, c1 = 0;
+                    for (int zi = 0; zi < nz; ++zi) {
+                        u64 tt2 = ((u64)z[1 + zi] * elt) & (2 * N - 1);
+                        if (tt2 < N) continue;
+                        tt2 -= N;
+                        const u64 ex0 = ((2 * (u64)bitrev((u32)ko0, logN) + 1) * tt2) & (2 * N - 1);
+                        const u64 ex1 = ((2 * (u64)bitrev((u32)ko1, logN) + 1) * tt2) & (2 * N - 1);
+                        c0 = addmod(c0, mulmod(cj, pp_pow[ex0], pr), q);
+                        c1 = addmod(c1, mulmod(cj, pp_pow[ex1], pr), q);
+                    }
+                    if (c0 == 0 && c1 == 0) continue;
+                    const u64 n0 = c0 ? q - c0 : 0, n1 = c1 ? q - c1 : 0;
+                    const u64 *kp = ch.c[c2].key + (((u64)(J * 2) * K + kI) << logN) + kc[c2];
+                    ulonglong2 k0 = *(const ulonglong2 *)kp, k1 = *(const ulonglong2 *)(kp + ((u64)K << logN));
+                    if (sw[c2]) {
+                        k0 = ulonglong2{k0.y, k0.x};
+                        k1 = ulonglong2{k1.y, k1.x};
+                    }
+                    if constexpr (FP) {
+                        f[c2][tb][0] += fp_mulmod(u2d(n0), u2d(k0.x), pr.qd, pr.qinv);
+                        f[c2][tb][1] += fp_mulmod(u2d(n1), u2d(k0.y), pr.qd, pr.qinv);
+                        f[c2][tb][2] += fp_mulmod(u2d(n0), u2d(k1.x), pr.qd, pr.qinv);
+                        f[c2][tb][3] += fp_mulmod(u2d(n1), u2d(k1.y), pr.qd, pr.qinv);
+                    } else {
+                        mac128(a[c2][tb][0], n0, k0.x);
+                        mac128(a[c2][tb][1], n1, k0.y);
+                        mac128(a[c2][tb][2], n0, k1.x);
+                        mac128(a[c2][tb][3], n1, k1.y);
+                    }
+                }
+            }
+        }
     }
 #pragma unroll
     for (int c2 = 0; c2 < CG; ++c2) {
@@ -1980,7 +2029,9 @@ __device__ __forceinline__ void hfuse2_body(u64 *lds, u64 *ltw, PolyArr X1, cons
     }
 }
 
-template <int LOGP, int BGF, int BGI, int BS, int CG>
+// CLS 0: both segments in one launch; 1: an FP64-only launch over Imap[nint, nI); 2: an integer-only launch
+// (separate launches give the FP64 kernel its own register budget)
+template <int LOGP, int BGF, int BGI, int BS, int CG, int CLS = 0>
 __global__ void __launch_bounds__((1 << LOGP) / 2 * BS)
     k_hfuse2(PolyArr X1, const u64 *__restrict__ E, const int *__restrict__ zl, const HFuseKids ch, int B, int l, int K,
              int logN, const DevPrime *__restrict__ primes, TwTables tt, const int *__restrict__ Imap, int nI, int nint,
@@ -1990,16 +2041,22 @@ __global__ void __launch_bounds__((1 << LOGP) / 2 * BS)
     extern __shared__ u64 hfuse_lds[];  // [2 P] twiddles, then the staged tiles
     u64 *ltw = hfuse_lds, *lds = hfuse_lds + 2 * P;
     const int X = 1 << (logN - LOGP);
-    const bool integer = (int)blockIdx.x < wsplit;
+    const bool integer = CLS == 2 || (CLS == 0 && (int)blockIdx.x < wsplit);
     const int bg = integer ? BGI : BGF, nbg = (B + bg - 1) / bg;
-    const int w = integer ? blockIdx.x : blockIdx.x - wsplit;
+    const int w = (integer || CLS == 1) ? blockIdx.x : blockIdx.x - wsplit;
     const int g8 = w & 7, rest = w >> 3, bgi = rest % nbg, G = (rest / nbg) * 8 + g8;
     if (G >= X * (integer ? nint : nI - nint)) return;
     const int yi = G / X + (integer ? 0 : nint), chunk = G % X;
     const int I = Imap[yi];
     const int kI = I == l ? K - 1 : I;
     const DevPrime pr = primes[kI];
-    if (integer)
+    if constexpr (CLS == 2)
+        hfuse2_body<LOGP, BGI, BS, CG, false>(lds, ltw, X1, E, zl, ch, B, l, K, logN, pr, tt, I, kI, chunk, bgi * BGI, cji,
+                                              psipow);
+    else if constexpr (CLS == 1)
+        hfuse2_body<LOGP, BGF, BS, CG, true>(lds, ltw, X1, E, zl, ch, B, l, K, logN, pr, tt, I, kI, chunk, bgi * BGF, cji,
+                                             psipow);
+    else if (integer)
         hfuse2_body<LOGP, BGI, BS, CG, false>(lds, ltw, X1, E, zl, ch, B, l, K, logN, pr, tt, I, kI, chunk, bgi * BGI, cji,
                                               psipow);
     else
@@ -2026,8 +2083,17 @@ static void launch_hfuse2(Ctx &c, PolyArr X1, const u64 *E, const int *zl, const
                                                                                          : std::max(CONC / BGI, 1) * BGI;
         const std::size_t shm = (std::size_t)(2 * P + tiles * hfuse_ld(LOGP)) * sizeof(u64);
         const TwTables fwd{c.tw, c.twb, c.twf, c.twbf};
-        k_hfuse2<LOGP, BGF, BGI, BS, CG><<<dim3((unsigned)total), THREADS, shm, c.stream>>>(
-            X1, E, zl, ch, B, l, (int)c.K, c.logN, c.primes, fwd, c.imap_at(l), l + 1, nint, c.cji, c.psipow, wsplit);
+        if (c.hfuse == 3) {  // the integer and FP64 segments as two launches
+            if (wsplit)
+                k_hfuse2<LOGP, BGF, BGI, BS, CG, 2><<<dim3((unsigned)wsplit), THREADS, shm, c.stream>>>(
+                    X1, E, zl, ch, B, l, (int)c.K, c.logN, c.primes, fwd, c.imap_at(l), l + 1, nint, c.cji, c.psipow,
+                    wsplit);
+            k_hfuse2<LOGP, BGF, BGI, BS, CG, 1><<<dim3((unsigned)(total - wsplit)), THREADS, shm, c.stream>>>(
+                X1, E, zl, ch, B, l, (int)c.K, c.logN, c.primes, fwd, c.imap_at(l), l + 1, nint, c.cji, c.psipow, wsplit);
+        } else {
+            k_hfuse2<LOGP, BGF, BGI, BS, CG><<<dim3((unsigned)total), THREADS, shm, c.stream>>>(
+                X1, E, zl, ch, B, l, (int)c.K, c.logN, c.primes, fwd, c.imap_at(l), l + 1, nint, c.cji, c.psipow, wsplit);
+        }
         HEC_HIP(hipGetLastError());
     }
 }
@@ -2036,7 +2102,7 @@ void hoisted_mac_fused(Ctx &c, PolyArr X1, const u64 *E, const int *zl, const HC
 {
     if (nkids < 1 || nkids > HFUSE_MAXK) throw std::invalid_argument("hoisted_mac_fused: children per launch");
     if (l > HEC_MAXL) throw std::invalid_argument("too many limbs");
-    if (c.hfuse == 2) {  // digit-outer k_hfuse2: <LOGP, FP64 batch tile, integer batch tile, batch sets, children>
+    if (c.hfuse >= 2) {  // digit-outer k_hfuse2: <LOGP, FP64 batch tile, integer batch tile, batch sets, children>
         switch (c.logN) {
         case 10: case 11: launch_hfuse2<5, 4, 4, 4, 4>(c, X1, E, zl, kids, nkids, B, l); break;
         case 12: case 13: launch_hfuse2<6, 4, 2, 2, 4>(c, X1, E, zl, kids, nkids, B, l); break;
