@@ -1353,6 +1353,7 @@ __device__ __forceinline__ void hmacm_body(PolyArr X1, const u64 *__restrict__ E
                 const int *z = zl + 1 + ((b0 + t) * l + J) * (HEC_ZCAP + 1);
                 const int nz = min(z[0], HEC_ZCAP);
                 if (nz == 0) continue;
+#pragma unroll
                 for (int q = 0; q < CG; ++q) {
                     if (q >= ch.n) break;
                     const u64 ko0 = kc[q] | (u64)sw[q], ko1 = kc[q] | (u64)!sw[q];
@@ -1969,6 +1970,7 @@ __device__ __forceinline__ void hfuse2_body(u64 *lds, u64 *ltw, PolyArr X1, cons
                 const int *z = zl + 1 + ((b0 + bb) * l + J) * (HEC_ZCAP + 1);
                 const int nz = min(z[0], HEC_ZCAP);
                 if (nz == 0) continue;
+#pragma unroll
                 for (int c2 = 0; c2 < CG; ++c2) {
                     if (c2 >= nk) break;
                     const u64 ko0 = kc[c2] | (u64)sw[c2], ko1 = kc[c2] | (u64)!sw[c2];

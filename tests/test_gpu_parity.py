@@ -371,7 +371,8 @@ def test_cfg5_params_matvec_bitexact(orc, hecdna):
                                  {"HEC_TENSOR_BG": "0"}, {"HEC_TENSOR_BG": "0", "HEC_TENSOR_DEFER": "3"},
                                  {"HEC_FANSPLIT": "0"}, {"HEC_DIVROUND_FP": "0"}, {"HEC_HMAC_ODD3": "0"}, {"HEC_HOIST_SCAN": "0"}, {"HEC_NTT_RD": "0"}, {"HEC_NTT_RD": "0", "HEC_HOIST": "0"},
                                  {"HEC_HFUSE": "0"}, {"HEC_HFUSE": "0", "HEC_HMAC": "0"},
-                                 {"HEC_HFUSE": "2"}, {"HEC_HFUSE": "2", "HEC_HOIST_MIN": "1"}, {"HEC_BMAC_KEYS": "3"}])
+                                 {"HEC_HFUSE": "2"}, {"HEC_HFUSE": "2", "HEC_HOIST_MIN": "1"}, {"HEC_BMAC_KEYS": "3"},
+                                 {"HEC_HFUSE": "3"}, {"HEC_HFUSE": "2", "HEC_HFUSE_CG": "2"}])
 def test_keyswitch_variants_bitexact(orc, hecdna, env):
     """The engine's alternative key-switch schedules (separate mod-up pass B + MAC kernels; the fused
     kernel's key-load placements) give the same bits as the oracle."""
@@ -515,11 +516,29 @@ def _with_coeff_zeros(e, ct, limbs_zeros):
     return e.orc.Ct(d, ct.scale)
 
 
+def _env_with(orc, hecdna, env, *args, **kw):
+    """An Env whose context was created under the given HEC_* switches (read at context creation)."""
+    import os
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        return Env(orc, hecdna, *args, **kw)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
 @pytest.mark.parametrize("nzeros", [3, 40])  # 40 > HEC_ZCAP: the hoisted walk recomputes without hoisting
-def test_hoisted_modup_zero_coefficients(env11, nzeros):
+@pytest.mark.parametrize("variant", [{}, {"HEC_HFUSE": "0"}, {"HEC_HFUSE": "2"}, {"HEC_HFUSE": "3"},
+                                     {"HEC_HFUSE": "0", "HEC_HMAC": "9"}])
+def test_hoisted_modup_zero_coefficients(orc, hecdna, nzeros, variant):
     """The hoisted mod-up corrects for zero digit coefficients that the Galois automorphism negates
-    (SEAL maps -0 to 0, not to q_J); a limb with more zeros than the kernels list falls back."""
-    e = env11
+    (SEAL maps -0 to 0, not to q_J); a limb with more zeros than the kernels list falls back.  Every hoisted MAC
+    schedule (k_hfuse, k_hfuse2, k_hmacm pairs and quadruples)."""
+    e = _env_with(orc, hecdna, variant, 1 << 11, [50, 36, 36, 50])
     rng = np.random.default_rng(nzeros)
     X = [_with_coeff_zeros(e, e.enc(seed=1100 + i), {0: rng.choice(e.N, nzeros, replace=False),
                                                      2: rng.choice(e.N, 2, replace=False)}) for i in range(2)]
