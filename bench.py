@@ -52,19 +52,20 @@ def algorithmic_bytes_per_matvec(N, l, n, B, ks):
     return (n * s_ct + ks * s_key + s_key) / B + ks * 2 * s_ct + n * s_ct + s_ct3 + s_ct
 
 
-def pmc_traffic(kernel, B, logn, level, n):
+def pmc_traffic(kernel, B, logn, level, n, variant="ctct"):
     """HBM bytes per launch of the roofline kernel from the committed rocprofv3 PMC passes
-    (profiles/r03_pmc_<kernel>_B<B>.json, else r02_ / r01_; written by tools/pmc_summary.py: FETCH_SIZE and WRITE_SIZE in
-    separate passes, gfx950 FETCH x2 correction for 16-B/lane reads) when they were taken on this
-    configuration; else None."""
+    (profiles/r03_pmc_<kernel>_B<B>[_ctpt].json, else r02_ / r01_; written by tools/pmc_summary.py: FETCH_SIZE and
+    WRITE_SIZE in separate passes, gfx950 FETCH x2 correction for 16-B/lane reads) when they were taken on this
+    configuration and matvec variant; else None."""
+    sfx = "" if variant == "ctct" else f"_{variant}"
     for tag in ("r03", "r02", "r01"):  # the newest round's pass for this kernel
-        path = os.path.join(ROOT, "profiles", f"{tag}_pmc_{kernel}_B{B}.json")
+        path = os.path.join(ROOT, "profiles", f"{tag}_pmc_{kernel}_B{B}{sfx}.json")
         if os.path.exists(path):
             break
     else:
         return None
     p = json.load(open(path))
-    if (p["batch"], p["logN"], p["level"], p.get("n")) != (B, logn, level, n):
+    if (p["batch"], p["logN"], p["level"], p.get("n"), p.get("variant", "ctct")) != (B, logn, level, n, variant):
         return None
     return p["traffic_bytes_per_dispatch"]
 
@@ -399,7 +400,7 @@ def main():
             k = kernels[kern]
             per = k["ms"] / k["launches"]
             roof = {"bound": "hbm", "achieved": k["GBps"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": k["frac"], "traffic": pmc_traffic(kern, args.batch, args.logn, L, args.n),
+                    "frac": k["frac"], "traffic": pmc_traffic(kern, args.batch, args.logn, L, args.n, args.variant),
                     "kernel": kern, "avg_ms": round(per, 4), "algorithmic_bytes_per_launch": k["bytes_per_launch"],
                     "launches_per_step": k["launches"],
                     "share_of_step_gpu_time": round(k["ms"] / sum(v["ms"] for v in kernels.values()), 3)}

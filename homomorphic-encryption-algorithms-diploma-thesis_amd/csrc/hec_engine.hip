@@ -454,40 +454,26 @@ constexpr int HOIST_GROUP = 6;  // sibling rotations per grouped mod-down (and p
 struct Hoist {
     u64 *D = nullptr, *E = nullptr;
     int *zl = nullptr;
-    // key-switch accumulators of up to `cap` siblings, contiguous (moddown_group), live across the recursion into
-    // their subtrees: HOIST_GROUP for the per-pair MAC, up to HFUSE_MAXK for one fused launch (k_hfuse)
+    // key-switch accumulators of up to HOIST_GROUP siblings, contiguous (moddown_group), live across the recursion
+    // into their subtrees
     u64 *acc0 = nullptr;
-    int cap = 0;
     u64 sacc = 0;
     u64 *acc(int q) const { return acc0 + (u64)q * sacc; }
 };
-int hoist_cap(const Ctx &c, int max_children)  // accumulator sets a depth needs
+std::size_t hoist_words(const Ctx &c, std::size_t B, std::size_t l)
 {
-    return c.hfuse ? std::max(1, std::min(HFUSE_MAXK, max_children)) : HOIST_GROUP;
+    return c.N * B * (l + (l + 1) * l + (std::size_t)HOIST_GROUP * 2 * (l + 1)) +
+           ((1 + B * l * (HEC_ZCAP + 1)) * sizeof(int) + 7) / 8 + 4 * 64;
 }
-std::size_t hoist_words(const Ctx &c, std::size_t B, std::size_t l, int cap)
-{
-    return c.N * B * (l + (l + 1) * l + (std::size_t)cap * 2 * (l + 1)) + ((1 + B * l * (HEC_ZCAP + 1)) * sizeof(int) + 7) / 8 +
-           4 * 64;
-}
-Hoist hoist_alloc(const Ctx &c, Scratch &s, int B, int l, int cap)
+Hoist hoist_alloc(const Ctx &c, Scratch &s, int B, int l)
 {
     Hoist h;
     h.D = s.take((u64)B * l * c.N);
     h.E = s.take((u64)B * (l + 1) * l * c.N);
     h.zl = reinterpret_cast<int *>(s.take(((1 + (u64)B * l * (HEC_ZCAP + 1)) * sizeof(int) + 7) / 8));
-    h.cap = cap;
     h.sacc = (u64)B * 2 * (l + 1) * c.N;
-    h.acc0 = s.take((u64)cap * h.sacc);
+    h.acc0 = s.take((u64)HOIST_GROUP * h.sacc);
     return h;
-}
-// k_hfuse's LDS for level l fits a block (64 KiB of dynamic LDS): otherwise the per-pair path
-bool hfuse_fits(const Ctx &c, int l)
-{
-    if (c.hfuse >= 2) return true;  // k_hfuse2 stages a few digits at a time
-    const int logp = c.logN - c.logR, bg = c.logN == 15 ? c.hfuse_bg : c.logN <= 13 ? 4 : c.logN == 14 ? 2 : 1;
-    const std::size_t words = 2 * ((std::size_t)1 << logp) + (std::size_t)l * bg * (((1 << logp) + (1 << logp) / 8 + 8));
-    return c.hfuse && words * sizeof(u64) <= 65536;
 }
 void hoist_node(Ctx &c, PolyArr X, int B, int l, const Hoist &h)
 {
@@ -505,7 +491,6 @@ void hoist_node(Ctx &c, PolyArr X, int B, int l, const Hoist &h)
             ProfScope k(c, "k:k_fan2/hoist", (double)B * l * (l + 1));
             fan_modup(c, h.D, h.E, B, l, false, h.zl);
         }
-        if (hfuse_fits(c, l)) return;  // k_hfuse runs the digits' pass B itself
         ProfScope k(c, "k:k_ntt/modup_h_b", 2.0 * B * l * l);
         ks_modup(c, h.D, h.E, B, l, 2);  // pass B, canonical NTT-form digits
         return;
@@ -737,37 +722,29 @@ void walk_trie_hoisted(Ctx &c, Scratch &s, const RotTrie &t, int node, PolyArr s
         return;
     }
     const Hoist &h = hs[depth];
-    const bool fused = hfuse_fits(c, l) && c.fan2 && c.hoist_scan;
     hoist_node(c, src, B, l, h);
     const u64 N = c.N;
-    // children in launches of up to `sup` siblings (fused: one k_hfuse launch, the digits' pass B included;
-    // otherwise one sibling-fused k_hmacm launch per hoisted_group() of them); accumulators h.acc(q), contiguous;
-    // then the mod-downs in groups of HOIST_GROUP share their small launches
-    const std::size_t grp = fused ? 1 : (std::size_t)hoisted_group(c);
-    const std::size_t sup = fused ? (std::size_t)h.cap : std::max<std::size_t>(grp, HOIST_GROUP / grp * grp);
+    // children in groups of up to `sup` siblings: one sibling-fused k_hmacm launch per hoisted_group() of them,
+    // accumulators h.acc(q), contiguous; then the mod-downs in groups of HOIST_GROUP share their small launches
+    const std::size_t grp = (std::size_t)hoisted_group(c);
+    const std::size_t sup = std::max<std::size_t>(grp, HOIST_GROUP / grp * grp);
     for (std::size_t g0 = 0; g0 < ch.size(); g0 += sup) {
         const int ng = (int)std::min<std::size_t>(sup, ch.size() - g0);
-        HChildSpec kids[HFUSE_MAXK > HOIST_GROUP ? HFUSE_MAXK : HOIST_GROUP];
+        HChildSpec kids[HOIST_GROUP];
         for (int q = 0; q < ng; ++q) {
             const u32 e = t.nodes[ch[g0 + q]].elt;
             kids[q] = HChildSpec{e, (u32)invm(e, 2 * N), gk.keys.at(e), galois_negw(ctx, gk, e), h.acc(q),
                                  galois_kw(ctx, gk, e, l)};
         }
         const double K = l + 1;  // per child: key (2 l K), W (K), KW (2 K), ACC (2 B K)
-        if (fused) {  // E pass-A digits (B l^2, J != I at every target) + c1 (B l), per child as above
-            ProfScope ps(c, "ks_hmac");
-            ProfScope k(c, "k:k_hfuse", (double)B * (l * l + l) + ng * (2.0 * l * K + 3.0 * K + 2.0 * B * K));
-            hoisted_mac_fused(c, PolyArr{src.p + src.sk, src.sb, 0}, h.E, h.zl, kids, ng, B, l);
-        } else {
-            for (int q0 = 0, nk = 0; q0 < ng; q0 += nk) {  // one profile scope per launch (bench.py's roofline)
-                nk = std::min((int)grp, ng - q0);
-                // an odd group's last three children as one 3-child launch (the digits read once, not twice)
-                if (c.hmac_odd3 && grp == 2 && ng - q0 == 3) nk = 3;
-                ProfScope ps(c, "ks_hmac");  // digits E (B l^2) + c1 (B l) + per child
-                ProfScope k(c, "k:k_hmacm", (double)B * (l * l + l) + nk * (2.0 * l * K + 3.0 * K + 2.0 * B * K));
-                if (nk == 3 && grp == 2) hoisted_mac_3(c, PolyArr{src.p + src.sk, src.sb, 0}, h.E, h.zl, kids + q0, B, l);
-                else hoisted_mac_multi(c, PolyArr{src.p + src.sk, src.sb, 0}, h.E, h.zl, kids + q0, nk, B, l);
-            }
+        for (int q0 = 0, nk = 0; q0 < ng; q0 += nk) {  // one profile scope per launch (bench.py's roofline)
+            nk = std::min((int)grp, ng - q0);
+            // an odd group's last three children as one 3-child launch (the digits read once, not twice)
+            if (c.hmac_odd3 && grp == 2 && ng - q0 == 3) nk = 3;
+            ProfScope ps(c, "ks_hmac");  // digits E (B l^2) + c1 (B l) + per child
+            ProfScope k(c, "k:k_hmacm", (double)B * (l * l + l) + nk * (2.0 * l * K + 3.0 * K + 2.0 * B * K));
+            if (nk == 3 && grp == 2) hoisted_mac_3(c, PolyArr{src.p + src.sk, src.sb, 0}, h.E, h.zl, kids + q0, B, l);
+            else hoisted_mac_multi(c, PolyArr{src.p + src.sk, src.sb, 0}, h.E, h.zl, kids + q0, nk, B, l);
         }
         for (int m0 = 0; m0 < ng; m0 += HOIST_GROUP) {  // mod-downs in groups, then each child's subtree
             const int nm = std::min(HOIST_GROUP, ng - m0);
@@ -881,20 +858,10 @@ void matvec_core(hec_context *ctx, const hec_ciphertext *const *diags, const hec
     const int D = trie.depth;
     const int nb = c.tensor_defer_bufs;  // rotation buffers per depth
     const bool hoist = c.hoist && D > 0;
-    std::vector<int> caps(std::max(D, 1), 0);  // accumulator sets per depth: the widest hoisted node there
-    if (hoist) {
-        std::vector<int> dep(trie.nodes.size(), 0);
-        std::vector<int> widest(D + 1, 0);
-        for (std::size_t nd = 0; nd < trie.nodes.size(); ++nd) {  // parents precede children in insertion order
-            for (int ch : trie.nodes[nd].children) dep[ch] = dep[nd] + 1;
-            widest[dep[nd]] = std::max(widest[dep[nd]], (int)trie.nodes[nd].children.size());
-        }
-        for (int d = 0; d < D; ++d) caps[d] = hoist_cap(c, widest[d]);
-    }
     std::size_t words = p * (S2 * (1 + (std::size_t)D * nb) + S3) + 2 * p * l * N + ks_words(c, p, l) +
                         (D * nb + 80) * 64;
     if (hoist) {
-        for (int d = 0; d < D; ++d) words += hoist_words(c, p, l, caps[d]);
+        words += (std::size_t)D * hoist_words(c, p, l);
         words += hoisted_child_words(c, p, l);
     }
     if (finish) words += rescale_words(c, p, 2, l) + p * 2 * (l - 1) * N;
@@ -934,7 +901,7 @@ void matvec_core(hec_context *ctx, const hec_ciphertext *const *diags, const hec
             galois_kw(ctx, gkm, trie.nodes[nd].elt, (int)l);
         }
         std::vector<Hoist> hs(D);
-        for (int d = 0; d < D; ++d) hs[d] = hoist_alloc(c, s, (int)p, (int)l, caps[d]);
+        for (int d = 0; d < D; ++d) hs[d] = hoist_alloc(c, s, (int)p, (int)l);
         HEC_HIP(hipMemsetAsync(c.zflag, 0, sizeof(int), c.stream));
         walk_trie_hoisted(c, s, trie, 0, Xa, 0, (int)p, (int)l, ctx, gkm, bufs, hs, S2, c.hoist_min_children, visit,
                           before_write);
@@ -1283,13 +1250,9 @@ int hec_context_create(uint64_t N, const uint64_t *mod, uint64_t K, int device, 
         Ctx &c = ctx->c;
         c.device = device;
         if (const char *f = std::getenv("HEC_FUSED_MODUP_MAC")) c.fused_modup_mac = f[0] != '0';
-        if (const char *f = std::getenv("HEC_BMAC_KEYS")) c.bmac_keys = f[0] - '0';
         if (const char *f = std::getenv("HEC_FUSE_GALOIS")) c.fuse_galois = f[0] != '0';
         if (const char *f = std::getenv("HEC_FAN")) c.fan_out = f[0] != '0';
         if (const char *f = std::getenv("HEC_FAN2")) c.fan2 = std::atoi(f);
-        if (const char *f = std::getenv("HEC_HFUSE")) c.hfuse = std::atoi(f);
-        if (const char *f = std::getenv("HEC_HFUSE_BG")) c.hfuse_bg = std::atoi(f);
-        if (const char *f = std::getenv("HEC_HFUSE_CG")) c.hfuse_cg = std::atoi(f);
         if (const char *f = std::getenv("HEC_FANSPLIT")) c.fan_split = std::atoi(f);
         if (const char *f = std::getenv("HEC_NTT_RD")) c.ntt_rd = std::atoi(f);
         if (const char *f = std::getenv("HEC_HOIST_SCAN")) c.hoist_scan = std::atoi(f);

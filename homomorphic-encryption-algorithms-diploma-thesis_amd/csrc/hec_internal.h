@@ -84,14 +84,12 @@ struct Ctx {
     // host-side constants
     std::vector<u64> p_inv, p_inv_q, p_half_mod;            // key switch mod-down (per data prime)
     std::vector<std::vector<u64>> ql_inv, ql_inv_q, ql_half_mod;  // rescale at level l (drop prime l-1)
-    int bmac_keys = 1;             // HEC_BMAC_KEYS: k_bmac key loads 0 late / 1 before the rounds / 2 one digit ahead
     int tensor_defer_max = 12;     // HEC_TENSOR_DEFER: terminals per deferred tensor batch (1 = immediate)
     int tensor_defer_bufs = 8;     // HEC_TENSOR_BUFS: rotation buffers per trie depth
     int tensor_bg = 1;             // HEC_TENSOR_BG=0: k_tensor_multi (one thread per coefficient, whole batch)
     bool hoist = true;             // HEC_HOIST=0: no hoisted mod-up in the rotation trie walk
     int hoist_min_children = 2;    // HEC_HOIST_MIN: children a trie node needs to be hoisted
-    int hmac_cfg = 3;              // HEC_HMAC: 0 one hoisted MAC per child; siblings fused: 1 (4 x 1 batch),
-                                   // 2 (2 x 2), 3 (2 x 4, default), 4 (3 x 2) children x batch entries per thread
+    int hmac_cfg = 1;              // HEC_HMAC=0: one hoisted MAC per child (1: sibling pairs fused, k_hmacm)
     int fan_groups_moddown = 1;    // HEC_FANG="moddown,modup,hoist": target groups per k_fan source (blocks
     int fan_groups_modup = 1;      // per launch x groups; the source's inverse pass is repeated per group)
     int fan_groups_hoist = 1;
@@ -103,9 +101,6 @@ struct Ctx {
     int fan_split = 1;             // HEC_FANSPLIT=0: Barrett (not the FP64 split) for the mod-down rounding limbs
                                    // at FP64 targets (FanDivRound::xf16)
     int fan2 = 1;                  // HEC_FAN2=0: the LDS-round k_fan instead of the register-direct k_fan2
-    int hfuse = 1;                 // HEC_HFUSE=0: hoisted node = ks_modup pass B, then k_hmacm per sibling pair
-    int hfuse_bg = 2;              // HEC_HFUSE_BG: batch entries per k_hfuse block at N = 2^15 (1, 2 or 4)
-    int hfuse_cg = 4;              // HEC_HFUSE_CG: children per k_hfuse2 launch at N = 2^14, 2^15 (2, 4 or 6)
     bool fan_out = true;           // HEC_FAN=0: separate INTT pass A (fan-out fuses it into the forward passes A)
     int lanes = 3;                 // HEC_LANES: concurrent batch lanes of a matvec (hec_engine.hip matvec_lanes)
     int lane_min_batch = 16;       // input vectors per lane at least
@@ -178,10 +173,6 @@ void hoisted_mac_multi(Ctx &c, PolyArr X1, const u64 *E, const int *zl, const HC
 // three children in one sibling-fused launch (3 x 4 FP64 / 3 x 2 integer batch entries per thread)
 void hoisted_mac_3(Ctx &c, PolyArr X1, const u64 *E, const int *zl, const HChildSpec *kids, int B, int l);
 int hoisted_group(const Ctx &c);  // children per hoisted_mac_multi call for c.hmac_cfg
-// fused hoisted MAC (k_hfuse): the node's pass-A-domain digits E -> pass B in LDS -> the key MACs of up to
-// HFUSE_MAXK sibling rotations (HEC_HFUSE=0: ks_modup pass B + k_hmacm per sibling pair)
-constexpr int HFUSE_MAXK = 12;
-void hoisted_mac_fused(Ctx &c, PolyArr X1, const u64 *E, const int *zl, const HChildSpec *kids, int nkids, int B, int l);
 void fan_divide_round(Ctx &c, const u64 *Y, u64 ysb, u64 ysk, u64 *Z, int B, int nk, int nl, int last_idx);
 void galois_permute(Ctx &c, PolyArr in, PolyArr out, int B, int nk, int nl, u32 elt);
 void tensor_acc(Ctx &c, PolyArr R, const u64 *A, u64 a_sk, PolyArr ACC, int B, int l, bool assign);

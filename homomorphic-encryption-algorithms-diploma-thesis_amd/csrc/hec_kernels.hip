@@ -1480,660 +1480,21 @@ static void launch_hmacm(Ctx &c, PolyArr X1, const u64 *E, const int *zl, const 
     HEC_HIP(hipGetLastError());
 }
 
-int hoisted_group(const Ctx &c)
-{
-    switch (c.hmac_cfg) {
-    case 1: case 9: case 10: case 11: return 4;
-    case 12: return 6;
-    case 2: case 3: case 5: case 6: case 8: case 13: case 14: return 2;
-    case 4: case 7: return 3;
-    default: return 1;
-    }
-}
+int hoisted_group(const Ctx &c) { return c.hmac_cfg ? 2 : 1; }
 
 void hoisted_mac_multi(Ctx &c, PolyArr X1, const u64 *E, const int *zl, const HChildSpec *kids, int nkids, int B,
                        int l)
 {
     if (nkids < 1 || nkids > hoisted_group(c)) throw std::invalid_argument("hoisted_mac_multi: group size");
-    switch (c.hmac_cfg) {
-    case 1: launch_hmacm<1, 1, 4>(c, X1, E, zl, kids, nkids, B, l); break;
-    case 2: launch_hmacm<2, 2, 2>(c, X1, E, zl, kids, nkids, B, l); break;
-    case 3: launch_hmacm<4, 2, 2>(c, X1, E, zl, kids, nkids, B, l); break;
-    case 4: launch_hmacm<2, 2, 3>(c, X1, E, zl, kids, nkids, B, l); break;
-    case 5: launch_hmacm<4, 4, 2>(c, X1, E, zl, kids, nkids, B, l); break;
-    case 6: launch_hmacm<4, 1, 2>(c, X1, E, zl, kids, nkids, B, l); break;
-    case 7: launch_hmacm<4, 2, 3>(c, X1, E, zl, kids, nkids, B, l); break;
-    case 8: launch_hmacm<8, 2, 2>(c, X1, E, zl, kids, nkids, B, l); break;
-    case 9: launch_hmacm<2, 1, 4>(c, X1, E, zl, kids, nkids, B, l); break;
-    case 10: launch_hmacm<2, 2, 4>(c, X1, E, zl, kids, nkids, B, l); break;
-    case 11: launch_hmacm<4, 1, 4>(c, X1, E, zl, kids, nkids, B, l); break;
-    case 12: launch_hmacm<2, 1, 6>(c, X1, E, zl, kids, nkids, B, l); break;
-    case 13: launch_hmacm<4, 2, 2, 2>(c, X1, E, zl, kids, nkids, B, l); break;
-    case 14: launch_hmacm<2, 2, 2, 4>(c, X1, E, zl, kids, nkids, B, l); break;
-    default: hoisted_mac(c, X1, E, kids[0].W, zl, kids[0].key, kids[0].ACC, B, l, kids[0].elt); break;
-    }
+    // <FP64 batch entries, integer batch entries, children> per thread (the 1x4, 2x2, 3x2, 4x4 ...
+    // shapes measured slower)
+    if (c.hmac_cfg) launch_hmacm<4, 2, 2>(c, X1, E, zl, kids, nkids, B, l);
+    else hoisted_mac(c, X1, E, kids[0].W, zl, kids[0].key, kids[0].ACC, B, l, kids[0].elt);
 }
 
 void hoisted_mac_3(Ctx &c, PolyArr X1, const u64 *E, const int *zl, const HChildSpec *kids, int B, int l)
 {
     launch_hmacm<4, 2, 3>(c, X1, E, zl, kids, 3, B, l);
-}
-
-// ======================================================= fused hoisted MAC: pass B of the digits + siblings ==
-// k_hfuse finishes the node's mod-up NTTs AND runs the key MAC of up to HFUSE_MAXK sibling rotations in one kernel,
-// so the node's digits go to HBM once, in the pass-A domain (k_fan2's output E), and are read once per launch
-// instead of: written in NTT form by a separate pass B, re-read and re-written by it, then re-read by every
-// sibling-pair MAC launch (those round trips were about half of a step's bytes).
-// A block owns one pass-B chunk (P = 2^LOGP contiguous coefficients) of one target prime I for BG batch entries:
-//   1. it stages every digit tile of its chunk into LDS: E[b][I][J] (pass-A domain) for J != I, and for J == I the
-//      node's own NTT-form c1 (X1), SEAL's reuse of the NTT-form input;
-//   2. it runs pass B (the last LOGP stages of NTT_I) on every J != I tile in LDS, 8 elements per thread, the
-//      chunk's twiddles staged once;
-//   3. for every child c (elt, its inverse einv) a thread owns two adjacent SOURCE positions s, s + 1 of BT batch
-//      entries and accumulates, at the child's output position t = gal_c^-1(s) (pairs stay pairs),
-//        ACC_c[b][k][I][t] = sum_J key_c[J][k][I][t] e_J[s] + W_c[I][t] KW_c[k][I][t]
-//      (the sign-mask term factored out of the digit loop, see k_hmacm; rare zero corrections as there), exact:
-//      FP64 targets as integer-valued double sums of fp_mulmod products, 60-bit targets in 128-bit sums, one
-//      reduction at the end.  Every term is SEAL's, so each child's key-switch input is bit-identical.
-// Grid: two segments (integer targets first, then FP64), each XCD-aware like k_hmacm: the batch groups of one
-// (chunk, I) get ids = mod 8, so they share an XCD and its L2 copy of the children's key chunk.
-struct HFuseKids {
-    HChild c[HFUSE_MAXK];
-    int n;
-};
-constexpr int hfuse_ld(int logp) { return (1 << logp) + (1 << logp) / 8 + 8; }  // tile stride (k_bmac's padding)
-
-template <int LOGP, int BG, int BS, bool FP>
-__device__ __forceinline__ void hfuse_body(u64 *lds, u64 *ltw, PolyArr X1, const u64 *__restrict__ E,
-                                           const int *__restrict__ zl, const HFuseKids &ch, int B, int l, int K,
-                                           int logN, const DevPrime &pr, const TwTables &tt, int I, int kI, int chunk,
-                                           int b0, const u64 *__restrict__ cji, const u64 *__restrict__ psipow)
-{
-    constexpr int P = 1 << LOGP, EPT = 8, TPT = P / EPT, PAIRS = P / 2, THREADS = PAIRS * BS, BT = BG / BS;
-    constexpr int LD = hfuse_ld(LOGP), CONC = THREADS / TPT;
-    static_assert(THREADS % TPT == 0 && BG % BS == 0, "thread layout");
-    const u64 N = 1ull << logN, base = (u64)chunk << LOGP;
-    const int nb = min(BG, B - b0);
-    auto addr_of = [](int tl, int x) { return tl * LD + x + (x >> 3); };
-    {  // the chunk's pass-B twiddles (entry k = 2^s - 1 + i of stage s), independent of the digit
-        const u64 R = 1ull << (logN - LOGP);
-        const ulonglong2 *tw = tt.b + ((u64)kI << logN);
-        const double *twf = tt.fb + ((u64)kI << logN);
-        for (int k = threadIdx.x; k < P - 1; k += THREADS) {
-            const int st = 31 - __clz(k + 1), i = k + 1 - (1 << st);
-            const u64 gi = R * ((1ull << st) - 1) + (u64)i * R + (u64)chunk;
-            if constexpr (FP) ltw[k] = (u64)__double_as_longlong(twf[gi]);
-            else {
-                const ulonglong2 w = tw[gi];
-                ltw[2 * k] = w.x;
-                ltw[2 * k + 1] = w.y;
-            }
-        }
-    }
-    // 1. every (J, batch entry) tile of the chunk, 16-B loads
-    for (int w = threadIdx.x; w < l * BG * PAIRS; w += THREADS) {
-        const int tl = w / PAIRS, pp = w % PAIRS, J = tl / BG, bb = tl % BG;
-        if (bb >= nb) continue;
-        const int b = b0 + bb;
-        const u64 *src = J == I ? X1.p + (u64)b * X1.sb + ((u64)J << logN)
-                                : E + (((u64)((b * (l + 1) + I) * l + J)) << logN);
-        ulonglong2 v = *(const ulonglong2 *)(src + base + 2 * pp);
-        if constexpr (FP) {
-            if (J == I) v = ulonglong2{(u64)__double_as_longlong(u2d(v.x)), (u64)__double_as_longlong(u2d(v.y))};
-        }
-        lds[addr_of(tl, 2 * pp)] = v.x;
-        lds[addr_of(tl, 2 * pp + 1)] = v.y;
-    }
-    __syncthreads();
-    // 2. pass B on the J != I tiles, CONC transforms at a time (rounds of 3 stages, 8 elements per thread)
-    const LdsTw twg{ltw};
-    const int ntf = l * BG;
-    for (int t0 = 0; t0 < ntf; t0 += CONC) {
-        const int tl = t0 + (int)threadIdx.x / TPT, ts = (int)threadIdx.x % TPT;
-        const bool act = tl < ntf && tl / BG != I && tl % BG < nb;
-        auto addr = [tl](int x) { return tl * LD + x + (x >> 3); };
-        if constexpr (LOGP <= 6) {
-            if (act) ntt_round_g<LOGP, 0, 3, EPT, false, FP, false>(lds, addr, ts, twg, pr, nullptr);
-            __syncthreads();
-            if (act) ntt_round_g<LOGP, 3, LOGP, EPT, false, FP, false>(lds, addr, ts, twg, pr, nullptr);
-        } else {
-            if (act) ntt_round_g<LOGP, 0, 3, EPT, false, FP, false>(lds, addr, ts, twg, pr, nullptr);
-            __syncthreads();
-            if (act) ntt_round_g<LOGP, 3, 6, EPT, false, FP, false>(lds, addr, ts, twg, pr, nullptr);
-            __syncthreads();
-            if (act) ntt_round_g<LOGP, 6, LOGP, EPT, false, FP, false>(lds, addr, ts, twg, pr, nullptr);
-        }
-        __syncthreads();
-    }
-    // 3. the children's MACs from the LDS tiles, two children per pass (independent key streams), each child's key
-    //    words for KCH digits issued together before their products
-    const int pp = (int)threadIdx.x % PAIRS, bs = (int)threadIdx.x / PAIRS;
-    const u64 s0 = base + 2 * pp;
-    const bool zeros = zl[0] != 0;
-    const u64 *pp_pow = psipow + ((u64)kI << (logN + 1));
-    const u64 q = pr.q, two_q = 2 * q;
-    constexpr int CGP = 2, KCH = 2;
-    for (int q0 = 0; q0 < ch.n; q0 += CGP) {
-        const int nq = min(CGP, ch.n - q0);
-        u64 kc[CGP];
-        bool sw[CGP];
-        double f[FP ? CGP : 1][FP ? BT : 1][4];
-        U128 a[FP ? 1 : CGP][FP ? 1 : BT][4];
-#pragma unroll
-        for (int c2 = 0; c2 < CGP; ++c2) {
-            const HChild &cc = ch.c[q0 + (c2 < nq ? c2 : 0)];
-            const u32 t = galois_src((u32)s0, cc.einv, logN);
-            kc[c2] = t & ~1u;
-            sw[c2] = t & 1;
-            // the sign-mask term W KW at the output pair, in source order
-            const ulonglong2 w = *(const ulonglong2 *)(cc.W + ((u64)kI << logN) + kc[c2]);
-            const ulonglong2 m0 = *(const ulonglong2 *)(cc.KW + ((u64)I << logN) + kc[c2]);
-            const ulonglong2 m1 = *(const ulonglong2 *)(cc.KW + ((u64)(l + 1 + I) << logN) + kc[c2]);
-            if constexpr (FP) {  // canonical operands < q < 2^42: fp_mulmod is exact
-                double wk[4] = {fp_mulmod(u2d(w.x), u2d(m0.x), pr.qd, pr.qinv), fp_mulmod(u2d(w.y), u2d(m0.y), pr.qd, pr.qinv),
-                                fp_mulmod(u2d(w.x), u2d(m1.x), pr.qd, pr.qinv), fp_mulmod(u2d(w.y), u2d(m1.y), pr.qd, pr.qinv)};
-                if (sw[c2]) {
-                    double x = wk[0]; wk[0] = wk[1]; wk[1] = x;
-                    x = wk[2]; wk[2] = wk[3]; wk[3] = x;
-                }
-#pragma unroll
-                for (int tb = 0; tb < BT; ++tb)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) f[c2][tb][r] = wk[r];
-            } else {
-                u64 wk[4] = {mulmod(w.x, m0.x, pr), mulmod(w.y, m0.y, pr), mulmod(w.x, m1.x, pr), mulmod(w.y, m1.y, pr)};
-                if (sw[c2]) {
-                    u64 x = wk[0]; wk[0] = wk[1]; wk[1] = x;
-                    x = wk[2]; wk[2] = wk[3]; wk[3] = x;
-                }
-#pragma unroll
-                for (int tb = 0; tb < BT; ++tb)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) a[c2][tb][r] = U128{wk[r], 0};
-            }
-        }
-        for (int J0 = 0; J0 < l; J0 += KCH) {
-            ulonglong2 kk[CGP][KCH][2];  // key words of digits J0 .. J0 + KCH - 1, both polys, in source order
-#pragma unroll
-            for (int c2 = 0; c2 < CGP; ++c2)
-#pragma unroll
-                for (int j = 0; j < KCH; ++j) {
-                    if (J0 + j < l && c2 < nq) {
-                        const u64 *kp = ch.c[q0 + c2].key + (((u64)((J0 + j) * 2) * K + kI) << logN) + kc[c2];
-                        kk[c2][j][0] = *(const ulonglong2 *)kp;
-                        kk[c2][j][1] = *(const ulonglong2 *)(kp + ((u64)K << logN));
-                    } else {
-                        kk[c2][j][0] = kk[c2][j][1] = ulonglong2{0, 0};
-                    }
-                }
-#pragma unroll
-            for (int j = 0; j < KCH; ++j) {
-                const int J = J0 + j;
-                if (J >= l) break;
-                const u64 cj = cji[J * K + kI];
-#pragma unroll
-                for (int tb = 0; tb < BT; ++tb) {
-                    const int bb = bs * BT + tb;
-                    if (bb >= nb) break;
-                    const int tl = J * BG + bb;
-                    const u64 r0 = lds[addr_of(tl, 2 * pp)], r1 = lds[addr_of(tl, 2 * pp + 1)];
-#pragma unroll
-                    for (int c2 = 0; c2 < CGP; ++c2) {
-                        if (c2 >= nq) break;
-                        u64 e0 = r0, e1 = r1;
-                        if (J != I && zeros) {  // output slots (in source order) of this child: kc ^ sw, kc ^ !sw
-                            const int *z = zl + 1 + ((b0 + bb) * l + J) * (HEC_ZCAP + 1);
-                            const int nz = min(z[0], HEC_ZCAP);
-                            if (nz > 0) {
-                                if constexpr (FP) {
-                                    e0 = fp_canon(__longlong_as_double((long long)e0), pr.qd, pr.qinv);
-                                    e1 = fp_canon(__longlong_as_double((long long)e1), pr.qd, pr.qinv);
-                                } else {
-                                    e0 = csub(csub(e0, two_q), q);
-                                    e1 = csub(csub(e1, two_q), q);
-                                }
-                                const u64 ko0 = kc[c2] | (u64)sw[c2], ko1 = kc[c2] | (u64)!sw[c2];
-                                const u32 elt = ch.c[q0 + c2].elt;
-                                for (int zi = 0; zi < nz; ++zi) {
-                                    u64 tt2 = ((u64)z[1 + zi] * elt) & (2 * N - 1);
-                                    if (tt2 < N) continue;
-                                    tt2 -= N;
-                                    const u64 ex0 = ((2 * (u64)bitrev((u32)ko0, logN) + 1) * tt2) & (2 * N - 1);
-                                    const u64 ex1 = ((2 * (u64)bitrev((u32)ko1, logN) + 1) * tt2) & (2 * N - 1);
-                                    e0 = submod(e0, mulmod(cj, pp_pow[ex0], pr), q);
-                                    e1 = submod(e1, mulmod(cj, pp_pow[ex1], pr), q);
-                                }
-                                if constexpr (FP) {
-                                    e0 = (u64)__double_as_longlong(u2d(e0));
-                                    e1 = (u64)__double_as_longlong(u2d(e1));
-                                }
-                            }
-                        }
-                        const ulonglong2 k0 = sw[c2] ? ulonglong2{kk[c2][j][0].y, kk[c2][j][0].x} : kk[c2][j][0];
-                        const ulonglong2 k1 = sw[c2] ? ulonglong2{kk[c2][j][1].y, kk[c2][j][1].x} : kk[c2][j][1];
-                        if constexpr (FP) {  // |e| < 10 q: the forward NTT's output before canonicalisation
-                            const double d0 = __longlong_as_double((long long)e0), d1 = __longlong_as_double((long long)e1);
-                            f[c2][tb][0] += fp_mulmod(d0, u2d(k0.x), pr.qd, pr.qinv);
-                            f[c2][tb][1] += fp_mulmod(d1, u2d(k0.y), pr.qd, pr.qinv);
-                            f[c2][tb][2] += fp_mulmod(d0, u2d(k1.x), pr.qd, pr.qinv);
-                            f[c2][tb][3] += fp_mulmod(d1, u2d(k1.y), pr.qd, pr.qinv);
-                        } else {
-                            if (J != I) {  // lazy [0, 4q) -> canonical
-                                e0 = csub(csub(e0, two_q), q);
-                                e1 = csub(csub(e1, two_q), q);
-                            }
-                            mac128(a[c2][tb][0], e0, k0.x);
-                            mac128(a[c2][tb][1], e1, k0.y);
-                            mac128(a[c2][tb][2], e0, k1.x);
-                            mac128(a[c2][tb][3], e1, k1.y);
-                        }
-                    }
-                }
-            }
-        }
-#pragma unroll
-        for (int c2 = 0; c2 < CGP; ++c2) {
-            if (c2 >= nq) break;
-            const HChild &cc = ch.c[q0 + c2];
-#pragma unroll
-            for (int tb = 0; tb < BT; ++tb) {
-                const int bb = bs * BT + tb;
-                if (bb >= nb) break;
-                const int b = b0 + bb;
-                u64 r[4];
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    if constexpr (FP) r[i] = fp_canon(f[c2][tb][i], pr.qd, pr.qinv);
-                    else r[i] = barrett128(a[c2][tb][i].lo, a[c2][tb][i].hi, q, pr.r0, pr.r1);
-                }
-                u64 *o0 = cc.ACC + (((u64)((b * 2 + 0) * (l + 1) + I)) << logN) + kc[c2];
-                u64 *o1 = cc.ACC + (((u64)((b * 2 + 1) * (l + 1) + I)) << logN) + kc[c2];
-                *(ulonglong2 *)o0 = sw[c2] ? ulonglong2{r[1], r[0]} : ulonglong2{r[0], r[1]};
-                *(ulonglong2 *)o1 = sw[c2] ? ulonglong2{r[3], r[2]} : ulonglong2{r[2], r[3]};
-            }
-        }
-    }
-}
-
-template <int LOGP, int BG, int BS>
-__global__ void __launch_bounds__((1 << LOGP) / 2 * BS)
-    k_hfuse(PolyArr X1, const u64 *__restrict__ E, const int *__restrict__ zl, const HFuseKids ch, int B, int l, int K,
-            int logN, const DevPrime *__restrict__ primes, TwTables tt, const int *__restrict__ Imap, int nI, int nint,
-            const u64 *__restrict__ cji, const u64 *__restrict__ psipow, int wsplit)
-{
-    constexpr int P = 1 << LOGP;
-    extern __shared__ u64 hfuse_lds[];  // [2 P] twiddles, then l BG tiles of hfuse_ld(LOGP) words
-    u64 *ltw = hfuse_lds, *lds = hfuse_lds + 2 * P;
-    const int X = 1 << (logN - LOGP);  // chunks
-    const int nbg = (B + BG - 1) / BG;
-    const bool integer = (int)blockIdx.x < wsplit;
-    const int w = integer ? blockIdx.x : blockIdx.x - wsplit;
-    const int g8 = w & 7, rest = w >> 3, bg = rest % nbg, G = (rest / nbg) * 8 + g8;
-    if (G >= X * (integer ? nint : nI - nint)) return;
-    const int yi = G / X + (integer ? 0 : nint), chunk = G % X;
-    const int I = Imap[yi];
-    const int kI = I == l ? K - 1 : I;
-    const DevPrime pr = primes[kI];
-    if (integer)
-        hfuse_body<LOGP, BG, BS, false>(lds, ltw, X1, E, zl, ch, B, l, K, logN, pr, tt, I, kI, chunk, bg * BG, cji, psipow);
-    else
-        hfuse_body<LOGP, BG, BS, true>(lds, ltw, X1, E, zl, ch, B, l, K, logN, pr, tt, I, kI, chunk, bg * BG, cji, psipow);
-}
-
-template <int LOGP, int BG, int BS>
-static void launch_hfuse(Ctx &c, PolyArr X1, const u64 *E, const int *zl, const HChildSpec *kids, int nkids, int B,
-                         int l)
-{
-    HFuseKids ch{};
-    ch.n = nkids;
-    for (int q = 0; q < nkids; ++q)
-        ch.c[q] = HChild{kids[q].elt, kids[q].einv, kids[q].key, kids[q].W, kids[q].ACC, kids[q].KW};
-    const int nint = c.imap_nint[l], X = (int)(c.N >> LOGP), nbg = (B + BG - 1) / BG;
-    const int gI = (X * nint + 7) / 8 * 8, gF = (X * (l + 1 - nint) + 7) / 8 * 8;
-    const int wsplit = gI * nbg, total = wsplit + gF * nbg;
-    const TwTables fwd{c.tw, c.twb, c.twf, c.twbf};
-    const std::size_t shm = (std::size_t)(2 * (1 << LOGP) + l * BG * hfuse_ld(LOGP)) * sizeof(u64);
-    k_hfuse<LOGP, BG, BS><<<dim3((unsigned)total), (1 << LOGP) / 2 * BS, shm, c.stream>>>(
-        X1, E, zl, ch, B, l, (int)c.K, c.logN, c.primes, fwd, c.imap_at(l), l + 1, nint, c.cji, c.psipow, wsplit);
-    HEC_HIP(hipGetLastError());
-}
-
-// k_hfuse2: the same fused computation with the digit loop outside the children.  A block (one pass-B chunk of one
-// target prime I, BG batch entries) stages D digits at a time (D BG tiles = one pass-B transform per 16 threads),
-// runs their pass B in LDS, then every thread multiply-accumulates its position pair x BT batch entries into the
-// accumulators of all CG children of the launch: per digit the CG children's key words are independent loads
-// (memory-level parallelism), and the LDS holds only D BG tiles.  Integer (60-bit) and FP64 targets are separate
-// grid segments with their own batch tile (BGI, BGF), as in k_hmacm.
-template <int LOGP, int BG, int BS, int CG, bool FP>
-__device__ __forceinline__ void hfuse2_body(u64 *lds, u64 *ltw, PolyArr X1, const u64 *__restrict__ E,
-                                            const int *__restrict__ zl, const HFuseKids &ch, int B, int l, int K,
-                                            int logN, const DevPrime &pr, const TwTables &tt, int I, int kI, int chunk,
-                                            int b0, const u64 *__restrict__ cji, const u64 *__restrict__ psipow)
-{
-    constexpr int P = 1 << LOGP, EPT = 8, TPT = P / EPT, PAIRS = P / 2, THREADS = PAIRS * BS, BT = BG / BS;
-    constexpr int LD = hfuse_ld(LOGP), CONC = THREADS / TPT, D = CONC / BG > 0 ? CONC / BG : 1;
-    static_assert(THREADS % TPT == 0 && BG % BS == 0, "thread layout");
-    const u64 N = 1ull << logN, base = (u64)chunk << LOGP;
-    const int nb = min(BG, B - b0);
-    const int nk = ch.n;
-    auto addr_of = [](int tl, int x) { return tl * LD + x + (x >> 3); };
-    {  // the chunk's pass-B twiddles
-        const u64 R = 1ull << (logN - LOGP);
-        const ulonglong2 *tw = tt.b + ((u64)kI << logN);
-        const double *twf = tt.fb + ((u64)kI << logN);
-        for (int k = threadIdx.x; k < P - 1; k += THREADS) {
-            const int st = 31 - __clz(k + 1), i = k + 1 - (1 << st);
-            const u64 gi = R * ((1ull << st) - 1) + (u64)i * R + (u64)chunk;
-            if constexpr (FP) ltw[k] = (u64)__double_as_longlong(twf[gi]);
-            else {
-                const ulonglong2 w = tw[gi];
-                ltw[2 * k] = w.x;
-                ltw[2 * k + 1] = w.y;
-            }
-        }
-    }
-    const int pp = (int)threadIdx.x % PAIRS, bs = (int)threadIdx.x / PAIRS;
-    const u64 s0 = base + 2 * pp;
-    const bool zeros = zl[0] != 0;
-    const u64 *pp_pow = psipow + ((u64)kI << (logN + 1));
-    const u64 q = pr.q, two_q = 2 * q;
-    u64 kc[CG];
-    bool sw[CG];
-    double f[FP ? CG : 1][FP ? BT : 1][4];
-    U128 a[FP ? 1 : CG][FP ? 1 : BT][4];
-#pragma unroll
-    for (int c2 = 0; c2 < CG; ++c2) {  // output pairs and the sign-mask terms W KW (source order)
-        const HChild &cc = ch.c[c2 < nk ? c2 : 0];
-        const u32 t = galois_src((u32)s0, cc.einv, logN);
-        kc[c2] = t & ~1u;
-        sw[c2] = t & 1;
-        const ulonglong2 w = *(const ulonglong2 *)(cc.W + ((u64)kI << logN) + kc[c2]);
-        const ulonglong2 m0 = *(const ulonglong2 *)(cc.KW + ((u64)I << logN) + kc[c2]);
-        const ulonglong2 m1 = *(const ulonglong2 *)(cc.KW + ((u64)(l + 1 + I) << logN) + kc[c2]);
-        if constexpr (FP) {
-            double wk[4] = {fp_mulmod(u2d(w.x), u2d(m0.x), pr.qd, pr.qinv), fp_mulmod(u2d(w.y), u2d(m0.y), pr.qd, pr.qinv),
-                            fp_mulmod(u2d(w.x), u2d(m1.x), pr.qd, pr.qinv), fp_mulmod(u2d(w.y), u2d(m1.y), pr.qd, pr.qinv)};
-            if (sw[c2]) {
-                double x = wk[0]; wk[0] = wk[1]; wk[1] = x;
-                x = wk[2]; wk[2] = wk[3]; wk[3] = x;
-            }
-#pragma unroll
-            for (int tb = 0; tb < BT; ++tb)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) f[c2][tb][r] = wk[r];
-        } else {
-            u64 wk[4] = {mulmod(w.x, m0.x, pr), mulmod(w.y, m0.y, pr), mulmod(w.x, m1.x, pr), mulmod(w.y, m1.y, pr)};
-            if (sw[c2]) {
-                u64 x = wk[0]; wk[0] = wk[1]; wk[1] = x;
-                x = wk[2]; wk[2] = wk[3]; wk[3] = x;
-            }
-#pragma unroll
-            for (int tb = 0; tb < BT; ++tb)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) a[c2][tb][r] = U128{wk[r], 0};
-        }
-    }
-    const LdsTw twg{ltw};
-    for (int J0 = 0; J0 < l; J0 += D) {
-        // stage the D BG tiles of digits J0 .. J0 + D - 1 (16-B loads), J == I from the node's NTT-form c1
-        for (int w = threadIdx.x; w < D * BG * PAIRS; w += THREADS) {
-            const int tl = w / PAIRS, p2 = w % PAIRS, J = J0 + tl / BG, bb = tl % BG;
-            if (J >= l || bb >= nb) continue;
-            const int b = b0 + bb;
-            const u64 *src = J == I ? X1.p + (u64)b * X1.sb + ((u64)J << logN)
-                                    : E + (((u64)((b * (l + 1) + I) * l + J)) << logN);
-            ulonglong2 v = *(const ulonglong2 *)(src + base + 2 * p2);
-            if constexpr (FP) {
-                if (J == I) v = ulonglong2{(u64)__double_as_longlong(u2d(v.x)), (u64)__double_as_longlong(u2d(v.y))};
-            }
-            lds[addr_of(tl, 2 * p2)] = v.x;
-            lds[addr_of(tl, 2 * p2 + 1)] = v.y;
-        }
-        __syncthreads();
-        {  // their pass B, one transform per TPT threads
-            const int tl = (int)threadIdx.x / TPT, ts = (int)threadIdx.x % TPT;
-            const int J = J0 + tl / BG;
-            const bool act = tl < D * BG && J < l && J != I && tl % BG < nb;
-            auto addr = [tl](int x) { return tl * LD + x + (x >> 3); };
-            if constexpr (LOGP <= 6) {
-                if (act) ntt_round_g<LOGP, 0, 3, EPT, false, FP, false>(lds, addr, ts, twg, pr, nullptr);
-                __syncthreads();
-                if (act) ntt_round_g<LOGP, 3, LOGP, EPT, false, FP, false>(lds, addr, ts, twg, pr, nullptr);
-            } else {
-                if (act) ntt_round_g<LOGP, 0, 3, EPT, false, FP, false>(lds, addr, ts, twg, pr, nullptr);
-                __syncthreads();
-                if (act) ntt_round_g<LOGP, 3, 6, EPT, false, FP, false>(lds, addr, ts, twg, pr, nullptr);
-                __syncthreads();
-                if (act) ntt_round_g<LOGP, 6, LOGP, EPT, false, FP, false>(lds, addr, ts, twg, pr, nullptr);
-            }
-            __syncthreads();
-        }
-#pragma unroll
-        for (int j = 0; j < D; ++j) {
-            const int J = J0 + j;
-            if (J >= l) break;
-            ulonglong2 kk[CG][2];  // the CG children's key words of digit J, both polys: independent loads
-#pragma unroll
-            for (int c2 = 0; c2 < CG; ++c2) {
-                if (c2 < nk) {
-                    const u64 *kp = ch.c[c2].key + (((u64)(J * 2) * K + kI) << logN) + kc[c2];
-                    kk[c2][0] = *(const ulonglong2 *)kp;
-                    kk[c2][1] = *(const ulonglong2 *)(kp + ((u64)K << logN));
-                } else {
-                    kk[c2][0] = kk[c2][1] = ulonglong2{0, 0};
-                }
-            }
-#pragma unroll
-            for (int tb = 0; tb < BT; ++tb) {
-                const int bb = bs * BT + tb;
-                if (bb >= nb) break;
-                const int tl = j * BG + bb;
-                u64 r0 = lds[addr_of(tl, 2 * pp)], r1 = lds[addr_of(tl, 2 * pp + 1)];
-                if constexpr (!FP) {
-                    if (J != I) {  // lazy [0, 4q) -> canonical
-                        r0 = csub(csub(r0, two_q), q);
-                        r1 = csub(csub(r1, two_q), q);
-                    }
-                }
-#pragma unroll
-                for (int c2 = 0; c2 < CG; ++c2) {
-                    if (c2 >= nk) break;
-                    const u64 e0 = r0, e1 = r1;
-                    const ulonglong2 k0 = sw[c2] ? ulonglong2{kk[c2][0].y, kk[c2][0].x} : kk[c2][0];
-                    const ulonglong2 k1 = sw[c2] ? ulonglong2{kk[c2][1].y, kk[c2][1].x} : kk[c2][1];
-                    if constexpr (FP) {  // |e| < 10 q: the forward NTT's output before canonicalisation
-                        const double d0 = __longlong_as_double((long long)e0), d1 = __longlong_as_double((long long)e1);
-                        f[c2][tb][0] += fp_mulmod(d0, u2d(k0.x), pr.qd, pr.qinv);
-                        f[c2][tb][1] += fp_mulmod(d1, u2d(k0.y), pr.qd, pr.qinv);
-                        f[c2][tb][2] += fp_mulmod(d0, u2d(k1.x), pr.qd, pr.qinv);
-                        f[c2][tb][3] += fp_mulmod(d1, u2d(k1.y), pr.qd, pr.qinv);
-                    } else {
-                        mac128(a[c2][tb][0], e0, k0.x);
-                        mac128(a[c2][tb][1], e1, k0.y);
-                        mac128(a[c2][tb][2], e0, k1.x);
-                        mac128(a[c2][tb][3], e1, k1.y);
-                    }
-                }
-            }
-        }
-        __syncthreads();  // the next digits overwrite the tiles
-    }
-    if (zeros) {  // the rare zero corrections: e_J - corr at the child's output slots (kc ^ sw, kc ^ !sw), applied
-                  // after the digit loop as + (q - corr) key_J (the MAC is linear, every term exact mod q)
-        for (int J = 0; J < l; ++J) {
-            if (J == I) continue;
-            const u64 cj = cji[J * K + kI];
-#pragma unroll
-            for (int tb = 0; tb < BT; ++tb) {
-                const int bb = bs * BT + tb;
-                if (bb >= nb) break;
-                const int *z = zl + 1 + ((b0 + bb) * l + J) * (HEC_ZCAP + 1);
-                const int nz = min(z[0], HEC_ZCAP);
-                if (nz == 0) continue;
-#pragma unroll
-                for (int c2 = 0; c2 < CG; ++c2) {
-                    if (c2 >= nk) break;
-                    const u64 ko0 = kc[c2] | (u64)sw[c2], ko1 = kc[c2] | (u64)!sw[c2];
-                    const u32 elt = ch.c[c2].elt;
-                    u64 c0 = 0, c1 = 0;
-                    for (int zi = 0; zi < nz; ++zi) {
-                        u64 tt2 = ((u64)z[1 + zi] * elt) & (2 * N - 1);
-                        if (tt2 < N) continue;
-                        tt2 -= N;
-                        const u64 ex0 = ((2 * (u64)bitrev((u32)ko0, logN) + 1) * tt2) & (2 * N - 1);
-                        const u64 ex1 = ((2 * (u64)bitrev((u32)ko1, logN) + 1) * tt2) & (2 * N - 1);
-                        c0 = addmod(c0, mulmod(cj, pp_pow[ex0], pr), q);
-                        c1 = addmod(c1, mulmod(cj, pp_pow[ex1], pr), q);
-                    }
-                    if (c0 == 0 && c1 == 0) continue;
-                    const u64 n0 = c0 ? q - c0 : 0, n1 = c1 ? q - c1 : 0;
-                    const u64 *kp = ch.c[c2].key + (((u64)(J * 2) * K + kI) << logN) + kc[c2];
-                    ulonglong2 k0 = *(const ulonglong2 *)kp, k1 = *(const ulonglong2 *)(kp + ((u64)K << logN));
-                    if (sw[c2]) {
-                        k0 = ulonglong2{k0.y, k0.x};
-                        k1 = ulonglong2{k1.y, k1.x};
-                    }
-                    if constexpr (FP) {
-                        f[c2][tb][0] += fp_mulmod(u2d(n0), u2d(k0.x), pr.qd, pr.qinv);
-                        f[c2][tb][1] += fp_mulmod(u2d(n1), u2d(k0.y), pr.qd, pr.qinv);
-                        f[c2][tb][2] += fp_mulmod(u2d(n0), u2d(k1.x), pr.qd, pr.qinv);
-                        f[c2][tb][3] += fp_mulmod(u2d(n1), u2d(k1.y), pr.qd, pr.qinv);
-                    } else {
-                        mac128(a[c2][tb][0], n0, k0.x);
-                        mac128(a[c2][tb][1], n1, k0.y);
-                        mac128(a[c2][tb][2], n0, k1.x);
-                        mac128(a[c2][tb][3], n1, k1.y);
-                    }
-                }
-            }
-        }
-    }
-#pragma unroll
-    for (int c2 = 0; c2 < CG; ++c2) {
-        if (c2 >= nk) break;
-        const HChild &cc = ch.c[c2];
-#pragma unroll
-        for (int tb = 0; tb < BT; ++tb) {
-            const int bb = bs * BT + tb;
-            if (bb >= nb) break;
-            const int b = b0 + bb;
-            u64 r[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                if constexpr (FP) r[i] = fp_canon(f[c2][tb][i], pr.qd, pr.qinv);
-                else r[i] = barrett128(a[c2][tb][i].lo, a[c2][tb][i].hi, q, pr.r0, pr.r1);
-            }
-            u64 *o0 = cc.ACC + (((u64)((b * 2 + 0) * (l + 1) + I)) << logN) + kc[c2];
-            u64 *o1 = cc.ACC + (((u64)((b * 2 + 1) * (l + 1) + I)) << logN) + kc[c2];
-            *(ulonglong2 *)o0 = sw[c2] ? ulonglong2{r[1], r[0]} : ulonglong2{r[0], r[1]};
-            *(ulonglong2 *)o1 = sw[c2] ? ulonglong2{r[3], r[2]} : ulonglong2{r[2], r[3]};
-        }
-    }
-}
-
-// CLS 0: both segments in one launch; 1: an FP64-only launch over Imap[nint, nI); 2: an integer-only launch
-// (separate launches give the FP64 kernel its own register budget)
-template <int LOGP, int BGF, int BGI, int BS, int CG, int CLS = 0>
-__global__ void __launch_bounds__((1 << LOGP) / 2 * BS)
-    k_hfuse2(PolyArr X1, const u64 *__restrict__ E, const int *__restrict__ zl, const HFuseKids ch, int B, int l, int K,
-             int logN, const DevPrime *__restrict__ primes, TwTables tt, const int *__restrict__ Imap, int nI, int nint,
-             const u64 *__restrict__ cji, const u64 *__restrict__ psipow, int wsplit)
-{
-    constexpr int P = 1 << LOGP;
-    extern __shared__ u64 hfuse_lds[];  // [2 P] twiddles, then the staged tiles
-    u64 *ltw = hfuse_lds, *lds = hfuse_lds + 2 * P;
-    const int X = 1 << (logN - LOGP);
-    const bool integer = CLS == 2 || (CLS == 0 && (int)blockIdx.x < wsplit);
-    const int bg = integer ? BGI : BGF, nbg = (B + bg - 1) / bg;
-    const int w = (integer || CLS == 1) ? blockIdx.x : blockIdx.x - wsplit;
-    const int g8 = w & 7, rest = w >> 3, bgi = rest % nbg, G = (rest / nbg) * 8 + g8;
-    if (G >= X * (integer ? nint : nI - nint)) return;
-    const int yi = G / X + (integer ? 0 : nint), chunk = G % X;
-    const int I = Imap[yi];
-    const int kI = I == l ? K - 1 : I;
-    const DevPrime pr = primes[kI];
-    if constexpr (CLS == 2)
-        hfuse2_body<LOGP, BGI, BS, CG, false>(lds, ltw, X1, E, zl, ch, B, l, K, logN, pr, tt, I, kI, chunk, bgi * BGI, cji,
-                                              psipow);
-    else if constexpr (CLS == 1)
-        hfuse2_body<LOGP, BGF, BS, CG, true>(lds, ltw, X1, E, zl, ch, B, l, K, logN, pr, tt, I, kI, chunk, bgi * BGF, cji,
-                                             psipow);
-    else if (integer)
-        hfuse2_body<LOGP, BGI, BS, CG, false>(lds, ltw, X1, E, zl, ch, B, l, K, logN, pr, tt, I, kI, chunk, bgi * BGI, cji,
-                                              psipow);
-    else
-        hfuse2_body<LOGP, BGF, BS, CG, true>(lds, ltw, X1, E, zl, ch, B, l, K, logN, pr, tt, I, kI, chunk, bgi * BGF, cji,
-                                             psipow);
-}
-
-template <int LOGP, int BGF, int BGI, int BS, int CG>
-static void launch_hfuse2(Ctx &c, PolyArr X1, const u64 *E, const int *zl, const HChildSpec *kids, int nkids, int B,
-                          int l)
-{
-    constexpr int P = 1 << LOGP, THREADS = P / 2 * BS, CONC = THREADS / (P / 8);
-    for (int k0 = 0; k0 < nkids; k0 += CG) {  // CG children per launch
-        HFuseKids ch{};
-        ch.n = std::min(CG, nkids - k0);
-        for (int q = 0; q < ch.n; ++q) {
-            const HChildSpec &k = kids[k0 + q];
-            ch.c[q] = HChild{k.elt, k.einv, k.key, k.W, k.ACC, k.KW};
-        }
-        const int nint = c.imap_nint[l], X = (int)(c.N >> LOGP);
-        const int gI = (X * nint + 7) / 8 * 8, gF = (X * (l + 1 - nint) + 7) / 8 * 8;
-        const int wsplit = gI * ((B + BGI - 1) / BGI), total = wsplit + gF * ((B + BGF - 1) / BGF);
-        const int tiles = std::max(CONC / BGF, 1) * BGF > std::max(CONC / BGI, 1) * BGI ? std::max(CONC / BGF, 1) * BGF
-                                                                                         : std::max(CONC / BGI, 1) * BGI;
-        const std::size_t shm = (std::size_t)(2 * P + tiles * hfuse_ld(LOGP)) * sizeof(u64);
-        const TwTables fwd{c.tw, c.twb, c.twf, c.twbf};
-        if (c.hfuse == 3) {  // the integer and FP64 segments as two launches
-            if (wsplit)
-                k_hfuse2<LOGP, BGF, BGI, BS, CG, 2><<<dim3((unsigned)wsplit), THREADS, shm, c.stream>>>(
-                    X1, E, zl, ch, B, l, (int)c.K, c.logN, c.primes, fwd, c.imap_at(l), l + 1, nint, c.cji, c.psipow,
-                    wsplit);
-            k_hfuse2<LOGP, BGF, BGI, BS, CG, 1><<<dim3((unsigned)(total - wsplit)), THREADS, shm, c.stream>>>(
-                X1, E, zl, ch, B, l, (int)c.K, c.logN, c.primes, fwd, c.imap_at(l), l + 1, nint, c.cji, c.psipow, wsplit);
-        } else {
-            k_hfuse2<LOGP, BGF, BGI, BS, CG><<<dim3((unsigned)total), THREADS, shm, c.stream>>>(
-                X1, E, zl, ch, B, l, (int)c.K, c.logN, c.primes, fwd, c.imap_at(l), l + 1, nint, c.cji, c.psipow, wsplit);
-        }
-        HEC_HIP(hipGetLastError());
-    }
-}
-
-void hoisted_mac_fused(Ctx &c, PolyArr X1, const u64 *E, const int *zl, const HChildSpec *kids, int nkids, int B, int l)
-{
-    if (nkids < 1 || nkids > HFUSE_MAXK) throw std::invalid_argument("hoisted_mac_fused: children per launch");
-    if (l > HEC_MAXL) throw std::invalid_argument("too many limbs");
-    if (c.hfuse >= 2) {  // digit-outer k_hfuse2: <LOGP, FP64 batch tile, integer batch tile, batch sets, children>
-        switch (c.logN) {
-        case 10: case 11: launch_hfuse2<5, 4, 4, 4, 4>(c, X1, E, zl, kids, nkids, B, l); break;
-        case 12: case 13: launch_hfuse2<6, 4, 2, 2, 4>(c, X1, E, zl, kids, nkids, B, l); break;
-        case 14: case 15:
-            if (c.hfuse_cg == 2) launch_hfuse2<7, 4, 2, 2, 2>(c, X1, E, zl, kids, nkids, B, l);
-            else if (c.hfuse_bg == 2) launch_hfuse2<7, 2, 2, 2, 4>(c, X1, E, zl, kids, nkids, B, l);
-            else launch_hfuse2<7, 4, 2, 2, 4>(c, X1, E, zl, kids, nkids, B, l);
-            break;
-        case 16: launch_hfuse2<8, 2, 2, 2, 4>(c, X1, E, zl, kids, nkids, B, l); break;
-        default: throw std::invalid_argument("poly_modulus_degree must be 2^10 .. 2^16");
-        }
-        return;
-    }
-    // <LOGP, batch entries per block, batch sets per block>: LDS = l BG hfuse_ld(LOGP) words (the largest static
-    // shape is HEC_MAXL digits), blocks of P / 2 x BS threads
-    switch (c.logN) {
-    case 10: launch_hfuse<5, 4, 4>(c, X1, E, zl, kids, nkids, B, l); break;
-    case 11: launch_hfuse<5, 4, 4>(c, X1, E, zl, kids, nkids, B, l); break;
-    case 12: launch_hfuse<6, 4, 2>(c, X1, E, zl, kids, nkids, B, l); break;
-    case 13: launch_hfuse<6, 4, 2>(c, X1, E, zl, kids, nkids, B, l); break;
-    case 14: launch_hfuse<7, 2, 2>(c, X1, E, zl, kids, nkids, B, l); break;
-    case 15:
-        if (c.hfuse_bg == 4) launch_hfuse<7, 4, 2>(c, X1, E, zl, kids, nkids, B, l);
-        else if (c.hfuse_bg == 1) launch_hfuse<7, 1, 1>(c, X1, E, zl, kids, nkids, B, l);
-        else launch_hfuse<7, 2, 2>(c, X1, E, zl, kids, nkids, B, l);
-        break;
-    case 16: launch_hfuse<8, 1, 1>(c, X1, E, zl, kids, nkids, B, l); break;
-    default: throw std::invalid_argument("poly_modulus_degree must be 2^10 .. 2^16");
-    }
 }
 
 void fan_divide_round(Ctx &c, const u64 *Y, u64 ysb, u64 ysk, u64 *Z, int B, int nk, int nl, int last_idx)
@@ -2166,30 +1527,25 @@ void fan_divide_round(Ctx &c, const u64 *Y, u64 ysb, u64 ysk, u64 *Z, int B, int
 // Grid (R / NSEG, l + 1, B): blocks of one (chunk block, I) for different b are R/NSEG * (l+1) apart,
 // a multiple of 8 for logN >= 14, so they run on one XCD and share its L2 copy of the key chunk.
 // The integer target primes come first in Imap: their blocks are the slowest, so they start first.
-// k_bmac LDS segment stride (words): P data words + P/8 pad words + 8
-constexpr int bmac_ld(int logp) { return (1 << logp) + (1 << logp) / 8 + 8; }
+// k_bmac LDS segment stride (words): P data words + P/8 (one pad word per 16 elements, and spare)
+constexpr int bmac_ld(int logp) { return (1 << logp) + (1 << logp) / 8; }
 
-template <int LOGP, int NSEG, int EPT, bool FP, int KEYM>
+template <int LOGP, int NSEG, int EPT, bool FP>
 __device__ __forceinline__ void bmac_body(u64 *lds, u64 *ltw, PolyArr T, const u64 *__restrict__ E, const u64 *__restrict__ key,
                                           u64 *__restrict__ ACC, const TwTables &tt, const DevPrime &pr, int I, int kI,
                                           int b, int xb, int logN, int l, int K, u32 elt)
 {
-    // KEYM 3: keys as 1, with the segment-major lane layout below (lanes = consecutive threads of one chunk,
-    // stride P + P/8, one pad word per 16): the staging writes and the rounds' reads and writes at about half the
-    // bank-conflict cycles of the chunk-interleaved layout (tools/lds_banks.py)
-    constexpr bool LAY = KEYM == 3;
-    constexpr int KM = LAY ? 1 : KEYM;
-    constexpr int P = 1 << LOGP, THREADS = NSEG * P / EPT, LD = LAY ? P + P / 8 : bmac_ld(LOGP), TWS = 2 * P + 2;
+    // segment-major lane layout: the P / EPT threads of one chunk are consecutive lanes, rows of P + P/8 words
+    // with one pad word per 16 elements.  The staging writes and the rounds' reads and writes then take about
+    // half the LDS bank-conflict cycles of the chunk-interleaved layout (tools/lds_banks.py; -7 % kernel time)
+    constexpr int P = 1 << LOGP, THREADS = NSEG * P / EPT, LD = bmac_ld(LOGP), TWS = 2 * P + 2;
     const u64 N = 1ull << logN;
     const int seg0 = xb * NSEG;
     const u64 base = (u64)seg0 << LOGP;
     const ulonglong2 *tw = tt.b + ((u64)kI << logN);
     const double *twf = tt.fb + ((u64)kI << logN);
-    const int ts = LAY ? (int)threadIdx.x % (P / EPT) : (int)threadIdx.x / NSEG;
-    const int sg = LAY ? (int)threadIdx.x / (P / EPT) : (int)threadIdx.x % NSEG;
-    // one pad word per 8 elements plus a segment stride of P + P/8 + 8: the three round access patterns
-    // and the staging writes go from 4-way to <= 2-way LDS bank conflicts (64 banks, 32-lane halves)
-    auto addr = [sg](int x) { return sg * LD + x + (LAY ? (x >> 4) : (x >> 3)); };
+    const int ts = (int)threadIdx.x % (P / EPT), sg = (int)threadIdx.x / (P / EPT);
+    auto addr = [sg](int x) { return sg * LD + x + (x >> 4); };
     const u64 R = 1ull << (logN - LOGP);
     // the pass-B twiddles of a chunk do not depend on the digit J: stage the block's (NSEG chunks x
     // (P - 1) entries) once into LDS, rows padded to TWS words (bank spread), lanes = consecutive chunks
@@ -2227,8 +1583,6 @@ __device__ __forceinline__ void bmac_body(u64 *lds, u64 *ltw, PolyArr T, const u
             k0[e] = a.x; k0[e + 1] = a.y; k1[e] = c.x; k1[e + 1] = c.y;
         }
     };
-    u64 kc0[KM == 2 ? EPT : 1], kc1[KM == 2 ? EPT : 1];
-    if constexpr (KM == 2) load_keys(0, kc0, kc1);
     // digit tiles move as 16-B pairs: pair w = threadIdx.x + e THREADS holds block elements 2w, 2w + 1
     u64 nx[EPT];
     auto load_tile = [&](int J) {
@@ -2261,16 +1615,11 @@ __device__ __forceinline__ void bmac_body(u64 *lds, u64 *ltw, PolyArr T, const u
             if constexpr (FP) {
                 if (!ntt) v = (u64)__double_as_longlong(u2d(v));  // canonical integer target
             }
-            lds[(li / P) * LD + (li % P) + (LAY ? ((li % P) >> 4) : ((li % P) >> 3))] = v;
+            lds[(li / P) * LD + (li % P) + ((li % P) >> 4)] = v;
         }
         if (J + 1 < l) load_tile(J + 1);
         u64 k0[EPT], k1[EPT];
-        if constexpr (KM == 2) {  // keys of digit J were loaded one iteration ago; issue J + 1's now
-#pragma unroll
-            for (int e = 0; e < EPT; ++e) { k0[e] = kc0[e]; k1[e] = kc1[e]; }
-            if (J + 1 < l) load_keys(J + 1, kc0, kc1);
-        }
-        if constexpr (KM == 1) load_keys(J, k0, k1);
+        load_keys(J, k0, k1);  // before the rounds: their latency hides behind the LDS work
         __syncthreads();
         u64 v[EPT];
         if (ntt) {
@@ -2290,7 +1639,6 @@ __device__ __forceinline__ void bmac_body(u64 *lds, u64 *ltw, PolyArr T, const u
 #pragma unroll
             for (int e = 0; e < EPT; ++e) v[e] = lds[addr(ts * EPT + e)];
         }
-        if constexpr (KM == 0) load_keys(J, k0, k1);
 #pragma unroll
         for (int e = 0; e < EPT; ++e) {
             if constexpr (FP) {
@@ -2320,10 +1668,9 @@ __device__ __forceinline__ void bmac_body(u64 *lds, u64 *ltw, PolyArr T, const u
     }
 }
 
-// one launch: blockIdx.y < nint -> integer target primes, the rest FP64 (blocks of both kinds overlap)
-// CLS 0: Imap lists every target prime, the first nint integer ones (per-block branch); CLS 1 / 2: an
-// FP64-only / integer-only launch over the nI primes of Imap (FP64-only: 162 VGPRs, 3 waves/SIMD).
-template <int LOGP, int NSEG, int EPT, int KEYM, int CLS>
+// one launch: Imap lists every target prime, the first nint integer ones (per-block branch; blocks of both
+// kinds overlap)
+template <int LOGP, int NSEG, int EPT>
 __global__ void __launch_bounds__(NSEG *(1 << LOGP) / EPT)
     k_bmac(PolyArr T, const u64 *__restrict__ E, const u64 *__restrict__ key, u64 *__restrict__ ACC, TwTables tt,
            const DevPrime *__restrict__ primes, const int *__restrict__ Imap, int nI, int logN, int l, int K,
@@ -2342,14 +1689,10 @@ __global__ void __launch_bounds__(NSEG *(1 << LOGP) / EPT)
     const int I = Imap[yi];
     const int kI = I == l ? K - 1 : I;
     const DevPrime pr = primes[kI];
-    if constexpr (CLS == 1)
-        bmac_body<LOGP, NSEG, EPT, true, KEYM>(lds, ltw, T, E, key, ACC, tt, pr, I, kI, b, xb, logN, l, K, elt);
-    else if constexpr (CLS == 2)
-        bmac_body<LOGP, NSEG, EPT, false, KEYM>(lds, ltw, T, E, key, ACC, tt, pr, I, kI, b, xb, logN, l, K, elt);
-    else if (yi < nint)
-        bmac_body<LOGP, NSEG, EPT, false, KEYM>(lds, ltw, T, E, key, ACC, tt, pr, I, kI, b, xb, logN, l, K, elt);
+    if (yi < nint)
+        bmac_body<LOGP, NSEG, EPT, false>(lds, ltw, T, E, key, ACC, tt, pr, I, kI, b, xb, logN, l, K, elt);
     else
-        bmac_body<LOGP, NSEG, EPT, true, KEYM>(lds, ltw, T, E, key, ACC, tt, pr, I, kI, b, xb, logN, l, K, elt);
+        bmac_body<LOGP, NSEG, EPT, true>(lds, ltw, T, E, key, ACC, tt, pr, I, kI, b, xb, logN, l, K, elt);
 }
 
 template <int LOGR, int LOGC, int NA, int NB2>
@@ -2373,18 +1716,9 @@ static void run_modup_fused(Ctx &c, const u64 *D, u64 *E, PolyArr T, const u64 *
     // (2b)+(3) fused; integer target primes first (slowest blocks start first)
     constexpr int TB = NB2 * C / EPT;
     constexpr int X = R / NB2;
-    auto launch = [&](auto cls, hipStream_t st, const int *Il, int nI) {
-        constexpr int CL = decltype(cls)::value;
-        const int gpad = (X * nI + 7) / 8 * 8;
-        const dim3 grid(gpad * B);
-        switch (c.bmac_keys) {  // key loads: 0 after the rounds, 1 before them, 2 one digit ahead; 3 = 1 + LDS layout
-        case 0: k_bmac<LOGC, NB2, EPT, 0, CL><<<grid, TB, 0, st>>>(T, E, key, ACC, fwd, c.primes, Il, nI, c.logN, l, (int)c.K, nint, gpad, elt); break;
-        case 1: k_bmac<LOGC, NB2, EPT, 1, CL><<<grid, TB, 0, st>>>(T, E, key, ACC, fwd, c.primes, Il, nI, c.logN, l, (int)c.K, nint, gpad, elt); break;
-        case 3: k_bmac<LOGC, NB2, EPT, 3, CL><<<grid, TB, 0, st>>>(T, E, key, ACC, fwd, c.primes, Il, nI, c.logN, l, (int)c.K, nint, gpad, elt); break;
-        default: k_bmac<LOGC, NB2, EPT, 2, CL><<<grid, TB, 0, st>>>(T, E, key, ACC, fwd, c.primes, Il, nI, c.logN, l, (int)c.K, nint, gpad, elt); break;
-        }
-    };
-    launch(std::integral_constant<int, 0>{}, c.stream, dm, l + 1);
+    const int gpad = (X * (l + 1) + 7) / 8 * 8;
+    k_bmac<LOGC, NB2, EPT><<<dim3(gpad * B), TB, 0, c.stream>>>(T, E, key, ACC, fwd, c.primes, dm, l + 1, c.logN, l,
+                                                                (int)c.K, nint, gpad, elt);
     HEC_HIP(hipGetLastError());
 }
 

@@ -1,7 +1,7 @@
 """LDS bank-conflict model for the engine's 8-byte LDS accesses (MI355X_MICROARCH.md §LDS): ds_read_b64 = 2 groups of
 32 lanes, bank of dword d = d mod 64; ds_write_b64 = 4 groups of 16 contiguous lanes, bank = d mod 32.  Extra
 cycles per instruction = sum over groups of (max distinct dwords on one bank - 1).  Used to choose the tile padding
-of k_bmac / k_hfuse2 (development tool; the counters are the judge: SQ_LDS_BANK_CONFLICT)."""
+of k_bmac (development tool; the counters are the judge: SQ_LDS_BANK_CONFLICT)."""
 from collections import defaultdict
 
 

@@ -7,7 +7,8 @@ bytes (calibrated for 16 B/lane); read bytes = 2 x FETCH_SIZE (kB = 1024 B).  WR
 stores.  Kernels with 8-B/lane accesses (k_ntt, k_fan, k_tensor_multi) are outside that calibration: their
 files also carry the raw counters and the ratio to the kernel's algorithmic bytes (bench.py's per-kernel
 table) so the factor can be read off a known byte count.
-usage: python tools/pmc_summary.py <fetch.csv> <write.csv> <batch> <logN> <level> <n> <tag> <cmd> <kernel>..."""
+usage: python tools/pmc_summary.py <fetch.csv> <write.csv> <batch> <logN> <level> <n> <tag> <cmd> <kernel>...
+PMC_VARIANT=ctpt in the environment tags the files as the ct x pt matvec's (pmc_<kernel>_B<B>_ctpt.json)."""
 import csv
 import json
 import os
@@ -25,6 +26,7 @@ def per_dispatch(path, kernel, counter):
 
 
 fetch_csv, write_csv, B, logN, level, n, tag, cmd = sys.argv[1:9]
+variant = os.environ.get("PMC_VARIANT", "ctct")
 outdir = os.path.dirname(os.path.abspath(fetch_csv))
 for kernel in sys.argv[9:]:
     f = per_dispatch(fetch_csv, kernel, "FETCH_SIZE")
@@ -35,7 +37,7 @@ for kernel in sys.argv[9:]:
     wk = sum(w.values()) / len(w)
     res = {
         "kernel": kernel, "batch": int(B), "logN": int(logN), "level": int(level), "n": int(n),
-        "dispatches": len(f),
+        "variant": variant, "dispatches": len(f),
         "FETCH_SIZE_kB_per_dispatch": round(fk, 1), "WRITE_SIZE_kB_per_dispatch": round(wk, 1),
         "FETCH_SIZE_kB_per_step": round(sum(f.values()), 1), "WRITE_SIZE_kB_per_step": round(sum(w.values()), 1),
         "correction": "read bytes = 2 x FETCH_SIZE (gfx950 tallies coalesced streaming reads at half their bytes); "
@@ -44,6 +46,6 @@ for kernel in sys.argv[9:]:
         "traffic_bytes_per_step": int(round((2 * sum(f.values()) + sum(w.values())) * 1024)),
         "command": cmd,
     }
-    path = os.path.join(outdir, f"pmc_{kernel}_B{B}.json")
+    path = os.path.join(outdir, f"pmc_{kernel}_B{B}{'' if variant == 'ctct' else '_' + variant}.json")
     json.dump(res, open(path, "w"), indent=1)
     print(json.dumps(res))
