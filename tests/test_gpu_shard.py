@@ -92,3 +92,22 @@ def test_cabi_sharded_matvec_one_rank_rccl(env, hecdna):
         assert np.array_equal(q.download(), r.download())
     with pytest.raises(hecdna.InvalidArgument, match="already"):
         ctx.comm_init(0, 1, hecdna.comm_unique_id())
+
+
+def test_cabi_sharded_null_planned_diagonal_rejected(env, hecdna):
+    """hecdna.h contract: a rank reads only the diagonals its plan assigns and NULL is allowed for the others; a
+    NULL (None) handle for a diagonal the rank must read is an HEC_EINVAL, never a dereference.  At world 1 every
+    diagonal is planned, so any None is rejected; bench.py's sharded stage exercises None for other ranks'
+    diagonals at world > 1."""
+    e = env
+    n = 6
+    gA = [e.up(e.enc(seed=900 + j)) for j in range(n)]
+    gX = [e.up(e.enc(seed=950))]
+    for hole in (0, 3, n - 1):
+        A = list(gA)
+        A[hole] = None
+        with pytest.raises(hecdna.InvalidArgument):
+            e.ctx.matmul_diag_col_sharded(A, gX, e.rk, e.gk)
+    ref = e.ctx.matmul_diag_col(gA, gX, e.rk, e.gk)[0]           # the context is still usable
+    got = e.ctx.matmul_diag_col_sharded(gA, gX, e.rk, e.gk)[0]
+    assert np.array_equal(got.download(), ref.download())
