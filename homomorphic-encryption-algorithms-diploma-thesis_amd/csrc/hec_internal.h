@@ -89,7 +89,7 @@ struct Ctx {
     int tensor_bg = 1;             // HEC_TENSOR_BG=0: k_tensor_multi (one thread per coefficient, whole batch)
     bool hoist = true;             // HEC_HOIST=0: no hoisted mod-up in the rotation trie walk
     int hoist_min_children = 2;    // HEC_HOIST_MIN: children a trie node needs to be hoisted
-    int hmac_cfg = 1;              // HEC_HMAC=0: one hoisted MAC per child (1: sibling pairs fused, k_hmacm; 3: triples)
+    int hmac_cfg = 1;              // HEC_HMAC=0: one hoisted MAC per child (1: sibling pairs fused, k_hmacm)
     int fan_groups_moddown = 1;    // HEC_FANG="moddown,modup,hoist": target groups per k_fan source (blocks
     int fan_groups_modup = 1;      // per launch x groups; the source's inverse pass is repeated per group)
     int fan_groups_hoist = 1;

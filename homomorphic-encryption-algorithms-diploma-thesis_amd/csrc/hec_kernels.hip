@@ -1480,7 +1480,7 @@ static void launch_hmacm(Ctx &c, PolyArr X1, const u64 *E, const int *zl, const 
     HEC_HIP(hipGetLastError());
 }
 
-int hoisted_group(const Ctx &c) { return c.hmac_cfg == 3 ? 3 : c.hmac_cfg ? 2 : 1; }
+int hoisted_group(const Ctx &c) { return c.hmac_cfg ? 2 : 1; }
 
 void hoisted_mac_multi(Ctx &c, PolyArr X1, const u64 *E, const int *zl, const HChildSpec *kids, int nkids, int B,
                        int l)
@@ -1488,8 +1488,7 @@ void hoisted_mac_multi(Ctx &c, PolyArr X1, const u64 *E, const int *zl, const HC
     if (nkids < 1 || nkids > hoisted_group(c)) throw std::invalid_argument("hoisted_mac_multi: group size");
     // <FP64 batch entries, integer batch entries, children> per thread (the 1x4, 2x2, 3x2, 4x4 ...
     // shapes measured slower)
-    if (c.hmac_cfg == 3) launch_hmacm<4, 2, 3>(c, X1, E, zl, kids, nkids, B, l);  // sibling triples
-    else if (c.hmac_cfg) launch_hmacm<4, 2, 2>(c, X1, E, zl, kids, nkids, B, l);
+    if (c.hmac_cfg) launch_hmacm<4, 2, 2>(c, X1, E, zl, kids, nkids, B, l);
     else hoisted_mac(c, X1, E, kids[0].W, zl, kids[0].key, kids[0].ACC, B, l, kids[0].elt);
 }
 
