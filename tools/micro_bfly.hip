@@ -52,6 +52,22 @@ __device__ __forceinline__ u64 fpq_lazy(u64 x, u64 w, double fh, double fl, u64 
     return x * w - qhat * q;                            // Q - qhat in (0.49, 1.51)
 }
 
+// V3: the engine's Shoup product with q = 2^60 - c (c < 2^32, SEAL's 60-bit primes): hi q mod 2^64 =
+// (hi << 60) - hi c, two multiplies instead of three.  V4: V3 plus the conditional subtractions by the sign of
+// x - 2q (no VCC compare / select).
+__device__ __forceinline__ u64 shoup_c(u64 x, u64 w, u64 wq, u32 c)
+{
+    const u64 hi = mulhi64(x, wq);
+    const u64 hc = (u64)(u32)hi * c + ((u64)((u32)(hi >> 32) * c) << 32);
+    return x * w + hc - (hi << 60);
+}
+__device__ __forceinline__ u64 csub_sign(u64 x, u64 m)  // x < 2m... : x - m if x >= m, as x + (-m) then add back
+{
+    const u64 d = x - m;
+    const u64 s = (u64)((long long)d >> 63);
+    return d + (m & s);
+}
+
 template <int V>
 __global__ void __launch_bounds__(256) k_bfly(u64 *io, const u64 *tw_in, const double *twd, u64 q, int iters)
 {
@@ -78,6 +94,21 @@ __global__ void __launch_bounds__(256) k_bfly(u64 *io, const u64 *tw_in, const d
                 t = t >= two_q ? t - two_q : t;
                 X[c] = x + t;
                 Y[c] = x - t + two_q;
+            } else if constexpr (V == 3) {
+                const u64 x = X[c] >= two_q ? X[c] - two_q : X[c];
+                const u64 tt = shoup_c(Y[c], W[c], WQ[c], (u32)((1ull << 60) - q));
+                X[c] = x + tt;
+                Y[c] = x - tt + two_q;
+            } else if constexpr (V == 4) {
+                const u64 x = csub_sign(X[c], two_q);
+                const u64 tt = shoup_c(Y[c], W[c], WQ[c], (u32)((1ull << 60) - q));
+                X[c] = x + tt;
+                Y[c] = x - tt + two_q;
+            } else if constexpr (V == 5) {
+                const u64 x = csub_sign(X[c], two_q);
+                const u64 tt = shoup_lazy(Y[c], W[c], WQ[c], q);
+                X[c] = x + tt;
+                Y[c] = x - tt + two_q;
             } else if constexpr (V == 2) {
                 const u64 x = X[c] >= two_q ? X[c] - two_q : X[c];
                 const u64 t = fpq_lazy(Y[c], W[c], FH[c], FL[c], q);  // in (0.49q, 1.51q)
@@ -157,5 +188,8 @@ int main()
     run<0>("shoup (engine ct_bfly)", q, init, d_io, d_tw, d_twd, ref);
     run<1>("shoup approx-hi + q_hi", q, init, d_io, d_tw, d_twd, ref);
     run<2>("fp64 quotient", q, init, d_io, d_tw, d_twd, ref);
+    run<3>("shoup, q = 2^60 - c", q, init, d_io, d_tw, d_twd, ref);
+    run<4>("shoup, q = 2^60 - c, sign csub", q, init, d_io, d_tw, d_twd, ref);
+    run<5>("shoup, sign csub", q, init, d_io, d_tw, d_twd, ref);
     return 0;
 }
