@@ -1497,6 +1497,261 @@ void hoisted_mac_3(Ctx &c, PolyArr X1, const u64 *E, const int *zl, const HChild
     launch_hmacm<4, 2, 3>(c, X1, E, zl, kids, 3, B, l);
 }
 
+// ============================================ fused hoisted MAC: the digits' pass B in LDS + the children's MAC ==
+// k_hmacf finishes a hoisted node's mod-up NTTs (pass B of every digit E[b][I][J], J != I, which the fan-out leaves
+// in the pass-A domain) in LDS and runs the key MAC of up to HMAC_MAX_CHILDREN sibling rotations from there, so the
+// digits cross HBM once more (read here) instead of three or more times (pass B read + write, one read per sibling
+// pair of k_hmacm).  A block owns one pass-B chunk (P = 2^LOGP contiguous source positions) of one target prime I
+// for BT batch entries (one wave at P = 128, BT = 1) and keeps all l digit tiles of its chunk in LDS (l BT (P + P/16)
+// words: 10.9 KB at cfg3).  A thread owns one source pair of one batch entry and loops over the children with one
+// child's four accumulators live, so the kernel needs few registers.  (The fused kernels deleted earlier in round 3,
+// DESIGN.md §10, kept several children's accumulators or batch tiles per thread and ran at 1-2 waves/SIMD.)
+// The MAC is k_hmacm's: the child's output pair is gal_c^-1(s) (keys, W, KW and ACC gathered there, all inside the
+// child's output chunk), the sign-mask term W KW starts the accumulators, the rare zero corrections follow the digit
+// loop.  FP64 targets keep the pass-B outputs as lazy doubles (|v| < 10 q, fp_mulmod's range); the 60-bit targets
+// keep [0, 4 q) words in 128-bit sums (l products < 2^126).
+template <int LOGP, int BT, bool FP>
+__device__ __forceinline__ void hmacf_body(u64 *ltw, u64 *lds, PolyArr X1, const u64 *__restrict__ E,
+                                           const int *__restrict__ zl, const HChildren<HMAC_MAX_CHILDREN> &ch, int B,
+                                           int l, int K, int logN, const DevPrime &pr, const TwTables &tt, int I, int kI,
+                                           int chunk, int b0, const u64 *__restrict__ cji,
+                                           const u64 *__restrict__ psipow)
+{
+    constexpr int P = 1 << LOGP, PAIRS = P / 2, THREADS = PAIRS * BT, LD = P + P / 16, EPT = 8, TPT = P / EPT;
+    constexpr int CONC = THREADS / TPT;
+    const u64 N = 1ull << logN, base = (u64)chunk << LOGP;
+    const int nb = min(BT, B - b0);
+    {  // the chunk's pass-B twiddles (k_bmac's staging, one chunk)
+        const u64 R = 1ull << (logN - LOGP);
+        const ulonglong2 *tw = tt.b + ((u64)kI << logN);
+        const double *twf = tt.fb + ((u64)kI << logN);
+        for (int k = threadIdx.x; k < P - 1; k += THREADS) {
+            const int st = 31 - __clz(k + 1), i = k + 1 - (1 << st);
+            const u64 gi = R * ((1ull << st) - 1) + (u64)i * R + (u64)chunk;
+            if constexpr (FP) ltw[k] = (u64)__double_as_longlong(twf[gi]);
+            else {
+                const ulonglong2 w = tw[gi];
+                ltw[2 * k] = w.x;
+                ltw[2 * k + 1] = w.y;
+            }
+        }
+    }
+    // every digit tile of the chunk: J != I from E (pass-A domain; FP64 targets hold double bits), J == I the node's
+    // NTT-form c1 (SEAL's reuse of the input), canonical
+#pragma unroll 4
+    for (int t = threadIdx.x; t < BT * l * PAIRS; t += THREADS) {
+        const int p2 = t % PAIRS, tile = t / PAIRS, bb = tile / l, J = tile % l;
+        if (bb >= nb) continue;
+        const int b = b0 + bb;
+        const u64 *src = J == I ? X1.p + (u64)b * X1.sb + ((u64)J << logN)
+                                : E + (((u64)((b * (l + 1) + I) * l + J)) << logN);
+        ulonglong2 v = *(const ulonglong2 *)(src + base + 2 * p2);
+        if constexpr (FP) {
+            if (J == I) v = ulonglong2{(u64)__double_as_longlong(u2d(v.x)), (u64)__double_as_longlong(u2d(v.y))};
+        }
+        u64 *d = lds + tile * LD + 2 * p2 + (p2 >> 3);
+        d[0] = v.x;
+        d[1] = v.y;
+    }
+    __syncthreads();
+    const LdsTw twg{ltw};
+    for (int t0 = 0; t0 < BT * l; t0 += CONC) {  // pass B of the J != I tiles, CONC transforms at a time
+        const int tile = t0 + (int)threadIdx.x / TPT, ts = (int)threadIdx.x % TPT;
+        const bool act = tile < BT * l && tile / l < nb && tile % l != I;
+        const int r0 = act ? tile * LD : 0;
+        auto addr = [r0](int x) { return r0 + x + (x >> 4); };
+        static_assert(LOGP >= 5 && LOGP <= 8, "pass-B sizes 2^5 .. 2^8");
+        if constexpr (LOGP <= 6) {
+            if (act) ntt_round_g<LOGP, 0, 3, EPT, false, FP, false>(lds, addr, ts, twg, pr, nullptr);
+            __syncthreads();
+            if (act) ntt_round_g<LOGP, 3, LOGP, EPT, false, FP, false>(lds, addr, ts, twg, pr, nullptr);
+        } else {
+            if (act) ntt_round_g<LOGP, 0, 3, EPT, false, FP, false>(lds, addr, ts, twg, pr, nullptr);
+            __syncthreads();
+            if (act) ntt_round_g<LOGP, 3, 6, EPT, false, FP, false>(lds, addr, ts, twg, pr, nullptr);
+            __syncthreads();
+            if (act) ntt_round_g<LOGP, 6, LOGP, EPT, false, FP, false>(lds, addr, ts, twg, pr, nullptr);
+        }
+        __syncthreads();
+    }
+    const int p = (int)threadIdx.x % PAIRS, bb = (int)threadIdx.x / PAIRS;
+    if (bb >= nb) return;  // after the last barrier
+    const int b = b0 + bb;
+    const u64 s0 = base + 2 * p;
+    const u64 *ev = lds + bb * l * LD + 2 * p + (p >> 3);  // digit J of this source pair: ev[J LD], ev[J LD + 1]
+    const bool zeros = zl[0] != 0;
+    const u64 *pp = psipow + ((u64)kI << (logN + 1));
+    for (int q = 0; q < ch.n; ++q) {
+        const HChild &cc = ch.c[q];
+        const u32 t = galois_src((u32)s0, cc.einv, logN);
+        const u64 kc = t & ~1u;
+        const bool sw = t & 1;
+        const ulonglong2 wv = *(const ulonglong2 *)(cc.W + ((u64)kI << logN) + kc);
+        const ulonglong2 m0 = *(const ulonglong2 *)(cc.KW + ((u64)I << logN) + kc);
+        const ulonglong2 m1 = *(const ulonglong2 *)(cc.KW + ((u64)(l + 1 + I) << logN) + kc);
+        const u64 *kp = cc.key + ((u64)kI << logN) + kc;  // key[J][k][kI] at ((J 2 + k) K + kI) N
+        const u64 kstep = (u64)K << logN;
+        double f[FP ? 4 : 1];
+        U128 a[FP ? 1 : 4];
+        if constexpr (FP) {  // W KW in source order (slot 0 = s0): lazy products, canonicalised with the sum
+            const double x0 = fp_mulmod(u2d(wv.x), u2d(m0.x), pr.qd, pr.qinv);
+            const double x1 = fp_mulmod(u2d(wv.y), u2d(m0.y), pr.qd, pr.qinv);
+            const double y0 = fp_mulmod(u2d(wv.x), u2d(m1.x), pr.qd, pr.qinv);
+            const double y1 = fp_mulmod(u2d(wv.y), u2d(m1.y), pr.qd, pr.qinv);
+            f[0] = sw ? x1 : x0;
+            f[1] = sw ? x0 : x1;
+            f[2] = sw ? y1 : y0;
+            f[3] = sw ? y0 : y1;
+        } else {
+            const u64 x0 = mulmod(wv.x, m0.x, pr), x1 = mulmod(wv.y, m0.y, pr);
+            const u64 y0 = mulmod(wv.x, m1.x, pr), y1 = mulmod(wv.y, m1.y, pr);
+            a[0] = U128{sw ? x1 : x0, 0};
+            a[1] = U128{sw ? x0 : x1, 0};
+            a[2] = U128{sw ? y1 : y0, 0};
+            a[3] = U128{sw ? y0 : y1, 0};
+        }
+        ulonglong2 k0 = *(const ulonglong2 *)kp, k1 = *(const ulonglong2 *)(kp + kstep);
+        for (int J = 0; J < l; ++J) {
+            ulonglong2 n0{0, 0}, n1{0, 0};
+            if (J + 1 < l) {  // next digit's key words, one digit ahead
+                const u64 *kn = kp + (u64)(2 * (J + 1)) * kstep;
+                n0 = *(const ulonglong2 *)kn;
+                n1 = *(const ulonglong2 *)(kn + kstep);
+            }
+            const u64 ka = sw ? k0.y : k0.x, kb = sw ? k0.x : k0.y;  // key words of source slots s0, s0 + 1
+            const u64 kc0 = sw ? k1.y : k1.x, kc1 = sw ? k1.x : k1.y;
+            const u64 e0 = ev[J * LD], e1 = ev[J * LD + 1];
+            if constexpr (FP) {
+                const double d0 = __longlong_as_double((long long)e0), d1 = __longlong_as_double((long long)e1);
+                f[0] += fp_mulmod(d0, u2d(ka), pr.qd, pr.qinv);
+                f[1] += fp_mulmod(d1, u2d(kb), pr.qd, pr.qinv);
+                f[2] += fp_mulmod(d0, u2d(kc0), pr.qd, pr.qinv);
+                f[3] += fp_mulmod(d1, u2d(kc1), pr.qd, pr.qinv);
+            } else {
+                mac128(a[0], e0, ka);
+                mac128(a[1], e1, kb);
+                mac128(a[2], e0, kc0);
+                mac128(a[3], e1, kc1);
+            }
+            k0 = n0;
+            k1 = n1;
+        }
+        if (zeros) {  // the rare zero corrections (k_hmacm's), + (q - corr) key_J at the output slots
+            const u64 ko0 = kc | (u64)sw, ko1 = kc | (u64)!sw;
+            for (int J = 0; J < l; ++J) {
+                if (J == I) continue;
+                const int *z = zl + 1 + (b * l + J) * (HEC_ZCAP + 1);
+                const int nz = min(z[0], HEC_ZCAP);
+                if (nz == 0) continue;
+                const u64 cj = cji[J * K + kI];
+                u64 c0 = 0, c1 = 0;
+                for (int zi = 0; zi < nz; ++zi) {
+                    u64 tt2 = ((u64)z[1 + zi] * cc.elt) & (2 * N - 1);
+                    if (tt2 < N) continue;
+                    tt2 -= N;
+                    const u64 ex0 = ((2 * (u64)bitrev((u32)ko0, logN) + 1) * tt2) & (2 * N - 1);
+                    const u64 ex1 = ((2 * (u64)bitrev((u32)ko1, logN) + 1) * tt2) & (2 * N - 1);
+                    c0 = addmod(c0, mulmod(cj, pp[ex0], pr), pr.q);
+                    c1 = addmod(c1, mulmod(cj, pp[ex1], pr), pr.q);
+                }
+                if (c0 == 0 && c1 == 0) continue;
+                const u64 z0 = c0 ? pr.q - c0 : 0, z1 = c1 ? pr.q - c1 : 0;
+                const u64 *kj = kp + (u64)(2 * J) * kstep;
+                const ulonglong2 q0 = *(const ulonglong2 *)kj, q1 = *(const ulonglong2 *)(kj + kstep);
+                const u64 ka = sw ? q0.y : q0.x, kb = sw ? q0.x : q0.y, kc0 = sw ? q1.y : q1.x, kc1 = sw ? q1.x : q1.y;
+                if constexpr (FP) {
+                    f[0] += fp_mulmod(u2d(z0), u2d(ka), pr.qd, pr.qinv);
+                    f[1] += fp_mulmod(u2d(z1), u2d(kb), pr.qd, pr.qinv);
+                    f[2] += fp_mulmod(u2d(z0), u2d(kc0), pr.qd, pr.qinv);
+                    f[3] += fp_mulmod(u2d(z1), u2d(kc1), pr.qd, pr.qinv);
+                } else {
+                    mac128(a[0], z0, ka);
+                    mac128(a[1], z1, kb);
+                    mac128(a[2], z0, kc0);
+                    mac128(a[3], z1, kc1);
+                }
+            }
+        }
+        u64 r[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            if constexpr (FP) r[i] = fp_canon(f[i], pr.qd, pr.qinv);
+            else r[i] = barrett128(a[i].lo, a[i].hi, pr.q, pr.r0, pr.r1);
+        }
+        u64 *o0 = cc.ACC + (((u64)((b * 2 + 0) * (l + 1) + I)) << logN) + kc;
+        u64 *o1 = cc.ACC + (((u64)((b * 2 + 1) * (l + 1) + I)) << logN) + kc;
+        *(ulonglong2 *)o0 = sw ? ulonglong2{r[1], r[0]} : ulonglong2{r[0], r[1]};
+        *(ulonglong2 *)o1 = sw ? ulonglong2{r[3], r[2]} : ulonglong2{r[2], r[3]};
+    }
+}
+
+// 1-D grid, XCD-aware as k_bmac: the batch groups of one (chunk, I) run on one XCD and share its L2 copy of the
+// children's key chunks.  Imap lists the integer target primes first (their blocks are the slowest).
+template <int LOGP, int BT>
+__global__ void __launch_bounds__((1 << LOGP) / 2 * BT)
+    k_hmacf(PolyArr X1, const u64 *__restrict__ E, const int *__restrict__ zl, const HChildren<HMAC_MAX_CHILDREN> ch,
+            int B, int l, int K, int logN, const DevPrime *__restrict__ primes, TwTables tt,
+            const int *__restrict__ Imap, int nI, int nint, const u64 *__restrict__ cji,
+            const u64 *__restrict__ psipow)
+{
+    extern __shared__ u64 hf_lds[];  // [2 P] twiddles, then BT l tiles of P + P/16 words
+    constexpr int P = 1 << LOGP;
+    const int nbg = (B + BT - 1) / BT;
+    const int w = blockIdx.x, g8 = w & 7, rest = w >> 3, bg = rest % nbg, G = (rest / nbg) * 8 + g8;
+    const int X = 1 << (logN - LOGP);
+    if (G >= X * nI) return;
+    const int yi = G / X, chunk = G % X;
+    const int I = Imap[yi];
+    const int kI = I == l ? K - 1 : I;
+    const DevPrime pr = primes[kI];
+    if (yi < nint)
+        hmacf_body<LOGP, BT, false>(hf_lds, hf_lds + 2 * P, X1, E, zl, ch, B, l, K, logN, pr, tt, I, kI, chunk, bg * BT,
+                                    cji, psipow);
+    else
+        hmacf_body<LOGP, BT, true>(hf_lds, hf_lds + 2 * P, X1, E, zl, ch, B, l, K, logN, pr, tt, I, kI, chunk, bg * BT,
+                                   cji, psipow);
+}
+
+template <int LOGP, int BT>
+static void launch_hmacf(Ctx &c, PolyArr X1, const u64 *E, const int *zl, const HChildSpec *kids, int nkids, int B,
+                         int l)
+{
+    constexpr int P = 1 << LOGP, THREADS = P / 2 * BT, LD = P + P / 16;
+    HChildren<HMAC_MAX_CHILDREN> ch{};
+    ch.n = nkids;
+    for (int q = 0; q < nkids; ++q)
+        ch.c[q] = HChild{kids[q].elt, kids[q].einv, kids[q].key, kids[q].W, kids[q].ACC, kids[q].KW};
+    const std::size_t shm = (std::size_t)(2 * P + BT * l * LD) * sizeof(u64);
+    if (shm > 65536) throw std::invalid_argument("hoisted_mac_fused: LDS tile too large for this level");
+    const int X = (int)(c.N >> LOGP), gpad = (X * (l + 1) + 7) / 8 * 8, nbg = (B + BT - 1) / BT;
+    const TwTables fwd{c.tw, c.twb, c.twf, c.twbf};
+    k_hmacf<LOGP, BT><<<dim3((unsigned)(gpad * nbg)), THREADS, shm, c.stream>>>(
+        X1, E, zl, ch, B, l, (int)c.K, c.logN, c.primes, fwd, c.imap_at(l), l + 1, c.imap_nint[l], c.cji, c.psipow);
+    HEC_HIP(hipGetLastError());
+}
+
+bool hoisted_mac_fused_fits(const Ctx &c, int l)
+{
+    const int logp = c.logN - c.logR, P = 1 << logp, bt = logp <= 5 ? 4 : logp == 6 ? 2 : logp == 7 ? c.hfuse_bt : 1;
+    return (std::size_t)(2 * P + bt * l * (P + P / 16)) * sizeof(u64) <= 65536;
+}
+
+void hoisted_mac_fused(Ctx &c, PolyArr X1, const u64 *E, const int *zl, const HChildSpec *kids, int nkids, int B, int l)
+{
+    if (nkids < 1 || nkids > HMAC_MAX_CHILDREN) throw std::invalid_argument("hoisted_mac_fused: children per launch");
+    if (l > HEC_MAXL) throw std::invalid_argument("too many limbs");
+    switch (c.logN - c.logR) {  // <pass-B size, batch entries per block>: 64-thread blocks at P <= 128
+    case 5: launch_hmacf<5, 4>(c, X1, E, zl, kids, nkids, B, l); break;
+    case 6: launch_hmacf<6, 2>(c, X1, E, zl, kids, nkids, B, l); break;
+    case 7:
+        if (c.hfuse_bt == 2) launch_hmacf<7, 2>(c, X1, E, zl, kids, nkids, B, l);
+        else launch_hmacf<7, 1>(c, X1, E, zl, kids, nkids, B, l);
+        break;
+    case 8: launch_hmacf<8, 1>(c, X1, E, zl, kids, nkids, B, l); break;
+    default: throw std::invalid_argument("poly_modulus_degree must be 2^10 .. 2^16");
+    }
+}
+
 void fan_divide_round(Ctx &c, const u64 *Y, u64 ysb, u64 ysk, u64 *Z, int B, int nk, int nl, int last_idx)
 {
     if (nl > HEC_MAXL) throw std::invalid_argument("too many limbs");
