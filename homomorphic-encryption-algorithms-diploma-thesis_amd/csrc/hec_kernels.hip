@@ -1503,9 +1503,9 @@ void hoisted_mac_3(Ctx &c, PolyArr X1, const u64 *E, const int *zl, const HChild
 // digits cross HBM once more (read here) instead of three or more times (pass B read + write, one read per sibling
 // pair of k_hmacm).  A block owns one pass-B chunk (P = 2^LOGP contiguous source positions) of one target prime I
 // for BT batch entries (one wave at P = 128, BT = 1) and keeps all l digit tiles of its chunk in LDS (l BT (P + P/16)
-// words: 10.9 KB at cfg3).  A thread owns one source pair of one batch entry and loops over the children with one
-// child's four accumulators live, so the kernel needs few registers.  (The fused kernels deleted earlier in round 3,
-// DESIGN.md §10, kept several children's accumulators or batch tiles per thread and ran at 1-2 waves/SIMD.)
+// words: 10.9 KB at cfg3).  A thread owns one source pair of one batch entry and keeps the four accumulators of
+// every child of the launch.  (The fused kernels deleted earlier in round 3, DESIGN.md §10, held several batch
+// entries or all digits of larger tiles per block and ran at 1-2 waves/SIMD.)
 // The MAC is k_hmacm's: the child's output pair is gal_c^-1(s) (keys, W, KW and ACC gathered there, all inside the
 // child's output chunk), the sign-mask term W KW starts the accumulators, the rare zero corrections follow the digit
 // loop.  FP64 targets keep the pass-B outputs as lazy doubles (|v| < 10 q, fp_mulmod's range); the 60-bit targets
@@ -1581,72 +1581,94 @@ __device__ __forceinline__ void hmacf_body(u64 *ltw, u64 *lds, PolyArr X1, const
     const u64 *ev = lds + bb * l * LD + 2 * p + (p >> 3);  // digit J of this source pair: ev[J LD], ev[J LD + 1]
     const bool zeros = zl[0] != 0;
     const u64 *pp = psipow + ((u64)kI << (logN + 1));
-    for (int q = 0; q < ch.n; ++q) {
-        const HChild &cc = ch.c[q];
-        const u32 t = galois_src((u32)s0, cc.einv, logN);
-        const u64 kc = t & ~1u;
-        const bool sw = t & 1;
-        const ulonglong2 wv = *(const ulonglong2 *)(cc.W + ((u64)kI << logN) + kc);
-        const ulonglong2 m0 = *(const ulonglong2 *)(cc.KW + ((u64)I << logN) + kc);
-        const ulonglong2 m1 = *(const ulonglong2 *)(cc.KW + ((u64)(l + 1 + I) << logN) + kc);
-        const u64 *kp = cc.key + ((u64)kI << logN) + kc;  // key[J][k][kI] at ((J 2 + k) K + kI) N
-        const u64 kstep = (u64)K << logN;
-        double f[FP ? 4 : 1];
-        U128 a[FP ? 1 : 4];
-        if constexpr (FP) {  // W KW in source order (slot 0 = s0): lazy products, canonicalised with the sum
+    // the children in passes of CG with their accumulators live (digit loop outside, children inside): per digit the
+    // pass's key words are independent loads issued together, so a block waits for l load latencies per pass instead
+    // of l per child.  CG = 3 FP64 / 2 integer children keep the kernel near 128 VGPRs.
+    constexpr int CG = FP ? 3 : 2;
+    const u64 kstep = (u64)K << logN;
+    for (int q0 = 0; q0 < ch.n; q0 += CG) {
+    const int nk = min(CG, ch.n - q0);
+    const HChild *cs = ch.c + q0;
+    u64 kc[CG];
+    bool sw[CG];
+    double f[FP ? CG : 1][4];
+    U128 a[FP ? 1 : CG][4];
+#pragma unroll
+    for (int q = 0; q < CG; ++q) {  // output pairs and the sign-mask terms W KW in source order (slot 0 = s0)
+        kc[q] = 0;
+        sw[q] = false;
+        ulonglong2 wv{0, 0}, m0{0, 0}, m1{0, 0};
+        if (q < nk) {
+            const HChild &cc = cs[q];
+            const u32 t = galois_src((u32)s0, cc.einv, logN);
+            kc[q] = t & ~1u;
+            sw[q] = t & 1;
+            wv = *(const ulonglong2 *)(cc.W + ((u64)kI << logN) + kc[q]);
+            m0 = *(const ulonglong2 *)(cc.KW + ((u64)I << logN) + kc[q]);
+            m1 = *(const ulonglong2 *)(cc.KW + ((u64)(l + 1 + I) << logN) + kc[q]);
+        }
+        if constexpr (FP) {  // lazy products, canonicalised with the sum
             const double x0 = fp_mulmod(u2d(wv.x), u2d(m0.x), pr.qd, pr.qinv);
             const double x1 = fp_mulmod(u2d(wv.y), u2d(m0.y), pr.qd, pr.qinv);
             const double y0 = fp_mulmod(u2d(wv.x), u2d(m1.x), pr.qd, pr.qinv);
             const double y1 = fp_mulmod(u2d(wv.y), u2d(m1.y), pr.qd, pr.qinv);
-            f[0] = sw ? x1 : x0;
-            f[1] = sw ? x0 : x1;
-            f[2] = sw ? y1 : y0;
-            f[3] = sw ? y0 : y1;
+            f[q][0] = sw[q] ? x1 : x0;
+            f[q][1] = sw[q] ? x0 : x1;
+            f[q][2] = sw[q] ? y1 : y0;
+            f[q][3] = sw[q] ? y0 : y1;
         } else {
             const u64 x0 = mulmod(wv.x, m0.x, pr), x1 = mulmod(wv.y, m0.y, pr);
             const u64 y0 = mulmod(wv.x, m1.x, pr), y1 = mulmod(wv.y, m1.y, pr);
-            a[0] = U128{sw ? x1 : x0, 0};
-            a[1] = U128{sw ? x0 : x1, 0};
-            a[2] = U128{sw ? y1 : y0, 0};
-            a[3] = U128{sw ? y0 : y1, 0};
+            a[q][0] = U128{sw[q] ? x1 : x0, 0};
+            a[q][1] = U128{sw[q] ? x0 : x1, 0};
+            a[q][2] = U128{sw[q] ? y1 : y0, 0};
+            a[q][3] = U128{sw[q] ? y0 : y1, 0};
         }
-        ulonglong2 k0 = *(const ulonglong2 *)kp, k1 = *(const ulonglong2 *)(kp + kstep);
-        for (int J = 0; J < l; ++J) {
-            ulonglong2 n0{0, 0}, n1{0, 0};
-            if (J + 1 < l) {  // next digit's key words, one digit ahead
-                const u64 *kn = kp + (u64)(2 * (J + 1)) * kstep;
-                n0 = *(const ulonglong2 *)kn;
-                n1 = *(const ulonglong2 *)(kn + kstep);
+    }
+    for (int J = 0; J < l; ++J) {
+        ulonglong2 k0[CG], k1[CG];
+#pragma unroll
+        for (int q = 0; q < CG; ++q) {
+            if (q < nk) {
+                const u64 *kj = cs[q].key + ((u64)kI << logN) + kc[q] + (u64)(2 * J) * kstep;
+                k0[q] = *(const ulonglong2 *)kj;
+                k1[q] = *(const ulonglong2 *)(kj + kstep);
             }
-            const u64 ka = sw ? k0.y : k0.x, kb = sw ? k0.x : k0.y;  // key words of source slots s0, s0 + 1
-            const u64 kc0 = sw ? k1.y : k1.x, kc1 = sw ? k1.x : k1.y;
-            const u64 e0 = ev[J * LD], e1 = ev[J * LD + 1];
+        }
+        const u64 e0 = ev[J * LD], e1 = ev[J * LD + 1];
+#pragma unroll
+        for (int q = 0; q < CG; ++q) {
+            if (q >= nk) break;
+            const u64 ka = sw[q] ? k0[q].y : k0[q].x, kb = sw[q] ? k0[q].x : k0[q].y;  // source slots s0, s0 + 1
+            const u64 kc0 = sw[q] ? k1[q].y : k1[q].x, kc1 = sw[q] ? k1[q].x : k1[q].y;
             if constexpr (FP) {
                 const double d0 = __longlong_as_double((long long)e0), d1 = __longlong_as_double((long long)e1);
-                f[0] += fp_mulmod(d0, u2d(ka), pr.qd, pr.qinv);
-                f[1] += fp_mulmod(d1, u2d(kb), pr.qd, pr.qinv);
-                f[2] += fp_mulmod(d0, u2d(kc0), pr.qd, pr.qinv);
-                f[3] += fp_mulmod(d1, u2d(kc1), pr.qd, pr.qinv);
+                f[q][0] += fp_mulmod(d0, u2d(ka), pr.qd, pr.qinv);
+                f[q][1] += fp_mulmod(d1, u2d(kb), pr.qd, pr.qinv);
+                f[q][2] += fp_mulmod(d0, u2d(kc0), pr.qd, pr.qinv);
+                f[q][3] += fp_mulmod(d1, u2d(kc1), pr.qd, pr.qinv);
             } else {
-                mac128(a[0], e0, ka);
-                mac128(a[1], e1, kb);
-                mac128(a[2], e0, kc0);
-                mac128(a[3], e1, kc1);
+                mac128(a[q][0], e0, ka);
+                mac128(a[q][1], e1, kb);
+                mac128(a[q][2], e0, kc0);
+                mac128(a[q][3], e1, kc1);
             }
-            k0 = n0;
-            k1 = n1;
         }
-        if (zeros) {  // the rare zero corrections (k_hmacm's), + (q - corr) key_J at the output slots
-            const u64 ko0 = kc | (u64)sw, ko1 = kc | (u64)!sw;
-            for (int J = 0; J < l; ++J) {
-                if (J == I) continue;
-                const int *z = zl + 1 + (b * l + J) * (HEC_ZCAP + 1);
-                const int nz = min(z[0], HEC_ZCAP);
-                if (nz == 0) continue;
-                const u64 cj = cji[J * K + kI];
+    }
+    if (zeros) {  // the rare zero corrections (k_hmacm's), + (q - corr) key_J at the output slots
+        for (int J = 0; J < l; ++J) {
+            if (J == I) continue;
+            const int *z = zl + 1 + (b * l + J) * (HEC_ZCAP + 1);
+            const int nz = min(z[0], HEC_ZCAP);
+            if (nz == 0) continue;
+            const u64 cj = cji[J * K + kI];
+#pragma unroll
+            for (int q = 0; q < CG; ++q) {
+                if (q >= nk) break;
+                const u64 ko0 = kc[q] | (u64)sw[q], ko1 = kc[q] | (u64)!sw[q];
                 u64 c0 = 0, c1 = 0;
                 for (int zi = 0; zi < nz; ++zi) {
-                    u64 tt2 = ((u64)z[1 + zi] * cc.elt) & (2 * N - 1);
+                    u64 tt2 = ((u64)z[1 + zi] * cs[q].elt) & (2 * N - 1);
                     if (tt2 < N) continue;
                     tt2 -= N;
                     const u64 ex0 = ((2 * (u64)bitrev((u32)ko0, logN) + 1) * tt2) & (2 * N - 1);
@@ -1656,32 +1678,38 @@ __device__ __forceinline__ void hmacf_body(u64 *ltw, u64 *lds, PolyArr X1, const
                 }
                 if (c0 == 0 && c1 == 0) continue;
                 const u64 z0 = c0 ? pr.q - c0 : 0, z1 = c1 ? pr.q - c1 : 0;
-                const u64 *kj = kp + (u64)(2 * J) * kstep;
+                const u64 *kj = cs[q].key + ((u64)kI << logN) + kc[q] + (u64)(2 * J) * kstep;
                 const ulonglong2 q0 = *(const ulonglong2 *)kj, q1 = *(const ulonglong2 *)(kj + kstep);
-                const u64 ka = sw ? q0.y : q0.x, kb = sw ? q0.x : q0.y, kc0 = sw ? q1.y : q1.x, kc1 = sw ? q1.x : q1.y;
+                const u64 ka = sw[q] ? q0.y : q0.x, kb = sw[q] ? q0.x : q0.y;
+                const u64 kc0 = sw[q] ? q1.y : q1.x, kc1 = sw[q] ? q1.x : q1.y;
                 if constexpr (FP) {
-                    f[0] += fp_mulmod(u2d(z0), u2d(ka), pr.qd, pr.qinv);
-                    f[1] += fp_mulmod(u2d(z1), u2d(kb), pr.qd, pr.qinv);
-                    f[2] += fp_mulmod(u2d(z0), u2d(kc0), pr.qd, pr.qinv);
-                    f[3] += fp_mulmod(u2d(z1), u2d(kc1), pr.qd, pr.qinv);
+                    f[q][0] += fp_mulmod(u2d(z0), u2d(ka), pr.qd, pr.qinv);
+                    f[q][1] += fp_mulmod(u2d(z1), u2d(kb), pr.qd, pr.qinv);
+                    f[q][2] += fp_mulmod(u2d(z0), u2d(kc0), pr.qd, pr.qinv);
+                    f[q][3] += fp_mulmod(u2d(z1), u2d(kc1), pr.qd, pr.qinv);
                 } else {
-                    mac128(a[0], z0, ka);
-                    mac128(a[1], z1, kb);
-                    mac128(a[2], z0, kc0);
-                    mac128(a[3], z1, kc1);
+                    mac128(a[q][0], z0, ka);
+                    mac128(a[q][1], z1, kb);
+                    mac128(a[q][2], z0, kc0);
+                    mac128(a[q][3], z1, kc1);
                 }
             }
         }
+    }
+#pragma unroll
+    for (int q = 0; q < CG; ++q) {
+        if (q >= nk) break;
         u64 r[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            if constexpr (FP) r[i] = fp_canon(f[i], pr.qd, pr.qinv);
-            else r[i] = barrett128(a[i].lo, a[i].hi, pr.q, pr.r0, pr.r1);
+            if constexpr (FP) r[i] = fp_canon(f[q][i], pr.qd, pr.qinv);
+            else r[i] = barrett128(a[q][i].lo, a[q][i].hi, pr.q, pr.r0, pr.r1);
         }
-        u64 *o0 = cc.ACC + (((u64)((b * 2 + 0) * (l + 1) + I)) << logN) + kc;
-        u64 *o1 = cc.ACC + (((u64)((b * 2 + 1) * (l + 1) + I)) << logN) + kc;
-        *(ulonglong2 *)o0 = sw ? ulonglong2{r[1], r[0]} : ulonglong2{r[0], r[1]};
-        *(ulonglong2 *)o1 = sw ? ulonglong2{r[3], r[2]} : ulonglong2{r[2], r[3]};
+        u64 *o0 = cs[q].ACC + (((u64)((b * 2 + 0) * (l + 1) + I)) << logN) + kc[q];
+        u64 *o1 = cs[q].ACC + (((u64)((b * 2 + 1) * (l + 1) + I)) << logN) + kc[q];
+        *(ulonglong2 *)o0 = sw[q] ? ulonglong2{r[1], r[0]} : ulonglong2{r[0], r[1]};
+        *(ulonglong2 *)o1 = sw[q] ? ulonglong2{r[3], r[2]} : ulonglong2{r[2], r[3]};
+    }
     }
 }
 
