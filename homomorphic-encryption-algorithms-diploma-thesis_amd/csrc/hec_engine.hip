@@ -1338,14 +1338,20 @@ int hec_context_create(uint64_t N, const uint64_t *mod, uint64_t K, int device, 
                         twb[dst] = tw[src];
                         itwb[dst] = itw[src];
                     }
+        // chunk-major forward pass-B tables (k_hmacf: one chunk's P - 1 twiddles contiguous): entry (r, k) at r C + k
+        std::vector<ulonglong2> twc(K * N);
+        for (uint64_t i = 0; i < K; ++i)
+            for (uint64_t r = 0; r < R; ++r)
+                for (uint64_t k = 0; k + 1 < C; ++k) twc[i * N + r * C + k] = twb[i * N + R * k + r];
         auto to_d = [](const std::vector<ulonglong2> &v) {
             std::vector<double> r(v.size());
             for (std::size_t k = 0; k < v.size(); ++k) r[k] = (double)v[k].x;  // exact when q < 2^42
             return r;
         };
-        const std::vector<double> twf = to_d(tw), itwf = to_d(itw), twbf = to_d(twb), itwbf = to_d(itwb);
+        const std::vector<double> twf = to_d(tw), itwf = to_d(itw), twbf = to_d(twb), itwbf = to_d(itwb),
+                                  twcf = to_d(twc);
         for (auto [dst, src] : {std::pair{&c.twf, &twf}, std::pair{&c.itwf, &itwf}, std::pair{&c.twbf, &twbf},
-                                std::pair{&c.itwbf, &itwbf}}) {
+                                std::pair{&c.itwbf, &itwbf}, std::pair{&c.twcf, &twcf}}) {
             HEC_HIP(hipMalloc(dst, K * N * sizeof(double)));
             HEC_HIP(hipMemcpy(*dst, src->data(), K * N * sizeof(double), hipMemcpyHostToDevice));
         }
@@ -1353,6 +1359,8 @@ int hec_context_create(uint64_t N, const uint64_t *mod, uint64_t K, int device, 
         HEC_HIP(hipMalloc(&c.itwb, K * N * sizeof(ulonglong2)));
         HEC_HIP(hipMemcpy(c.twb, twb.data(), K * N * sizeof(ulonglong2), hipMemcpyHostToDevice));
         HEC_HIP(hipMemcpy(c.itwb, itwb.data(), K * N * sizeof(ulonglong2), hipMemcpyHostToDevice));
+        HEC_HIP(hipMalloc(&c.twc, K * N * sizeof(ulonglong2)));
+        HEC_HIP(hipMemcpy(c.twc, twc.data(), K * N * sizeof(ulonglong2), hipMemcpyHostToDevice));
         {   // hoisted mod-up constants: psi powers per key prime, q_J mod q_I
             HEC_HIP(hipMalloc(&c.psipow, psipow.size() * sizeof(u64)));
             HEC_HIP(hipMemcpy(c.psipow, psipow.data(), psipow.size() * sizeof(u64), hipMemcpyHostToDevice));
@@ -1428,7 +1436,8 @@ int hec_context_destroy(hec_context *ctx)
         (void)hipFree(c.itw);
         (void)hipFree(c.twb);
         (void)hipFree(c.itwb);
-        for (double *p : {c.twf, c.itwf, c.twbf, c.itwbf}) (void)hipFree(p);
+        (void)hipFree(c.twc);
+        for (double *p : {c.twf, c.itwf, c.twbf, c.itwbf, c.twcf}) (void)hipFree(p);
         (void)hipFree(c.enc_map);
         (void)hipFree(c.enc_tw);
         if (c.own_stream) (void)hipStreamDestroy(c.stream);

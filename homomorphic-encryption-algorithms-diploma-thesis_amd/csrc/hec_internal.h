@@ -65,6 +65,8 @@ struct Ctx {
     ulonglong2 *twb = nullptr;      // device [K][N] pass-B layout of tw: [s][i][chunk] (see hec_kernels.hip)
     ulonglong2 *itwb = nullptr;     // same for itw
     double *twf = nullptr, *itwf = nullptr, *twbf = nullptr, *itwbf = nullptr;  // FP64 twins (q < 2^42)
+    ulonglong2 *twc = nullptr;      // device [K][N] chunk-major forward pass-B layout: [chunk][2^s - 1 + i] (k_hmacf)
+    double *twcf = nullptr;
     // key-switch target primes I in [0, l] (I == l is P) per level l, integer-arithmetic primes first:
     // device table imap + l * (HEC_MAXL + 2), built once at context creation; imap_nint[l] of them integer
     int *imap = nullptr;

@@ -1521,13 +1521,11 @@ __device__ __forceinline__ void hmacf_body(u64 *ltw, u64 *lds, PolyArr X1, const
     constexpr int CONC = THREADS / TPT;
     const u64 N = 1ull << logN, base = (u64)chunk << LOGP;
     const int nb = min(BT, B - b0);
-    {  // the chunk's pass-B twiddles (k_bmac's staging, one chunk)
-        const u64 R = 1ull << (logN - LOGP);
-        const ulonglong2 *tw = tt.b + ((u64)kI << logN);
-        const double *twf = tt.fb + ((u64)kI << logN);
+    {  // the chunk's pass-B twiddles, contiguous in the chunk-major table (tt.b / tt.fb = Ctx::twc / twcf)
+        const ulonglong2 *tw = tt.b + ((u64)kI << logN) + base;
+        const double *twf = tt.fb + ((u64)kI << logN) + base;
         for (int k = threadIdx.x; k < P - 1; k += THREADS) {
-            const int st = 31 - __clz(k + 1), i = k + 1 - (1 << st);
-            const u64 gi = R * ((1ull << st) - 1) + (u64)i * R + (u64)chunk;
+            const int gi = k;
             if constexpr (FP) ltw[k] = (u64)__double_as_longlong(twf[gi]);
             else {
                 const ulonglong2 w = tw[gi];
@@ -1752,7 +1750,7 @@ static void launch_hmacf(Ctx &c, PolyArr X1, const u64 *E, const int *zl, const 
     const std::size_t shm = (std::size_t)(2 * P + BT * l * LD) * sizeof(u64);
     if (shm > 65536) throw std::invalid_argument("hoisted_mac_fused: LDS tile too large for this level");
     const int X = (int)(c.N >> LOGP), gpad = (X * (l + 1) + 7) / 8 * 8, nbg = (B + BT - 1) / BT;
-    const TwTables fwd{c.tw, c.twb, c.twf, c.twbf};
+    const TwTables fwd{c.tw, c.twc, c.twf, c.twcf};  // pass B from the chunk-major table
     k_hmacf<LOGP, BT><<<dim3((unsigned)(gpad * nbg)), THREADS, shm, c.stream>>>(
         X1, E, zl, ch, B, l, (int)c.K, c.logN, c.primes, fwd, c.imap_at(l), l + 1, c.imap_nint[l], c.cji, c.psipow);
     HEC_HIP(hipGetLastError());
