@@ -1623,6 +1623,7 @@ __device__ __forceinline__ void hmacf_body(u64 *ltw, u64 *lds, PolyArr X1, const
             a[q][3] = U128{sw[q] ? y0 : y1, 0};
         }
     }
+#pragma unroll 2
     for (int J = 0; J < l; ++J) {
         ulonglong2 k0[CG], k1[CG];
 #pragma unroll
