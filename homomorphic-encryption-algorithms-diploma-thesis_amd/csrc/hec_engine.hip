@@ -450,8 +450,7 @@ void keyswitch(Ctx &c, Scratch &s, PolyArr T, const u64 *key, PolyArr IN, int in
 
 // hoisted mod-up data of one trie node (B targets at level l): D = INTT(c1) (canonical coefficient form),
 // E[b][I][J] = NTT_I(D_J mod q_I) (canonical NTT form, J != I), zero lists of D (see hec_kernels.hip)
-constexpr int HOIST_GROUP = 6;  // sibling rotations per grouped mod-down (and per k_hmacm / k_hmacf accumulator set)
-static_assert(HOIST_GROUP <= HMAC_MAX_CHILDREN, "a k_hmacf launch covers one group");
+constexpr int HOIST_GROUP = 6;  // sibling rotations per grouped mod-down (and per k_hmacm accumulator set)
 struct Hoist {
     u64 *D = nullptr, *E = nullptr;
     int *zl = nullptr;
@@ -476,8 +475,7 @@ Hoist hoist_alloc(const Ctx &c, Scratch &s, int B, int l)
     h.acc0 = s.take((u64)HOIST_GROUP * h.sacc);
     return h;
 }
-// pass_b = false: the digits stay in the pass-A domain for k_hmacf, which finishes them in LDS
-void hoist_node(Ctx &c, PolyArr X, int B, int l, const Hoist &h, bool pass_b = true)
+void hoist_node(Ctx &c, PolyArr X, int B, int l, const Hoist &h)
 {
     const u64 N = c.N;
     int pmap[HEC_MAXL + 1];
@@ -493,7 +491,6 @@ void hoist_node(Ctx &c, PolyArr X, int B, int l, const Hoist &h, bool pass_b = t
             ProfScope k(c, "k:k_fan2/hoist", (double)B * l * (l + 1));
             fan_modup(c, h.D, h.E, B, l, false, h.zl);
         }
-        if (!pass_b) return;
         ProfScope k(c, "k:k_ntt/modup_h_b", 2.0 * B * l * l);
         ks_modup(c, h.D, h.E, B, l, 2);  // pass B, canonical NTT-form digits
         return;
@@ -516,7 +513,6 @@ void hoist_node(Ctx &c, PolyArr X, int B, int l, const Hoist &h, bool pass_b = t
         ProfScope k(c, c.fan2 ? "k:k_fan2/hoist" : "k:k_fan/hoist", (double)B * l * (l + 1));
         fan_modup(c, h.D, h.E, B, l, true);  // pass A of every NTT_I(D_J mod q_I), from the canonical D
     }
-    if (!pass_b) return;
     ProfScope k(c, "k:k_ntt/modup_h_b", 2.0 * B * l * l);
     ks_modup(c, h.D, h.E, B, l, 2);      // pass B, canonical NTT-form digits
 }
@@ -726,13 +722,11 @@ void walk_trie_hoisted(Ctx &c, Scratch &s, const RotTrie &t, int node, PolyArr s
         return;
     }
     const Hoist &h = hs[depth];
-    const bool fused = c.hfuse && hoisted_mac_fused_fits(c, l);
-    hoist_node(c, src, B, l, h, !fused);
+    hoist_node(c, src, B, l, h);
     const u64 N = c.N;
-    // children in groups of up to `sup` siblings, accumulators h.acc(q), contiguous: fused, one k_hmacf launch per
-    // group (the digits' pass B in LDS, redone per group); otherwise one sibling-fused k_hmacm launch per
-    // hoisted_group() of them.  Then the mod-downs in groups of HOIST_GROUP share their small launches
-    const std::size_t grp = fused ? (std::size_t)HOIST_GROUP : (std::size_t)hoisted_group(c);
+    // children in groups of up to `sup` siblings: one sibling-fused k_hmacm launch per hoisted_group() of them,
+    // accumulators h.acc(q), contiguous; then the mod-downs in groups of HOIST_GROUP share their small launches
+    const std::size_t grp = (std::size_t)hoisted_group(c);
     const std::size_t sup = std::max<std::size_t>(grp, HOIST_GROUP / grp * grp);
     for (std::size_t g0 = 0; g0 < ch.size(); g0 += sup) {
         const int ng = (int)std::min<std::size_t>(sup, ch.size() - g0);
@@ -743,12 +737,7 @@ void walk_trie_hoisted(Ctx &c, Scratch &s, const RotTrie &t, int node, PolyArr s
                                  galois_kw(ctx, gk, e, l)};
         }
         const double K = l + 1;  // per child: key (2 l K), W (K), KW (2 K), ACC (2 B K)
-        if (fused) {  // pass-A digits E (B l^2) + c1 (B l) + per child as above
-            ProfScope ps(c, "ks_hmac");
-            ProfScope k(c, "k:k_hmacf", (double)B * (l * l + l) + ng * (2.0 * l * K + 3.0 * K + 2.0 * B * K));
-            hoisted_mac_fused(c, PolyArr{src.p + src.sk, src.sb, 0}, h.E, h.zl, kids, ng, B, l);
-        }
-        for (int q0 = 0, nk = 0; !fused && q0 < ng; q0 += nk) {  // one profile scope per launch (bench.py's roofline)
+        for (int q0 = 0, nk = 0; q0 < ng; q0 += nk) {  // one profile scope per launch (bench.py's roofline)
             nk = std::min((int)grp, ng - q0);
             // an odd group's last three children as one 3-child launch (the digits read once, not twice)
             if (c.hmac_odd3 && grp == 2 && ng - q0 == 3) nk = 3;
@@ -1274,8 +1263,6 @@ int hec_context_create(uint64_t N, const uint64_t *mod, uint64_t K, int device, 
             std::sscanf(f, "%d,%d,%d", &c.fan_groups_moddown, &c.fan_groups_modup, &c.fan_groups_hoist);
         if (const char *f = std::getenv("HEC_HOIST")) c.hoist = f[0] != '0';
         if (const char *f = std::getenv("HEC_HMAC")) c.hmac_cfg = std::atoi(f);
-        if (const char *f = std::getenv("HEC_HFUSE")) c.hfuse = std::atoi(f);
-        if (const char *f = std::getenv("HEC_HFUSE_BT")) c.hfuse_bt = std::atoi(f) == 2 ? 2 : 1;
         if (const char *f = std::getenv("HEC_HMAC_ODD3")) c.hmac_odd3 = std::atoi(f);
         if (const char *f = std::getenv("HEC_HOIST_MIN")) c.hoist_min_children = std::max(1, std::atoi(f));
         if (const char *f = std::getenv("HEC_TENSOR_DEFER")) c.tensor_defer_max = std::max(1, std::atoi(f));
@@ -1338,20 +1325,14 @@ int hec_context_create(uint64_t N, const uint64_t *mod, uint64_t K, int device, 
                         twb[dst] = tw[src];
                         itwb[dst] = itw[src];
                     }
-        // chunk-major forward pass-B tables (k_hmacf: one chunk's P - 1 twiddles contiguous): entry (r, k) at r C + k
-        std::vector<ulonglong2> twc(K * N);
-        for (uint64_t i = 0; i < K; ++i)
-            for (uint64_t r = 0; r < R; ++r)
-                for (uint64_t k = 0; k + 1 < C; ++k) twc[i * N + r * C + k] = twb[i * N + R * k + r];
         auto to_d = [](const std::vector<ulonglong2> &v) {
             std::vector<double> r(v.size());
             for (std::size_t k = 0; k < v.size(); ++k) r[k] = (double)v[k].x;  // exact when q < 2^42
             return r;
         };
-        const std::vector<double> twf = to_d(tw), itwf = to_d(itw), twbf = to_d(twb), itwbf = to_d(itwb),
-                                  twcf = to_d(twc);
+        const std::vector<double> twf = to_d(tw), itwf = to_d(itw), twbf = to_d(twb), itwbf = to_d(itwb);
         for (auto [dst, src] : {std::pair{&c.twf, &twf}, std::pair{&c.itwf, &itwf}, std::pair{&c.twbf, &twbf},
-                                std::pair{&c.itwbf, &itwbf}, std::pair{&c.twcf, &twcf}}) {
+                                std::pair{&c.itwbf, &itwbf}}) {
             HEC_HIP(hipMalloc(dst, K * N * sizeof(double)));
             HEC_HIP(hipMemcpy(*dst, src->data(), K * N * sizeof(double), hipMemcpyHostToDevice));
         }
@@ -1359,8 +1340,6 @@ int hec_context_create(uint64_t N, const uint64_t *mod, uint64_t K, int device, 
         HEC_HIP(hipMalloc(&c.itwb, K * N * sizeof(ulonglong2)));
         HEC_HIP(hipMemcpy(c.twb, twb.data(), K * N * sizeof(ulonglong2), hipMemcpyHostToDevice));
         HEC_HIP(hipMemcpy(c.itwb, itwb.data(), K * N * sizeof(ulonglong2), hipMemcpyHostToDevice));
-        HEC_HIP(hipMalloc(&c.twc, K * N * sizeof(ulonglong2)));
-        HEC_HIP(hipMemcpy(c.twc, twc.data(), K * N * sizeof(ulonglong2), hipMemcpyHostToDevice));
         {   // hoisted mod-up constants: psi powers per key prime, q_J mod q_I
             HEC_HIP(hipMalloc(&c.psipow, psipow.size() * sizeof(u64)));
             HEC_HIP(hipMemcpy(c.psipow, psipow.data(), psipow.size() * sizeof(u64), hipMemcpyHostToDevice));
@@ -1436,8 +1415,7 @@ int hec_context_destroy(hec_context *ctx)
         (void)hipFree(c.itw);
         (void)hipFree(c.twb);
         (void)hipFree(c.itwb);
-        (void)hipFree(c.twc);
-        for (double *p : {c.twf, c.itwf, c.twbf, c.itwbf, c.twcf}) (void)hipFree(p);
+        for (double *p : {c.twf, c.itwf, c.twbf, c.itwbf}) (void)hipFree(p);
         (void)hipFree(c.enc_map);
         (void)hipFree(c.enc_tw);
         if (c.own_stream) (void)hipStreamDestroy(c.stream);

@@ -65,8 +65,6 @@ struct Ctx {
     ulonglong2 *twb = nullptr;      // device [K][N] pass-B layout of tw: [s][i][chunk] (see hec_kernels.hip)
     ulonglong2 *itwb = nullptr;     // same for itw
     double *twf = nullptr, *itwf = nullptr, *twbf = nullptr, *itwbf = nullptr;  // FP64 twins (q < 2^42)
-    ulonglong2 *twc = nullptr;      // device [K][N] chunk-major forward pass-B layout: [chunk][2^s - 1 + i] (k_hmacf)
-    double *twcf = nullptr;
     // key-switch target primes I in [0, l] (I == l is P) per level l, integer-arithmetic primes first:
     // device table imap + l * (HEC_MAXL + 2), built once at context creation; imap_nint[l] of them integer
     int *imap = nullptr;
@@ -91,8 +89,6 @@ struct Ctx {
     int tensor_bg = 1;             // HEC_TENSOR_BG=0: k_tensor_multi (one thread per coefficient, whole batch)
     bool hoist = true;             // HEC_HOIST=0: no hoisted mod-up in the rotation trie walk
     int hoist_min_children = 2;    // HEC_HOIST_MIN: children a trie node needs to be hoisted
-    int hfuse = 1;                 // HEC_HFUSE=0: hoisted node = ks_modup pass B, then k_hmacm per sibling pair
-    int hfuse_bt = 1;              // HEC_HFUSE_BT: batch entries per k_hmacf block at N = 2^14, 2^15 (1 or 2)
     int hmac_cfg = 1;              // HEC_HMAC=0: one hoisted MAC per child (1: sibling pairs fused, k_hmacm)
     int fan_groups_moddown = 1;    // HEC_FANG="moddown,modup,hoist": target groups per k_fan source (blocks
     int fan_groups_modup = 1;      // per launch x groups; the source's inverse pass is repeated per group)
@@ -177,10 +173,6 @@ void hoisted_mac_multi(Ctx &c, PolyArr X1, const u64 *E, const int *zl, const HC
 // three children in one sibling-fused launch (3 x 4 FP64 / 3 x 2 integer batch entries per thread)
 void hoisted_mac_3(Ctx &c, PolyArr X1, const u64 *E, const int *zl, const HChildSpec *kids, int B, int l);
 int hoisted_group(const Ctx &c);  // children per hoisted_mac_multi call for c.hmac_cfg
-// fused hoisted MAC (k_hmacf): the node's pass-A-domain digits E -> pass B in LDS -> the key MACs of up to
-// HMAC_MAX_CHILDREN sibling rotations (HEC_HFUSE=0: ks_modup pass B, then k_hmacm per sibling pair)
-void hoisted_mac_fused(Ctx &c, PolyArr X1, const u64 *E, const int *zl, const HChildSpec *kids, int nkids, int B, int l);
-bool hoisted_mac_fused_fits(const Ctx &c, int l);  // its LDS tile fits a block at level l
 void fan_divide_round(Ctx &c, const u64 *Y, u64 ysb, u64 ysk, u64 *Z, int B, int nk, int nl, int last_idx);
 void galois_permute(Ctx &c, PolyArr in, PolyArr out, int B, int nk, int nl, u32 elt);
 void tensor_acc(Ctx &c, PolyArr R, const u64 *A, u64 a_sk, PolyArr ACC, int B, int l, bool assign);

@@ -1497,288 +1497,6 @@ void hoisted_mac_3(Ctx &c, PolyArr X1, const u64 *E, const int *zl, const HChild
     launch_hmacm<4, 2, 3>(c, X1, E, zl, kids, 3, B, l);
 }
 
-// ============================================ fused hoisted MAC: the digits' pass B in LDS + the children's MAC ==
-// k_hmacf finishes a hoisted node's mod-up NTTs (pass B of every digit E[b][I][J], J != I, which the fan-out leaves
-// in the pass-A domain) in LDS and runs the key MAC of up to HMAC_MAX_CHILDREN sibling rotations from there, so the
-// digits cross HBM once more (read here) instead of three or more times (pass B read + write, one read per sibling
-// pair of k_hmacm).  A block owns one pass-B chunk (P = 2^LOGP contiguous source positions) of one target prime I
-// for BT batch entries (one wave at P = 128, BT = 1) and keeps all l digit tiles of its chunk in LDS (l BT (P + P/16)
-// words: 10.9 KB at cfg3).  A thread owns one source pair of one batch entry and keeps the four accumulators of
-// every child of the launch.  (The fused kernels deleted earlier in round 3, DESIGN.md §10, held several batch
-// entries or all digits of larger tiles per block and ran at 1-2 waves/SIMD.)
-// The MAC is k_hmacm's: the child's output pair is gal_c^-1(s) (keys, W, KW and ACC gathered there, all inside the
-// child's output chunk), the sign-mask term W KW starts the accumulators, the rare zero corrections follow the digit
-// loop.  FP64 targets keep the pass-B outputs as lazy doubles (|v| < 10 q, fp_mulmod's range); the 60-bit targets
-// keep [0, 4 q) words in 128-bit sums (l products < 2^126).
-template <int LOGP, int BT, bool FP>
-__device__ __forceinline__ void hmacf_body(u64 *ltw, u64 *lds, PolyArr X1, const u64 *__restrict__ E,
-                                           const int *__restrict__ zl, const HChildren<HMAC_MAX_CHILDREN> &ch, int B,
-                                           int l, int K, int logN, const DevPrime &pr, const TwTables &tt, int I, int kI,
-                                           int chunk, int b0, const u64 *__restrict__ cji,
-                                           const u64 *__restrict__ psipow)
-{
-    constexpr int P = 1 << LOGP, PAIRS = P / 2, THREADS = PAIRS * BT, LD = P + P / 16, EPT = 8, TPT = P / EPT;
-    constexpr int CONC = THREADS / TPT;
-    const u64 N = 1ull << logN, base = (u64)chunk << LOGP;
-    const int nb = min(BT, B - b0);
-    {  // the chunk's pass-B twiddles, contiguous in the chunk-major table (tt.b / tt.fb = Ctx::twc / twcf)
-        const ulonglong2 *tw = tt.b + ((u64)kI << logN) + base;
-        const double *twf = tt.fb + ((u64)kI << logN) + base;
-        for (int k = threadIdx.x; k < P - 1; k += THREADS) {
-            const int gi = k;
-            if constexpr (FP) ltw[k] = (u64)__double_as_longlong(twf[gi]);
-            else {
-                const ulonglong2 w = tw[gi];
-                ltw[2 * k] = w.x;
-                ltw[2 * k + 1] = w.y;
-            }
-        }
-    }
-    // every digit tile of the chunk: J != I from E (pass-A domain; FP64 targets hold double bits), J == I the node's
-    // NTT-form c1 (SEAL's reuse of the input), canonical
-#pragma unroll 4
-    for (int t = threadIdx.x; t < BT * l * PAIRS; t += THREADS) {
-        const int p2 = t % PAIRS, tile = t / PAIRS, bb = tile / l, J = tile % l;
-        if (bb >= nb) continue;
-        const int b = b0 + bb;
-        const u64 *src = J == I ? X1.p + (u64)b * X1.sb + ((u64)J << logN)
-                                : E + (((u64)((b * (l + 1) + I) * l + J)) << logN);
-        ulonglong2 v = *(const ulonglong2 *)(src + base + 2 * p2);
-        if constexpr (FP) {
-            if (J == I) v = ulonglong2{(u64)__double_as_longlong(u2d(v.x)), (u64)__double_as_longlong(u2d(v.y))};
-        }
-        u64 *d = lds + tile * LD + 2 * p2 + (p2 >> 3);
-        d[0] = v.x;
-        d[1] = v.y;
-    }
-    __syncthreads();
-    const LdsTw twg{ltw};
-    for (int t0 = 0; t0 < BT * l; t0 += CONC) {  // pass B of the J != I tiles, CONC transforms at a time
-        const int tile = t0 + (int)threadIdx.x / TPT, ts = (int)threadIdx.x % TPT;
-        const bool act = tile < BT * l && tile / l < nb && tile % l != I;
-        const int r0 = act ? tile * LD : 0;
-        auto addr = [r0](int x) { return r0 + x + (x >> 4); };
-        static_assert(LOGP >= 5 && LOGP <= 8, "pass-B sizes 2^5 .. 2^8");
-        if constexpr (LOGP <= 6) {
-            if (act) ntt_round_g<LOGP, 0, 3, EPT, false, FP, false>(lds, addr, ts, twg, pr, nullptr);
-            __syncthreads();
-            if (act) ntt_round_g<LOGP, 3, LOGP, EPT, false, FP, false>(lds, addr, ts, twg, pr, nullptr);
-        } else {
-            if (act) ntt_round_g<LOGP, 0, 3, EPT, false, FP, false>(lds, addr, ts, twg, pr, nullptr);
-            __syncthreads();
-            if (act) ntt_round_g<LOGP, 3, 6, EPT, false, FP, false>(lds, addr, ts, twg, pr, nullptr);
-            __syncthreads();
-            if (act) ntt_round_g<LOGP, 6, LOGP, EPT, false, FP, false>(lds, addr, ts, twg, pr, nullptr);
-        }
-        __syncthreads();
-    }
-    const int p = (int)threadIdx.x % PAIRS, bb = (int)threadIdx.x / PAIRS;
-    if (bb >= nb) return;  // after the last barrier
-    const int b = b0 + bb;
-    const u64 s0 = base + 2 * p;
-    const u64 *ev = lds + bb * l * LD + 2 * p + (p >> 3);  // digit J of this source pair: ev[J LD], ev[J LD + 1]
-    const bool zeros = zl[0] != 0;
-    const u64 *pp = psipow + ((u64)kI << (logN + 1));
-    // the children in passes of CG with their accumulators live (digit loop outside, children inside): per digit the
-    // pass's key words are independent loads issued together, so a block waits for l load latencies per pass instead
-    // of l per child.  CG = 3 FP64 / 2 integer children keep the kernel near 128 VGPRs.
-    constexpr int CG = FP ? 3 : 2;
-    const u64 kstep = (u64)K << logN;
-    for (int q0 = 0; q0 < ch.n; q0 += CG) {
-    const int nk = min(CG, ch.n - q0);
-    const HChild *cs = ch.c + q0;
-    u64 kc[CG];
-    bool sw[CG];
-    double f[FP ? CG : 1][4];
-    U128 a[FP ? 1 : CG][4];
-#pragma unroll
-    for (int q = 0; q < CG; ++q) {  // output pairs and the sign-mask terms W KW in source order (slot 0 = s0)
-        kc[q] = 0;
-        sw[q] = false;
-        ulonglong2 wv{0, 0}, m0{0, 0}, m1{0, 0};
-        if (q < nk) {
-            const HChild &cc = cs[q];
-            const u32 t = galois_src((u32)s0, cc.einv, logN);
-            kc[q] = t & ~1u;
-            sw[q] = t & 1;
-            wv = *(const ulonglong2 *)(cc.W + ((u64)kI << logN) + kc[q]);
-            m0 = *(const ulonglong2 *)(cc.KW + ((u64)I << logN) + kc[q]);
-            m1 = *(const ulonglong2 *)(cc.KW + ((u64)(l + 1 + I) << logN) + kc[q]);
-        }
-        if constexpr (FP) {  // lazy products, canonicalised with the sum
-            const double x0 = fp_mulmod(u2d(wv.x), u2d(m0.x), pr.qd, pr.qinv);
-            const double x1 = fp_mulmod(u2d(wv.y), u2d(m0.y), pr.qd, pr.qinv);
-            const double y0 = fp_mulmod(u2d(wv.x), u2d(m1.x), pr.qd, pr.qinv);
-            const double y1 = fp_mulmod(u2d(wv.y), u2d(m1.y), pr.qd, pr.qinv);
-            f[q][0] = sw[q] ? x1 : x0;
-            f[q][1] = sw[q] ? x0 : x1;
-            f[q][2] = sw[q] ? y1 : y0;
-            f[q][3] = sw[q] ? y0 : y1;
-        } else {
-            const u64 x0 = mulmod(wv.x, m0.x, pr), x1 = mulmod(wv.y, m0.y, pr);
-            const u64 y0 = mulmod(wv.x, m1.x, pr), y1 = mulmod(wv.y, m1.y, pr);
-            a[q][0] = U128{sw[q] ? x1 : x0, 0};
-            a[q][1] = U128{sw[q] ? x0 : x1, 0};
-            a[q][2] = U128{sw[q] ? y1 : y0, 0};
-            a[q][3] = U128{sw[q] ? y0 : y1, 0};
-        }
-    }
-#pragma unroll 2
-    for (int J = 0; J < l; ++J) {
-        ulonglong2 k0[CG], k1[CG];
-#pragma unroll
-        for (int q = 0; q < CG; ++q) {
-            if (q < nk) {
-                const u64 *kj = cs[q].key + ((u64)kI << logN) + kc[q] + (u64)(2 * J) * kstep;
-                k0[q] = *(const ulonglong2 *)kj;
-                k1[q] = *(const ulonglong2 *)(kj + kstep);
-            }
-        }
-        const u64 e0 = ev[J * LD], e1 = ev[J * LD + 1];
-#pragma unroll
-        for (int q = 0; q < CG; ++q) {
-            if (q >= nk) break;
-            const u64 ka = sw[q] ? k0[q].y : k0[q].x, kb = sw[q] ? k0[q].x : k0[q].y;  // source slots s0, s0 + 1
-            const u64 kc0 = sw[q] ? k1[q].y : k1[q].x, kc1 = sw[q] ? k1[q].x : k1[q].y;
-            if constexpr (FP) {
-                const double d0 = __longlong_as_double((long long)e0), d1 = __longlong_as_double((long long)e1);
-                f[q][0] += fp_mulmod(d0, u2d(ka), pr.qd, pr.qinv);
-                f[q][1] += fp_mulmod(d1, u2d(kb), pr.qd, pr.qinv);
-                f[q][2] += fp_mulmod(d0, u2d(kc0), pr.qd, pr.qinv);
-                f[q][3] += fp_mulmod(d1, u2d(kc1), pr.qd, pr.qinv);
-            } else {
-                mac128(a[q][0], e0, ka);
-                mac128(a[q][1], e1, kb);
-                mac128(a[q][2], e0, kc0);
-                mac128(a[q][3], e1, kc1);
-            }
-        }
-    }
-    if (zeros) {  // the rare zero corrections (k_hmacm's), + (q - corr) key_J at the output slots
-        for (int J = 0; J < l; ++J) {
-            if (J == I) continue;
-            const int *z = zl + 1 + (b * l + J) * (HEC_ZCAP + 1);
-            const int nz = min(z[0], HEC_ZCAP);
-            if (nz == 0) continue;
-            const u64 cj = cji[J * K + kI];
-#pragma unroll
-            for (int q = 0; q < CG; ++q) {
-                if (q >= nk) break;
-                const u64 ko0 = kc[q] | (u64)sw[q], ko1 = kc[q] | (u64)!sw[q];
-                u64 c0 = 0, c1 = 0;
-                for (int zi = 0; zi < nz; ++zi) {
-                    u64 tt2 = ((u64)z[1 + zi] * cs[q].elt) & (2 * N - 1);
-                    if (tt2 < N) continue;
-                    tt2 -= N;
-                    const u64 ex0 = ((2 * (u64)bitrev((u32)ko0, logN) + 1) * tt2) & (2 * N - 1);
-                    const u64 ex1 = ((2 * (u64)bitrev((u32)ko1, logN) + 1) * tt2) & (2 * N - 1);
-                    c0 = addmod(c0, mulmod(cj, pp[ex0], pr), pr.q);
-                    c1 = addmod(c1, mulmod(cj, pp[ex1], pr), pr.q);
-                }
-                if (c0 == 0 && c1 == 0) continue;
-                const u64 z0 = c0 ? pr.q - c0 : 0, z1 = c1 ? pr.q - c1 : 0;
-                const u64 *kj = cs[q].key + ((u64)kI << logN) + kc[q] + (u64)(2 * J) * kstep;
-                const ulonglong2 q0 = *(const ulonglong2 *)kj, q1 = *(const ulonglong2 *)(kj + kstep);
-                const u64 ka = sw[q] ? q0.y : q0.x, kb = sw[q] ? q0.x : q0.y;
-                const u64 kc0 = sw[q] ? q1.y : q1.x, kc1 = sw[q] ? q1.x : q1.y;
-                if constexpr (FP) {
-                    f[q][0] += fp_mulmod(u2d(z0), u2d(ka), pr.qd, pr.qinv);
-                    f[q][1] += fp_mulmod(u2d(z1), u2d(kb), pr.qd, pr.qinv);
-                    f[q][2] += fp_mulmod(u2d(z0), u2d(kc0), pr.qd, pr.qinv);
-                    f[q][3] += fp_mulmod(u2d(z1), u2d(kc1), pr.qd, pr.qinv);
-                } else {
-                    mac128(a[q][0], z0, ka);
-                    mac128(a[q][1], z1, kb);
-                    mac128(a[q][2], z0, kc0);
-                    mac128(a[q][3], z1, kc1);
-                }
-            }
-        }
-    }
-#pragma unroll
-    for (int q = 0; q < CG; ++q) {
-        if (q >= nk) break;
-        u64 r[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            if constexpr (FP) r[i] = fp_canon(f[q][i], pr.qd, pr.qinv);
-            else r[i] = barrett128(a[q][i].lo, a[q][i].hi, pr.q, pr.r0, pr.r1);
-        }
-        u64 *o0 = cs[q].ACC + (((u64)((b * 2 + 0) * (l + 1) + I)) << logN) + kc[q];
-        u64 *o1 = cs[q].ACC + (((u64)((b * 2 + 1) * (l + 1) + I)) << logN) + kc[q];
-        *(ulonglong2 *)o0 = sw[q] ? ulonglong2{r[1], r[0]} : ulonglong2{r[0], r[1]};
-        *(ulonglong2 *)o1 = sw[q] ? ulonglong2{r[3], r[2]} : ulonglong2{r[2], r[3]};
-    }
-    }
-}
-
-// 1-D grid, XCD-aware as k_bmac: the batch groups of one (chunk, I) run on one XCD and share its L2 copy of the
-// children's key chunks.  Imap lists the integer target primes first (their blocks are the slowest).
-template <int LOGP, int BT>
-__global__ void __launch_bounds__((1 << LOGP) / 2 * BT)
-    k_hmacf(PolyArr X1, const u64 *__restrict__ E, const int *__restrict__ zl, const HChildren<HMAC_MAX_CHILDREN> ch,
-            int B, int l, int K, int logN, const DevPrime *__restrict__ primes, TwTables tt,
-            const int *__restrict__ Imap, int nI, int nint, const u64 *__restrict__ cji,
-            const u64 *__restrict__ psipow)
-{
-    extern __shared__ u64 hf_lds[];  // [2 P] twiddles, then BT l tiles of P + P/16 words
-    constexpr int P = 1 << LOGP;
-    const int nbg = (B + BT - 1) / BT;
-    const int w = blockIdx.x, g8 = w & 7, rest = w >> 3, bg = rest % nbg, G = (rest / nbg) * 8 + g8;
-    const int X = 1 << (logN - LOGP);
-    if (G >= X * nI) return;
-    const int yi = G / X, chunk = G % X;
-    const int I = Imap[yi];
-    const int kI = I == l ? K - 1 : I;
-    const DevPrime pr = primes[kI];
-    if (yi < nint)
-        hmacf_body<LOGP, BT, false>(hf_lds, hf_lds + 2 * P, X1, E, zl, ch, B, l, K, logN, pr, tt, I, kI, chunk, bg * BT,
-                                    cji, psipow);
-    else
-        hmacf_body<LOGP, BT, true>(hf_lds, hf_lds + 2 * P, X1, E, zl, ch, B, l, K, logN, pr, tt, I, kI, chunk, bg * BT,
-                                   cji, psipow);
-}
-
-template <int LOGP, int BT>
-static void launch_hmacf(Ctx &c, PolyArr X1, const u64 *E, const int *zl, const HChildSpec *kids, int nkids, int B,
-                         int l)
-{
-    constexpr int P = 1 << LOGP, THREADS = P / 2 * BT, LD = P + P / 16;
-    HChildren<HMAC_MAX_CHILDREN> ch{};
-    ch.n = nkids;
-    for (int q = 0; q < nkids; ++q)
-        ch.c[q] = HChild{kids[q].elt, kids[q].einv, kids[q].key, kids[q].W, kids[q].ACC, kids[q].KW};
-    const std::size_t shm = (std::size_t)(2 * P + BT * l * LD) * sizeof(u64);
-    if (shm > 65536) throw std::invalid_argument("hoisted_mac_fused: LDS tile too large for this level");
-    const int X = (int)(c.N >> LOGP), gpad = (X * (l + 1) + 7) / 8 * 8, nbg = (B + BT - 1) / BT;
-    const TwTables fwd{c.tw, c.twc, c.twf, c.twcf};  // pass B from the chunk-major table
-    k_hmacf<LOGP, BT><<<dim3((unsigned)(gpad * nbg)), THREADS, shm, c.stream>>>(
-        X1, E, zl, ch, B, l, (int)c.K, c.logN, c.primes, fwd, c.imap_at(l), l + 1, c.imap_nint[l], c.cji, c.psipow);
-    HEC_HIP(hipGetLastError());
-}
-
-bool hoisted_mac_fused_fits(const Ctx &c, int l)
-{
-    const int logp = c.logN - c.logR, P = 1 << logp, bt = logp <= 5 ? 4 : logp == 6 ? 2 : logp == 7 ? c.hfuse_bt : 1;
-    return (std::size_t)(2 * P + bt * l * (P + P / 16)) * sizeof(u64) <= 65536;
-}
-
-void hoisted_mac_fused(Ctx &c, PolyArr X1, const u64 *E, const int *zl, const HChildSpec *kids, int nkids, int B, int l)
-{
-    if (nkids < 1 || nkids > HMAC_MAX_CHILDREN) throw std::invalid_argument("hoisted_mac_fused: children per launch");
-    if (l > HEC_MAXL) throw std::invalid_argument("too many limbs");
-    switch (c.logN - c.logR) {  // <pass-B size, batch entries per block>: 64-thread blocks at P <= 128
-    case 5: launch_hmacf<5, 4>(c, X1, E, zl, kids, nkids, B, l); break;
-    case 6: launch_hmacf<6, 2>(c, X1, E, zl, kids, nkids, B, l); break;
-    case 7:
-        if (c.hfuse_bt == 2) launch_hmacf<7, 2>(c, X1, E, zl, kids, nkids, B, l);
-        else launch_hmacf<7, 1>(c, X1, E, zl, kids, nkids, B, l);
-        break;
-    case 8: launch_hmacf<8, 1>(c, X1, E, zl, kids, nkids, B, l); break;
-    default: throw std::invalid_argument("poly_modulus_degree must be 2^10 .. 2^16");
-    }
-}
-
 void fan_divide_round(Ctx &c, const u64 *Y, u64 ysb, u64 ysk, u64 *Z, int B, int nk, int nl, int last_idx)
 {
     if (nl > HEC_MAXL) throw std::invalid_argument("too many limbs");
