@@ -41,17 +41,18 @@ def test_launcher_command(bench):
     assert cmd[8:] == ["--gpus", "8", "--steps", "3"]
 
 
-def test_gpus_2_launches_two_ranks_one_line():
-    """`bench.py --gpus 2` with no WORLD_SIZE starts 2 ranks itself (gloo dry run: no GPU) and exactly one JSON line
+@pytest.mark.parametrize("gpus", [2, 4])
+def test_gpus_n_launches_n_ranks_one_line(gpus):
+    """`bench.py --gpus N` with no WORLD_SIZE starts N ranks itself (gloo dry run: no GPU) and exactly one JSON line
     comes out, from rank 0, with the world size the process group saw."""
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR",
                                                              "MASTER_PORT")}
-    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run", "--steps", "2",
-                          "--warmup", "1"], capture_output=True, text=True, env=env, timeout=300, check=True)
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(gpus), "--dry-run", "--steps",
+                          "2", "--warmup", "1"], capture_output=True, text=True, env=env, timeout=300, check=True)
     lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, out.stdout
     r = json.loads(lines[0])
-    assert r["n_gpus"] == 2 and r["rccl_world"] == 2 and r["dry_run"] and r["steps"] == 2
+    assert r["n_gpus"] == gpus and r["rccl_world"] == gpus and r["dry_run"] and r["steps"] == 2
 
 
 def test_cpu_leg_sizing(bench, monkeypatch):

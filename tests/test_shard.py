@@ -121,13 +121,15 @@ def _worker(rank, world, port, p, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("p", [2, 3])  # 2: reduce-scatter path, 3: all-reduce + round robin
-def test_gloo_world2_exchange_bit_exact(shard, p):
+# p == world: the reduce-scatter path; otherwise all-reduce + round-robin owners.  World 4 rehearses the exchange
+# the driver's multi-GPU runs use over RCCL, on gloo (CPU).
+@pytest.mark.parametrize("world,p", [(2, 2), (2, 3), (4, 4), (4, 5)])
+def test_gloo_world2_exchange_bit_exact(shard, world, p):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, p, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, p, q)) for r in range(world)]
     for pr in procs:
         pr.start()
     res = [q.get(timeout=300) for _ in procs]
