@@ -365,7 +365,7 @@ void moddown(Ctx &c, u64 *ACC, u64 *Z, PolyArr IN, int in_nk, PolyArr OUT, int B
         ntt_strided(c, true, ACC + l * N, (l + 1) * N, ACC + l * N, (l + 1) * N, 1, pP, 2 * B, 1, fan ? 1 : 3);
     }
     if (fan) {  // 2B P limbs -> 2B l rounding limbs (pass-A domain)
-        ProfScope k(c, c.fan2 ? "k:k_fan2/moddown" : "k:k_fan/moddown", 2.0 * B * (l + 1));
+        ProfScope k(c, "k:k_fan2/moddown", 2.0 * B * (l + 1));
         fan_divide_round(c, ACC + l * N, 2 * (l + 1) * N, (l + 1) * N, Z, B, 2, l, (int)c.K - 1);
     }
     {  // Z (2Bl), ACC data limbs (2Bl), IN (in_nk B l), OUT (2Bl)
@@ -392,7 +392,7 @@ void moddown_group(Ctx &c, u64 *ACC, u64 *Z, PolyArr IN, const PolyArr *OUT, con
         ntt_strided(c, true, ACC + l * N, (l + 1) * N, ACC + l * N, (l + 1) * N, 1, pP, 2 * B * ng, 1, 1);
     }
     {
-        ProfScope k(c, c.fan2 ? "k:k_fan2/moddown" : "k:k_fan/moddown", 2.0 * B * ng * (l + 1));
+        ProfScope k(c, "k:k_fan2/moddown", 2.0 * B * ng * (l + 1));
         fan_divide_round(c, ACC + l * N, 2 * (l + 1) * N, (l + 1) * N, Z, B * ng, 2, l, (int)c.K - 1);
     }
     for (int q = 0; q < ng; ++q) {
@@ -424,7 +424,7 @@ void keyswitch(Ctx &c, Scratch &s, PolyArr T, const u64 *key, PolyArr IN, int in
     if (c.fused_modup_mac) {  // mod-up pass A, then pass B fused with the key MAC (no E round trip)
         {
             ProfScope ps(c, "ks_modup_a");
-            ProfScope k(c, fan ? (c.fan2 ? "k:k_fan2/modup" : "k:k_fan/modup") : "k:k_ntt/modup_a", (double)B * l * (l + 1), 1);
+            ProfScope k(c, fan ? "k:k_fan2/modup" : "k:k_ntt/modup_a", (double)B * l * (l + 1), 1);
             if (fan) fan_modup(c, D, E, B, l);
             else ks_modup_mac(c, D, E, T, key, ACC, B, l, 1, elt);
         }
@@ -480,7 +480,7 @@ void hoist_node(Ctx &c, PolyArr X, int B, int l, const Hoist &h)
     const u64 N = c.N;
     int pmap[HEC_MAXL + 1];
     for (int i = 0; i <= HEC_MAXL; ++i) pmap[i] = i;
-    if (c.fan2 && c.hoist_scan) {  // the fan-out finishes the INTT and lists the zeros: no D round trip
+    if (c.hoist_scan) {  // the fan-out finishes the INTT and lists the zeros: no D round trip
         {
             ProfScope ps(c, "ks_intt");
             ProfScope k(c, "k:k_ntt/intt_b", 2.0 * B * l);
@@ -510,7 +510,7 @@ void hoist_node(Ctx &c, PolyArr X, int B, int l, const Hoist &h)
     }
     ProfScope ps(c, "ks_modup_h");
     {
-        ProfScope k(c, c.fan2 ? "k:k_fan2/hoist" : "k:k_fan/hoist", (double)B * l * (l + 1));
+        ProfScope k(c, "k:k_fan2/hoist", (double)B * l * (l + 1));
         fan_modup(c, h.D, h.E, B, l, true);  // pass A of every NTT_I(D_J mod q_I), from the canonical D
     }
     ProfScope k(c, "k:k_ntt/modup_h_b", 2.0 * B * l * l);
@@ -880,7 +880,7 @@ void matvec_core(hec_context *ctx, const hec_ciphertext *const *diags, const hec
         ProfScope pr(c, "tensor");
         // T rotated inputs (2 B l each) + T diagonals (2 l, or l plaintext) + ACC read (unless first) + write
         const double accl = (pt ? 2.0 : 3.0) * p * l;
-        ProfScope k(c, c.tensor_bg ? "k:k_tensor_multi2" : "k:k_tensor_multi", tb.T * (2.0 * p * l + (pt ? 1.0 : 2.0) * l) + (first ? 1 : 2) * accl);
+        ProfScope k(c, "k:k_tensor_multi2", tb.T * (2.0 * p * l + (pt ? 1.0 : 2.0) * l) + (first ? 1 : 2) * accl);
         tensor_multi(c, tb, S2, l * N, l * N, Aa, (int)p, (int)l, first, pt);
         first = false;
         tb.T = 0;
@@ -1252,15 +1252,9 @@ int hec_context_create(uint64_t N, const uint64_t *mod, uint64_t K, int device, 
         if (const char *f = std::getenv("HEC_FUSED_MODUP_MAC")) c.fused_modup_mac = f[0] != '0';
         if (const char *f = std::getenv("HEC_FUSE_GALOIS")) c.fuse_galois = f[0] != '0';
         if (const char *f = std::getenv("HEC_FAN")) c.fan_out = f[0] != '0';
-        if (const char *f = std::getenv("HEC_FAN2")) c.fan2 = std::atoi(f);
-        if (const char *f = std::getenv("HEC_FANSPLIT")) c.fan_split = std::atoi(f);
         if (const char *f = std::getenv("HEC_NTT_RD")) c.ntt_rd = std::atoi(f);
         if (const char *f = std::getenv("HEC_HOIST_SCAN")) c.hoist_scan = std::atoi(f);
-        if (const char *f = std::getenv("HEC_DIVROUND_FP")) c.divround_fp = std::atoi(f);
-        if (const char *f = std::getenv("HEC_TENSOR_BG")) c.tensor_bg = std::atoi(f);
         if (const char *f = std::getenv("HEC_LANES")) c.lanes = std::max(1, std::atoi(f));
-        if (const char *f = std::getenv("HEC_FANG"))
-            std::sscanf(f, "%d,%d,%d", &c.fan_groups_moddown, &c.fan_groups_modup, &c.fan_groups_hoist);
         if (const char *f = std::getenv("HEC_HOIST")) c.hoist = f[0] != '0';
         if (const char *f = std::getenv("HEC_HMAC")) c.hmac_cfg = std::atoi(f);
         if (const char *f = std::getenv("HEC_HMAC_ODD3")) c.hmac_odd3 = std::atoi(f);

@@ -86,21 +86,13 @@ struct Ctx {
     std::vector<std::vector<u64>> ql_inv, ql_inv_q, ql_half_mod;  // rescale at level l (drop prime l-1)
     int tensor_defer_max = 12;     // HEC_TENSOR_DEFER: terminals per deferred tensor batch (1 = immediate)
     int tensor_defer_bufs = 8;     // HEC_TENSOR_BUFS: rotation buffers per trie depth
-    int tensor_bg = 1;             // HEC_TENSOR_BG=0: k_tensor_multi (one thread per coefficient, whole batch)
     bool hoist = true;             // HEC_HOIST=0: no hoisted mod-up in the rotation trie walk
     int hoist_min_children = 2;    // HEC_HOIST_MIN: children a trie node needs to be hoisted
     int hmac_cfg = 1;              // HEC_HMAC=0: one hoisted MAC per child (1: sibling pairs fused, k_hmacm)
-    int fan_groups_moddown = 1;    // HEC_FANG="moddown,modup,hoist": target groups per k_fan source (blocks
-    int fan_groups_modup = 1;      // per launch x groups; the source's inverse pass is repeated per group)
-    int fan_groups_hoist = 1;
-    int divround_fp = 1;           // HEC_DIVROUND_FP=0: the mod-down post-op on u64 (Shoup) at FP64 primes too
     int hoist_scan = 1;            // HEC_HOIST_SCAN=0: hoisted node as INTT pass B, pass A, k_zscan, direct fan-out
                                    // (1: INTT pass B, then the fan-out finishes the INTT and lists the zeros)
     int ntt_rd = 1;                // HEC_NTT_RD=0: k_ntt stages every round through LDS (ntt_pass_body)
     int hmac_odd3 = 1;             // HEC_HMAC_ODD3=0: an odd sibling group ends in a pair and a single-child launch
-    int fan_split = 1;             // HEC_FANSPLIT=0: Barrett (not the FP64 split) for the mod-down rounding limbs
-                                   // at FP64 targets (FanDivRound::xf16)
-    int fan2 = 1;                  // HEC_FAN2=0: the LDS-round k_fan instead of the register-direct k_fan2
     bool fan_out = true;           // HEC_FAN=0: separate INTT pass A (fan-out fuses it into the forward passes A)
     int lanes = 3;                 // HEC_LANES: concurrent batch lanes of a matvec (hec_engine.hip matvec_lanes)
     int lane_min_batch = 16;       // input vectors per lane at least

@@ -670,7 +670,7 @@ void divide_round(Ctx &c, const u64 *Y, u64 ysb, u64 ysk, PolyArr X, PolyArr IN,
     DivRoundIO_B b{};
     b.Z = Z; b.X = X; b.IN = IN; b.OUT = OUT; b.nk = nk; b.nl = nl; b.logN = c.logN; b.in_nk = in_nk; b.elt = in_elt;
     b.primes = c.primes;
-    b.fpstore = c.divround_fp;
+    b.fpstore = 1;
     for (int i = 0; i < nl; ++i) { b.inv[i] = inv[i]; b.inv_q[i] = inv_q[i]; }
     ntt_dispatch<false>(c, B * nk * nl, a, b, stages);
 }
@@ -814,79 +814,6 @@ struct FanDivRound {  // source (b, k) = last limb (inverse pass-B domain) -> Z[
     }
 };
 
-template <int LOGP, int NSEG, bool FP, class Lds>
-__device__ __forceinline__ void fan_rounds(u64 *lds, const Lds &addr, int ts, const TwTables &tt, const DevPrime &pr,
-                                           int prime, int logN, bool inverse)
-{
-    auto twidx = [](int s, int i) -> u64 { return (1ull << s) + (u64)i; };
-    const ulonglong2 *tw = tt.a + ((u64)prime << logN);
-    const double *twf = tt.fa + ((u64)prime << logN);
-    if (!inverse) {
-        ntt_round<LOGP, 0, false, FP>(lds, addr, ts, twidx, tw, twf, pr);
-        __syncthreads();
-        ntt_round<LOGP, 1, false, FP>(lds, addr, ts, twidx, tw, twf, pr);
-    } else {
-        ntt_round<LOGP, 1, true, FP>(lds, addr, ts, twidx, tw, twf, pr);
-        __syncthreads();
-        ntt_round<LOGP, 0, true, FP>(lds, addr, ts, twidx, tw, twf, pr);
-    }
-}
-
-template <int LOGP, int NSEG, class FAN>
-__global__ void __launch_bounds__(NSEG *(1 << LOGP) / 16)
-    k_fan(const FAN fan, TwTables inv, TwTables fwd, const DevPrime *__restrict__ primes, int logN)
-{
-    constexpr int P = 1 << LOGP, THREADS = NSEG * P / 16, LD = NSEG + 1, ITS = 16;
-    __shared__ u64 lds[P * LD];
-    const int seg0 = blockIdx.x * NSEG, lc = logN - LOGP;
-    const int ts = threadIdx.x / NSEG, sg = threadIdx.x % NSEG;
-    auto addr = [sg](int x) { return x * LD + sg; };
-    auto gidx = [&](int it) { const int li = threadIdx.x + it * THREADS; return ((u64)(li / NSEG) << lc) + seg0 + li % NSEG; };
-    auto lidx = [&](int it) { const int li = threadIdx.x + it * THREADS; return (li / NSEG) * LD + li % NSEG; };
-    const auto src = fan.src(blockIdx.y);
-    const DevPrime ps = primes[src.prime];
-    u64 d[ITS];  // canonical coefficient-form values of the source limb
-    if constexpr (FAN::kDirect) {
-#pragma unroll
-        for (int it = 0; it < ITS; ++it) d[it] = src.in[gidx(it)];
-    } else {
-#pragma unroll
-        for (int it = 0; it < ITS; ++it) lds[lidx(it)] = src.in[gidx(it)];
-        __syncthreads();
-        if (ps.fp) fan_rounds<LOGP, NSEG, true>(lds, addr, ts, inv, ps, src.prime, logN, true);
-        else fan_rounds<LOGP, NSEG, false>(lds, addr, ts, inv, ps, src.prime, logN, true);
-        __syncthreads();
-#pragma unroll
-        for (int it = 0; it < ITS; ++it) {
-            const u64 v = lds[lidx(it)];
-            if (ps.fp) d[it] = fp_canon(fp_mulmod(__longlong_as_double((long long)v), ps.ninv_d, ps.qd, ps.qinv), ps.qd, ps.qinv);
-            else d[it] = shoup(v, ps.ninv, ps.ninv_q, ps.q);
-            d[it] = fan.src_fix(d[it]);
-        }
-    }
-    // target group blockIdx.z of gridDim.z: more blocks per launch when the job count is small (the
-    // source pass is then repeated per group)
-    const int nt = fan.ntargets(), t0 = blockIdx.z * nt / gridDim.z, t1 = (blockIdx.z + 1) * nt / gridDim.z;
-    for (int t = t0; t < t1; ++t) {
-        const auto tg = fan.tgt(blockIdx.y, t);
-        if (!tg.valid) continue;
-        const DevPrime pt = primes[tg.prime];
-        __syncthreads();  // the previous target's tile has been read out
-#pragma unroll
-        for (int it = 0; it < ITS; ++it) {
-            u64 v = fan.xf(tg, d[it]);
-            if (pt.fp) v = (u64)__double_as_longlong(u2d(v));
-            lds[lidx(it)] = v;
-        }
-        __syncthreads();
-        if (pt.fp) fan_rounds<LOGP, NSEG, true>(lds, addr, ts, fwd, pt, tg.prime, logN, false);
-        else fan_rounds<LOGP, NSEG, false>(lds, addr, ts, fwd, pt, tg.prime, logN, false);
-        __syncthreads();
-#pragma unroll
-        for (int it = 0; it < ITS; ++it) tg.out[gidx(it)] = lds[lidx(it)];
-    }
-}
-
 // ------------------------------------------------------------------ register-direct fan-out (k_fan2)
 // The stages of one round on 16 register-resident elements: thread ts of a P = 2^LOGP point column holds the
 // elements ntt_round_g gives it for stages [S0, S1): v[gi 2^D + a] <-> x = xb(ts G + gi) | (a << (LOGP - S1)).
@@ -928,10 +855,10 @@ __device__ __forceinline__ void ntt_round_r(u64 *v, int ts, const TwG &twg, cons
     }
 }
 
-// k_fan with the NTT rounds on registers: the source is loaded straight into the thread's element set and
+// The fan-out with the NTT rounds on registers: the source is loaded straight into the thread's element set and
 // the target tiles are stored straight from it, so each transform (the INTT and every target's forward
-// pass) exchanges through LDS once instead of three times, with one barrier per exchange (two LDS tiles
-// alternate between consecutive exchanges).  Same inputs, outputs and intermediate formats as k_fan.
+// pass) exchanges through LDS once (round 1's LDS-round k_fan exchanged three times; deleted in round 3), with one
+// barrier per exchange (two LDS tiles alternate between consecutive exchanges).
 // DB: two alternating LDS tiles and one barrier per exchange (2 blocks per CU at N = 2^15); DB = false: one
 // tile and a second barrier per target.  (One tile with 3 waves per SIMD forced, 168 VGPRs and 20-30 spilled,
 // measured slower: k_fan 3,565 vs 2,601 ms per step.)
@@ -1022,8 +949,7 @@ static void run_fan(Ctx &c, int njobs, const FAN &fan, int groups)
 {
     constexpr int R = 1 << LOGR, C = 1 << LOGC;
     const TwTables fwd{c.tw, c.twb, c.twf, c.twbf}, inv{c.itw, c.itwb, c.itwf, c.itwbf};
-    if (c.fan2) k_fan2<LOGR, NA><<<dim3(C / NA, njobs, groups), NA * R / 16, 0, c.stream>>>(fan, inv, fwd, c.primes, c.logN);
-    else k_fan<LOGR, NA><<<dim3(C / NA, njobs, groups), NA * R / 16, 0, c.stream>>>(fan, inv, fwd, c.primes, c.logN);
+    k_fan2<LOGR, NA><<<dim3(C / NA, njobs, groups), NA * R / 16, 0, c.stream>>>(fan, inv, fwd, c.primes, c.logN);
     HEC_HIP(hipGetLastError());
 }
 template <class FAN>
@@ -1044,7 +970,7 @@ static void fan_dispatch(Ctx &c, int njobs, const FAN &fan, int groups = 1)
 
 void fan_modup(Ctx &c, const u64 *D, u64 *E, int B, int l, bool direct, int *zl)
 {
-    const int g = std::min(direct || zl ? c.fan_groups_hoist : c.fan_groups_modup, l + 1);
+    const int g = 1;  // target groups per source (gridDim.z): more than one measured slower
     if (direct) {
         fan_dispatch(c, B * l, FanModUpT<true>{D, E, l, c.logN, (int)c.K - 1, c.primes}, g);
         return;
@@ -1505,10 +1431,10 @@ void fan_divide_round(Ctx &c, const u64 *Y, u64 ysb, u64 ysk, u64 *Z, int B, int
     f.last = c.q[last_idx]; f.half = f.last >> 1; f.primes = c.primes;
     for (int i = 0; i < nl; ++i) {
         f.fix[i] = c.q[i] - (f.half % c.q[i]);
-        f.c30[i] = c.fan_split && c.q[i] < (1ull << 42) && c.q[i] > (1ull << 32) ? (double)((1ull << 30) % c.q[i]) : 0.0;
-        if (c.fan_split && f.last < 2 * c.q[i] && i < 32) f.sub1 |= 1u << i;
+        f.c30[i] = c.q[i] < (1ull << 42) && c.q[i] > (1ull << 32) ? (double)((1ull << 30) % c.q[i]) : 0.0;
+        if (f.last < 2 * c.q[i] && i < 32) f.sub1 |= 1u << i;
     }
-    fan_dispatch(c, B * nk, f, std::min(c.fan_groups_moddown, nl));
+    fan_dispatch(c, B * nk, f);
 }
 
 // ====================================================================== fused mod-up B + MAC ==
@@ -1927,63 +1853,8 @@ void tensor_acc(Ctx &c, PolyArr R, const u64 *A, u64 a_sk, PolyArr ACC, int B, i
 // successive k_tensor_acc calls.  FP64 primes: exact fp_mulmod products (|.| <= 0.53 q) summed as
 // integer-valued doubles (|sum| <= 1.6 q T < 2^53), canonicalised once.
 // PT: the A_t are plaintexts (ct x pt: d0 = r0 p, d1 = r1 p, multiply_plain), ACC has 2 polys.
-template <bool PT>
-__global__ void __launch_bounds__(256)
-    k_tensor_multi(TensorBatch tb, u64 r_sb, u64 r_sk, u64 a_sk, PolyArr ACC, int B, int logN, u64 total, int assign,
-                   const DevPrime *__restrict__ primes)
-{
-    const u64 idx = (u64)blockIdx.x * 256 + threadIdx.x;
-    if (idx >= total) return;
-    const DevPrime pr = primes[idx >> logN];
-    for (int b = 0; b < B; ++b) {
-        u64 d0, d1, d2 = 0;
-        if (pr.fp) {
-            double s0 = 0, s1 = 0, s2 = 0;
-            for (int t = 0; t < tb.T; ++t) {
-                const u64 *r = tb.r[t] + b * r_sb;
-                const double r0 = u2d(r[idx]), r1 = u2d(r[r_sk + idx]), a0 = u2d(tb.a[t][idx]);
-                s0 += fp_mulmod(r0, a0, pr.qd, pr.qinv);
-                if constexpr (PT) {
-                    s1 += fp_mulmod(r1, a0, pr.qd, pr.qinv);
-                } else {
-                    const double a1 = u2d(tb.a[t][a_sk + idx]);
-                    s1 += fp_mulmod(r0, a1, pr.qd, pr.qinv) + fp_mulmod(r1, a0, pr.qd, pr.qinv);
-                    s2 += fp_mulmod(r1, a1, pr.qd, pr.qinv);
-                }
-            }
-            d0 = fp_canon(s0, pr.qd, pr.qinv);
-            d1 = fp_canon(s1, pr.qd, pr.qinv);
-            if constexpr (!PT) d2 = fp_canon(s2, pr.qd, pr.qinv);
-        } else {
-            d0 = d1 = 0;
-            for (int t = 0; t < tb.T; ++t) {
-                const u64 *r = tb.r[t] + b * r_sb;
-                const u64 r0 = r[idx], r1 = r[r_sk + idx], a0 = tb.a[t][idx];
-                d0 = addmod(d0, mulmod(r0, a0, pr), pr.q);
-                if constexpr (PT) {
-                    d1 = addmod(d1, mulmod(r1, a0, pr), pr.q);
-                } else {
-                    const u64 a1 = tb.a[t][a_sk + idx];
-                    U128 m{r0 * a1, mulhi64(r0, a1)};
-                    mac128(m, r1, a0);
-                    d1 = addmod(d1, barrett128(m.lo, m.hi, pr.q, pr.r0, pr.r1), pr.q);
-                    d2 = addmod(d2, mulmod(r1, a1, pr), pr.q);
-                }
-            }
-        }
-        u64 *o = ACC.p + b * ACC.sb;
-        if (assign) {
-            o[idx] = d0; o[ACC.sk + idx] = d1;
-            if constexpr (!PT) o[2 * ACC.sk + idx] = d2;
-        } else {
-            o[idx] = addmod(o[idx], d0, pr.q);
-            o[ACC.sk + idx] = addmod(o[ACC.sk + idx], d1, pr.q);
-            if constexpr (!PT) o[2 * ACC.sk + idx] = addmod(o[2 * ACC.sk + idx], d2, pr.q);
-        }
-    }
-}
-
-// k_tensor_multi with the batch split over the grid: a thread owns one coefficient of BG batch entries
+// The deferred tensor products with the batch split over the grid (k_tensor_multi2; round 2's one-thread-per-coefficient
+// k_tensor_multi was deleted in round 3): a thread owns one coefficient of BG batch entries
 // (blockIdx.y picks the group), loads each diagonal word once for its BG entries and keeps BG sets of
 // accumulators, so a wave has BG rotated-input loads in flight per diagonal and the diagonals are re-read
 // B / BG times (from L2) instead of B times.  Products are reduced as SEAL reduces them; sums are exact
@@ -2069,24 +1940,14 @@ void tensor_multi(Ctx &c, const TensorBatch &tb, u64 r_sb, u64 r_sk, u64 a_sk, P
 {
     const u64 total = (u64)l * c.N;
     const unsigned grid = (unsigned)((total + 255) / 256);
-    if (c.tensor_bg > 0) {
-        constexpr int BG = 4;
-        const dim3 g2(grid, (unsigned)((B + BG - 1) / BG));
-        if (plain)
-            k_tensor_multi2<true, BG><<<g2, 256, 0, c.stream>>>(tb, r_sb, r_sk, a_sk, ACC, B, c.logN, total, assign ? 1 : 0,
-                                                               c.primes);
-        else
-            k_tensor_multi2<false, BG><<<g2, 256, 0, c.stream>>>(tb, r_sb, r_sk, a_sk, ACC, B, c.logN, total,
-                                                                assign ? 1 : 0, c.primes);
-        HEC_HIP(hipGetLastError());
-        return;
-    }
+    constexpr int BG = 4;
+    const dim3 g2(grid, (unsigned)((B + BG - 1) / BG));
     if (plain)
-        k_tensor_multi<true><<<grid, 256, 0, c.stream>>>(tb, r_sb, r_sk, a_sk, ACC, B, c.logN, total, assign ? 1 : 0,
-                                                          c.primes);
-    else
-        k_tensor_multi<false><<<grid, 256, 0, c.stream>>>(tb, r_sb, r_sk, a_sk, ACC, B, c.logN, total, assign ? 1 : 0,
+        k_tensor_multi2<true, BG><<<g2, 256, 0, c.stream>>>(tb, r_sb, r_sk, a_sk, ACC, B, c.logN, total, assign ? 1 : 0,
                                                            c.primes);
+    else
+        k_tensor_multi2<false, BG><<<g2, 256, 0, c.stream>>>(tb, r_sb, r_sk, a_sk, ACC, B, c.logN, total,
+                                                            assign ? 1 : 0, c.primes);
     HEC_HIP(hipGetLastError());
 }
 

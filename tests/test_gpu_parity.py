@@ -364,9 +364,7 @@ def test_cfg5_params_matvec_bitexact(orc, hecdna):
                                  {"HEC_FAN": "0"}, {"HEC_FAN": "1", "HEC_FUSE_GALOIS": "0"},
                                  {"HEC_HOIST": "0"}, {"HEC_HOIST_MIN": "1"}, {"HEC_HOIST_MIN": "1", "HEC_FAN": "0"},
                                  {"HEC_HMAC": "0"}, {"HEC_HMAC": "0", "HEC_HOIST_MIN": "1"},
-                                 {"HEC_FANG": "5,2,3"}, {"HEC_FAN2": "0"}, {"HEC_FAN2": "0", "HEC_FANG": "5,2,3"},
-                                 {"HEC_TENSOR_BG": "0"}, {"HEC_TENSOR_BG": "0", "HEC_TENSOR_DEFER": "3"},
-                                 {"HEC_FANSPLIT": "0"}, {"HEC_DIVROUND_FP": "0"}, {"HEC_HMAC_ODD3": "0"},
+                                 {"HEC_HMAC_ODD3": "0"},
                                  {"HEC_HOIST_SCAN": "0"}, {"HEC_NTT_RD": "0"}, {"HEC_NTT_RD": "0", "HEC_HOIST": "0"}])
 def test_keyswitch_variants_bitexact(orc, hecdna, env):
     """The engine's alternative key-switch schedules (separate mod-up pass B + MAC kernels; the fused
