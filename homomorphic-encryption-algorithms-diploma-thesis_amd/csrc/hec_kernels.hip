@@ -563,10 +563,9 @@ __device__ __forceinline__ void ntt_pass_body_rd(u64 *lds, const Bound &bio, con
     }
 }
 
-// CLS 0: per-block branch on the prime's arithmetic class; 1 / 2: an FP64-only / integer-only launch
-// (a smaller register budget for the FP64 kernel when a launch's jobs are all of one class)
-// RD: the register-direct pass (ntt_pass_body_rd)
-template <int LOGP, int NSEG, bool INV, bool PASS_A, bool FINAL, class IO, int CLS = 0, bool RD = false>
+// A per-block branch on the prime's arithmetic class.  RD: the register-direct pass (ntt_pass_body_rd); otherwise
+// every round through LDS (ntt_pass_body: the forward pass B, where register-direct measured slower)
+template <int LOGP, int NSEG, bool INV, bool PASS_A, bool FINAL, class IO, bool RD = false>
 __global__ void __launch_bounds__(NSEG *(1 << LOGP) / 16)
     k_ntt(const IO io, TwTables tt, const DevPrime *__restrict__ primes, int logN)
 {
@@ -580,9 +579,7 @@ __global__ void __launch_bounds__(NSEG *(1 << LOGP) / 16)
     if constexpr (RD) {
         if (pr.fp) ntt_pass_body_rd<LOGP, NSEG, INV, PASS_A, FINAL, true>(lds, bio, pr, tt, logN);
         else ntt_pass_body_rd<LOGP, NSEG, INV, PASS_A, FINAL, false>(lds, bio, pr, tt, logN);
-    } else if constexpr (CLS == 1) ntt_pass_body<LOGP, NSEG, INV, PASS_A, FINAL, true>(lds, bio, pr, tt, logN);
-    else if constexpr (CLS == 2) ntt_pass_body<LOGP, NSEG, INV, PASS_A, FINAL, false>(lds, bio, pr, tt, logN);
-    else if (pr.fp) ntt_pass_body<LOGP, NSEG, INV, PASS_A, FINAL, true>(lds, bio, pr, tt, logN);
+    } else if (pr.fp) ntt_pass_body<LOGP, NSEG, INV, PASS_A, FINAL, true>(lds, bio, pr, tt, logN);
     else ntt_pass_body<LOGP, NSEG, INV, PASS_A, FINAL, false>(lds, bio, pr, tt, logN);
 }
 
@@ -593,23 +590,15 @@ static void run_ntt2(Ctx &c, int njobs, const IO1 &first, const IO2 &second, int
     const dim3 gA(C / NA, njobs), gB(R / NB, njobs);
     constexpr int TA = NA * R / 16, TB = NB * C / 16;
     const TwTables fwd{c.tw, c.twb, c.twf, c.twbf}, inv{c.itw, c.itwb, c.itwf, c.itwbf};
-    if (c.ntt_rd) {
-        if constexpr (!INV) {  // the forward pass B stays on ntt_pass_body (register-direct measured slower:
-                               // divide-and-round pass B 1,948 vs 1,894 ms, mod-up pass B 1,152 vs 1,077 ms per step;
-                               // SQ counters: a third fewer LDS and VMEM instructions, no bank conflicts either way,
-                               // but 2.2x the cycles waiting on load dependencies and 15 % more wave cycles)
-            if (stages & 1) k_ntt<LOGR, NA, false, true, false, IO1, 0, true><<<gA, TA, 0, c.stream>>>(first, fwd, c.primes, c.logN);
-            if (stages & 2) k_ntt<LOGC, NB, false, false, true><<<gB, TB, 0, c.stream>>>(second, fwd, c.primes, c.logN);
-        } else {
-            if (stages & 1) k_ntt<LOGC, NB, true, false, false, IO1, 0, true><<<gB, TB, 0, c.stream>>>(first, inv, c.primes, c.logN);
-            if (stages & 2) k_ntt<LOGR, NA, true, true, true, IO2, 0, true><<<gA, TA, 0, c.stream>>>(second, inv, c.primes, c.logN);
-        }
-    } else if constexpr (!INV) {
-        if (stages & 1) k_ntt<LOGR, NA, false, true, false><<<gA, TA, 0, c.stream>>>(first, fwd, c.primes, c.logN);
+    if constexpr (!INV) {  // the forward pass B stays on ntt_pass_body (register-direct measured slower:
+                           // divide-and-round pass B 1,948 vs 1,894 ms, mod-up pass B 1,152 vs 1,077 ms per step;
+                           // SQ counters: a third fewer LDS and VMEM instructions, no bank conflicts either way,
+                           // but 2.2x the cycles waiting on load dependencies and 15 % more wave cycles)
+        if (stages & 1) k_ntt<LOGR, NA, false, true, false, IO1, true><<<gA, TA, 0, c.stream>>>(first, fwd, c.primes, c.logN);
         if (stages & 2) k_ntt<LOGC, NB, false, false, true><<<gB, TB, 0, c.stream>>>(second, fwd, c.primes, c.logN);
     } else {
-        if (stages & 1) k_ntt<LOGC, NB, true, false, false><<<gB, TB, 0, c.stream>>>(first, inv, c.primes, c.logN);
-        if (stages & 2) k_ntt<LOGR, NA, true, true, true><<<gA, TA, 0, c.stream>>>(second, inv, c.primes, c.logN);
+        if (stages & 1) k_ntt<LOGC, NB, true, false, false, IO1, true><<<gB, TB, 0, c.stream>>>(first, inv, c.primes, c.logN);
+        if (stages & 2) k_ntt<LOGR, NA, true, true, true, IO2, true><<<gA, TA, 0, c.stream>>>(second, inv, c.primes, c.logN);
     }
     HEC_HIP(hipGetLastError());
 }
