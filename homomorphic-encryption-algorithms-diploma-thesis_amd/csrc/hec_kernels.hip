@@ -1848,19 +1848,14 @@ void tensor_acc(Ctx &c, PolyArr R, const u64 *A, u64 a_sk, PolyArr ACC, int B, i
 // accumulators, so a wave has BG rotated-input loads in flight per diagonal and the diagonals are re-read
 // B / BG times (from L2) instead of B times.  Products are reduced as SEAL reduces them; sums are exact
 // (FP64: |sum| < 12 x 0.53 q; 60-bit primes: 128-bit sums of < 2^120 products) and canonicalised once.
-// 1-D grid, XCD-aware (round 3): the batch groups of one coefficient block get consecutive ids on one XCD
-// (w = ((x / 8) nbg + bg) 8 + x % 8), so they run together and read that block's diagonal words from the XCD's L2
-// instead of from HBM once per batch group (PMC: 7.78 GB per launch against 6.58 GB algorithmic in round 2).
 template <bool PT, int BG>
 __global__ void __launch_bounds__(256)
     k_tensor_multi2(TensorBatch tb, u64 r_sb, u64 r_sk, u64 a_sk, PolyArr ACC, int B, int logN, u64 total, int assign,
                     const DevPrime *__restrict__ primes)
 {
-    const int nbg = (B + BG - 1) / BG;
-    const int w = blockIdx.x, g8 = w & 7, rest = w >> 3, bg = rest % nbg, x = (rest / nbg) * 8 + g8;
-    const u64 idx = (u64)x * 256 + threadIdx.x;
+    const u64 idx = (u64)blockIdx.x * 256 + threadIdx.x;
     if (idx >= total) return;
-    const int b0 = bg * BG;
+    const int b0 = blockIdx.y * BG;
     const int nb = min(BG, B - b0);
     const DevPrime pr = primes[idx >> logN];
     u64 d0[BG], d1[BG], d2[BG];
@@ -1935,7 +1930,7 @@ void tensor_multi(Ctx &c, const TensorBatch &tb, u64 r_sb, u64 r_sk, u64 a_sk, P
     const u64 total = (u64)l * c.N;
     const unsigned grid = (unsigned)((total + 255) / 256);
     constexpr int BG = 4;
-    const dim3 g2((grid + 7) / 8 * 8 * ((B + BG - 1) / BG));  // x padded to a multiple of 8, times the batch groups
+    const dim3 g2(grid, (unsigned)((B + BG - 1) / BG));
     if (plain)
         k_tensor_multi2<true, BG><<<g2, 256, 0, c.stream>>>(tb, r_sb, r_sk, a_sk, ACC, B, c.logN, total, assign ? 1 : 0,
                                                            c.primes);
