@@ -1539,26 +1539,15 @@ __device__ __forceinline__ void bmac_body(u64 *lds, u64 *ltw, PolyArr T, const u
         u64 v[EPT];
         if (ntt) {
             static_assert(LOGP >= 5 && LOGP <= 8, "pass-B sizes 2^5 .. 2^8");
-            if constexpr (EPT == 4) {  // rounds of 2 stages
-                ntt_round_g<LOGP, 0, 2, EPT, false, FP, false>(lds, addr, ts, twg, pr, nullptr);
-                __syncthreads();
-                ntt_round_g<LOGP, 2, 4, EPT, false, FP, false>(lds, addr, ts, twg, pr, nullptr);
-                __syncthreads();
-                if constexpr (LOGP <= 6) {
-                    ntt_round_g<LOGP, 4, LOGP, EPT, false, FP, true>(lds, addr, ts, twg, pr, v);
-                } else {
-                    ntt_round_g<LOGP, 4, 6, EPT, false, FP, false>(lds, addr, ts, twg, pr, nullptr);
-                    __syncthreads();
-                    ntt_round_g<LOGP, 6, LOGP, EPT, false, FP, true>(lds, addr, ts, twg, pr, v);
-                }
-            } else if constexpr (LOGP <= 6) {
-                ntt_round_g<LOGP, 0, 3, EPT, false, FP, false>(lds, addr, ts, twg, pr, nullptr);
-                __syncthreads();
-                ntt_round_g<LOGP, 3, LOGP, EPT, false, FP, true>(lds, addr, ts, twg, pr, v);
+            static_assert(EPT == 4, "rounds of 2 stages");
+            ntt_round_g<LOGP, 0, 2, EPT, false, FP, false>(lds, addr, ts, twg, pr, nullptr);
+            __syncthreads();
+            ntt_round_g<LOGP, 2, 4, EPT, false, FP, false>(lds, addr, ts, twg, pr, nullptr);
+            __syncthreads();
+            if constexpr (LOGP <= 6) {
+                ntt_round_g<LOGP, 4, LOGP, EPT, false, FP, true>(lds, addr, ts, twg, pr, v);
             } else {
-                ntt_round_g<LOGP, 0, 3, EPT, false, FP, false>(lds, addr, ts, twg, pr, nullptr);
-                __syncthreads();
-                ntt_round_g<LOGP, 3, 6, EPT, false, FP, false>(lds, addr, ts, twg, pr, nullptr);
+                ntt_round_g<LOGP, 4, 6, EPT, false, FP, false>(lds, addr, ts, twg, pr, nullptr);
                 __syncthreads();
                 ntt_round_g<LOGP, 6, LOGP, EPT, false, FP, true>(lds, addr, ts, twg, pr, v);
             }
@@ -1622,7 +1611,9 @@ __global__ void __launch_bounds__(NSEG *(1 << LOGP) / EPT)
         bmac_body<LOGP, NSEG, EPT, true>(lds, ltw, T, E, key, ACC, tt, pr, I, kI, b, xb, logN, l, K, elt);
 }
 
-template <int LOGR, int LOGC, int NA, int NB2, int EPT = 8>
+// k_bmac: EPT = 4 elements per thread (rounds of 2 stages, 118 VGPRs, 4 waves/SIMD); 8 per thread (3-stage rounds,
+// 200 VGPRs, 2 waves/SIMD) measured 1,062 vs 951 ms per step at cfg3 (round 3, gpurun_out/r03s)
+template <int LOGR, int LOGC, int NA, int NB2, int EPT = 4>
 static void run_modup_fused(Ctx &c, const u64 *D, u64 *E, PolyArr T, const u64 *key, u64 *ACC, int B, int l,
                             int part, u32 elt)
 {
@@ -1661,11 +1652,7 @@ void ks_modup_mac(Ctx &c, const u64 *D, u64 *E, PolyArr T, const u64 *key, u64 *
     case 12: run_modup_fused<6, 6, 64, 8>(c, D, E, T, key, ACC, B, l, part, elt); break;
     case 13: run_modup_fused<7, 6, 32, 8>(c, D, E, T, key, ACC, B, l, part, elt); break;
     case 14: run_modup_fused<7, 7, 32, 4>(c, D, E, T, key, ACC, B, l, part, elt); break;
-    case 15:
-        if (c.bmac_ept == 4) run_modup_fused<8, 7, 16, 4, 4>(c, D, E, T, key, ACC, B, l, part, elt);  // experiment
-        else if (c.bmac_ept == 2) run_modup_fused<8, 7, 16, 2, 4>(c, D, E, T, key, ACC, B, l, part, elt);
-        else run_modup_fused<8, 7, 16, 4>(c, D, E, T, key, ACC, B, l, part, elt);
-        break;
+    case 15: run_modup_fused<8, 7, 16, 4>(c, D, E, T, key, ACC, B, l, part, elt); break;
     case 16: run_modup_fused<8, 8, 16, 4>(c, D, E, T, key, ACC, B, l, part, elt); break;
     default: throw std::invalid_argument("poly_modulus_degree must be 2^10 .. 2^16");
     }
