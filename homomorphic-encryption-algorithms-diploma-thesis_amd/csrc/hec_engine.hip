@@ -1256,7 +1256,6 @@ int hec_context_create(uint64_t N, const uint64_t *mod, uint64_t K, int device, 
         if (const char *f = std::getenv("HEC_LANES")) c.lanes = std::max(1, std::atoi(f));
         if (const char *f = std::getenv("HEC_HOIST")) c.hoist = f[0] != '0';
         if (const char *f = std::getenv("HEC_HMAC")) c.hmac_cfg = std::atoi(f);
-        if (const char *f = std::getenv("HEC_NTTB_EPT")) c.nttb_ept = std::atoi(f);
         if (const char *f = std::getenv("HEC_HMAC_ODD3")) c.hmac_odd3 = std::atoi(f);
         if (const char *f = std::getenv("HEC_HOIST_MIN")) c.hoist_min_children = std::max(1, std::atoi(f));
         if (const char *f = std::getenv("HEC_TENSOR_DEFER")) c.tensor_defer_max = std::max(1, std::atoi(f));

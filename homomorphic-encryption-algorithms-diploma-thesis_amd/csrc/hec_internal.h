@@ -88,7 +88,6 @@ struct Ctx {
     int tensor_defer_bufs = 8;     // HEC_TENSOR_BUFS: rotation buffers per trie depth
     bool hoist = true;             // HEC_HOIST=0: no hoisted mod-up in the rotation trie walk
     int hoist_min_children = 2;    // HEC_HOIST_MIN: children a trie node needs to be hoisted
-    int nttb_ept = 16;             // experiment: HEC_NTTB_EPT=8, forward pass B with 8 elements per thread
     int hmac_cfg = 1;              // HEC_HMAC=0: one hoisted MAC per child (1: sibling pairs fused, k_hmacm)
     int hoist_scan = 1;            // HEC_HOIST_SCAN=0: hoisted node as INTT pass B, pass A, k_zscan, direct fan-out
                                    // (1: INTT pass B, then the fan-out finishes the INTT and lists the zeros)

@@ -335,14 +335,11 @@ __device__ __forceinline__ void ntt_round(u64 *lds, const AddrF &addr, int ts, c
     ntt_round_g<LOGP, S0, S1, 16, INV, FP, false>(lds, addr, ts, twg, pr, nullptr);
 }
 
-// EPT elements per thread: 16 (rounds of 4 stages) or 8 (rounds of 3: twice the threads and half the registers
-// per block, for the register-heavy post-ops)
-template <int LOGP, int NSEG, bool INV, bool PASS_A, bool FINAL, bool FP, class Bound, int EPT = 16>
+template <int LOGP, int NSEG, bool INV, bool PASS_A, bool FINAL, bool FP, class Bound>
 __device__ __forceinline__ void ntt_pass_body(u64 *lds, const Bound &bio, const DevPrime &pr, const TwTables &tt,
                                               int logN)
 {
-    static_assert(EPT == 16 || EPT == 8, "16 or 8 elements per thread");
-    constexpr int P = 1 << LOGP, TPS = P / EPT, THREADS = NSEG * TPS;
+    constexpr int P = 1 << LOGP, TPS = P / 16, THREADS = NSEG * TPS;
     constexpr int LD = PASS_A ? (NSEG + 1) : (P + 1);
     constexpr bool FIRST = !FINAL;  // forward: A then B; inverse: B then A
     (void)TPS;
@@ -390,19 +387,7 @@ __device__ __forceinline__ void ntt_pass_body(u64 *lds, const Bound &bio, const 
         if constexpr (PASS_A) return (1ull << s) + (u64)i;
         else return R * ((1ull << s) - 1) + (u64)i * R + chunk;
     };
-    if constexpr (EPT == 8) {  // forward only (the pass-B post-op launches)
-        static_assert(!INV, "EPT 8: forward passes");
-        const GlobalTw<decltype(twidx)> twg{twidx, tw, twf};
-        ntt_round_g<LOGP, 0, 3, 8, false, FP, false>(lds, addr, ts, twg, pr, nullptr);
-        __syncthreads();
-        if constexpr (LOGP <= 6) {
-            ntt_round_g<LOGP, 3, LOGP, 8, false, FP, false>(lds, addr, ts, twg, pr, nullptr);
-        } else {
-            ntt_round_g<LOGP, 3, 6, 8, false, FP, false>(lds, addr, ts, twg, pr, nullptr);
-            __syncthreads();
-            ntt_round_g<LOGP, 6, LOGP, 8, false, FP, false>(lds, addr, ts, twg, pr, nullptr);
-        }
-    } else if constexpr (!INV) {
+    if constexpr (!INV) {
         ntt_round<LOGP, 0, false, FP>(lds, addr, ts, twidx, tw, twf, pr);
         __syncthreads();
         ntt_round<LOGP, 1, false, FP>(lds, addr, ts, twidx, tw, twf, pr);
@@ -580,8 +565,8 @@ __device__ __forceinline__ void ntt_pass_body_rd(u64 *lds, const Bound &bio, con
 
 // A per-block branch on the prime's arithmetic class.  RD: the register-direct pass (ntt_pass_body_rd); otherwise
 // every round through LDS (ntt_pass_body: the forward pass B, where register-direct measured slower)
-template <int LOGP, int NSEG, bool INV, bool PASS_A, bool FINAL, class IO, bool RD = false, int EPT = 16>
-__global__ void __launch_bounds__(NSEG *(1 << LOGP) / EPT)
+template <int LOGP, int NSEG, bool INV, bool PASS_A, bool FINAL, class IO, bool RD = false>
+__global__ void __launch_bounds__(NSEG *(1 << LOGP) / 16)
     k_ntt(const IO io, TwTables tt, const DevPrime *__restrict__ primes, int logN)
 {
     static_assert(LOGP >= 5 && LOGP <= 8, "two rounds of 4 stages");
@@ -594,8 +579,8 @@ __global__ void __launch_bounds__(NSEG *(1 << LOGP) / EPT)
     if constexpr (RD) {
         if (pr.fp) ntt_pass_body_rd<LOGP, NSEG, INV, PASS_A, FINAL, true>(lds, bio, pr, tt, logN);
         else ntt_pass_body_rd<LOGP, NSEG, INV, PASS_A, FINAL, false>(lds, bio, pr, tt, logN);
-    } else if (pr.fp) ntt_pass_body<LOGP, NSEG, INV, PASS_A, FINAL, true, typename IO::Bound, EPT>(lds, bio, pr, tt, logN);
-    else ntt_pass_body<LOGP, NSEG, INV, PASS_A, FINAL, false, typename IO::Bound, EPT>(lds, bio, pr, tt, logN);
+    } else if (pr.fp) ntt_pass_body<LOGP, NSEG, INV, PASS_A, FINAL, true>(lds, bio, pr, tt, logN);
+    else ntt_pass_body<LOGP, NSEG, INV, PASS_A, FINAL, false>(lds, bio, pr, tt, logN);
 }
 
 template <int LOGR, int LOGC, int NA, int NB, bool INV, class IO1, class IO2>
@@ -610,12 +595,7 @@ static void run_ntt2(Ctx &c, int njobs, const IO1 &first, const IO2 &second, int
                            // SQ counters: a third fewer LDS and VMEM instructions, no bank conflicts either way,
                            // but 2.2x the cycles waiting on load dependencies and 15 % more wave cycles)
         if (stages & 1) k_ntt<LOGR, NA, false, true, false, IO1, true><<<gA, TA, 0, c.stream>>>(first, fwd, c.primes, c.logN);
-        if (stages & 2) {
-            if (c.nttb_ept == 8)  // experiment
-                k_ntt<LOGC, NB, false, false, true, IO2, false, 8><<<gB, NB * C / 8, 0, c.stream>>>(second, fwd, c.primes, c.logN);
-            else
-                k_ntt<LOGC, NB, false, false, true><<<gB, TB, 0, c.stream>>>(second, fwd, c.primes, c.logN);
-        }
+        if (stages & 2) k_ntt<LOGC, NB, false, false, true><<<gB, TB, 0, c.stream>>>(second, fwd, c.primes, c.logN);
     } else {
         if (stages & 1) k_ntt<LOGC, NB, true, false, false, IO1, true><<<gB, TB, 0, c.stream>>>(first, inv, c.primes, c.logN);
         if (stages & 2) k_ntt<LOGR, NA, true, true, true, IO2, true><<<gA, TA, 0, c.stream>>>(second, inv, c.primes, c.logN);
