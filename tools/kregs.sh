@@ -2,7 +2,7 @@
 # VGPR / spill / LDS per kernel of the built engine object (development tool)
 # usage: bash tools/kregs.sh [regex]
 set -e
-O=$(dirname $0)/../homomorphic-encryption-algorithms-diploma-thesis_amd/build/hec_kernels.o
+O=${KO:-$(dirname $0)/../homomorphic-encryption-algorithms-diploma-thesis_amd/build/hec_kernels.o}
 T=$(mktemp -d)
 /opt/rocm/lib/llvm/bin/llvm-objcopy --dump-section=.hip_fatbin=$T/fat.bin $O
 /opt/rocm/lib/llvm/bin/clang-offload-bundler --unbundle --type=o --input=$T/fat.bin --targets=hipv4-amdgcn-amd-amdhsa--gfx950 --output=$T/k.co

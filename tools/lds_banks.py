@@ -138,3 +138,91 @@ if __name__ == "__main__":
                 best.append((score_bmac(LD, f, lo), LD, name, pn))
     best.sort()
     print(best[:10])
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# Round 3 (EPT = 4, rounds of 2 stages, segment-major lanes: lane = consecutive ts of one chunk): the XOR swizzle of
+# a chunk row, word = x ^ f(x), f linear in the bits from SH up, touching bits 1..4 (element pairs stay 16-B pairs).
+# The staging stores and the final round's reads are 16-B accesses (ds_write_b128 / ds_read_b128).
+
+G128 = [[*range(0, 4), *range(12, 16), *range(20, 28)], [*range(4, 12), *range(16, 20), *range(28, 32)],
+        [*range(32, 36), *range(44, 48), *range(52, 60)], [*range(36, 44), *range(48, 52), *range(60, 64)]]
+
+
+def extra_cycles_b128(words, write=False):
+    """16-B accesses: words[lane] = first u64 word of the lane's pair"""
+    groups = [list(range(g * 8, g * 8 + 8)) for g in range(8)] if write else G128
+    nb = 32 if write else 64
+    tot = 0
+    for g in groups:
+        banks = defaultdict(set)
+        for ln in g:
+            w = words[ln]
+            for d in range(4 * (w // 2), 4 * (w // 2) + 4):
+                banks[d % nb].add(d)
+        tot += max(len(v) for v in banks.values()) - 1
+    return tot
+
+
+def bmac4_rounds(logp):
+    return [(0, 2), (2, 4), (4, logp)] if logp <= 6 else [(0, 2), (2, 4), (4, 6), (6, logp)]
+
+
+def bmac4_cost(logp, swz, nseg=4):
+    """extra LDS cycles per instruction: rounds' ds_read_b64 / ds_write_b64 (final round: 16-B reads), staging
+    ds_write_b128.  swz(x) -> word within the chunk row (rows P words apart)."""
+    P = 1 << logp
+    T, tpc = nseg * P // 4, P // 4
+    tot = n = 0
+    for w in range(T // 64):
+        lane_of = lambda ln, w=w: ((w * 64 + ln) // tpc, (w * 64 + ln) % tpc)  # noqa: E731
+        for (s0, s1) in bmac4_rounds(logp):
+            insts = round_accesses(logp, s0, s1, 4, lane_of, lambda sg, x: sg * P + swz(x))
+            if s1 == logp:
+                for ws in insts[0::2]:
+                    tot += extra_cycles_b128(ws)
+                    n += 1
+            else:
+                for ws in insts:
+                    tot += extra_cycles(ws) + extra_cycles(ws, write=True)
+                    n += 2
+        for e in range(0, 4, 2):
+            ws = [((2 * (w * 64 + ln + (e // 2) * T)) // P) * P + swz((2 * (w * 64 + ln + (e // 2) * T)) % P)
+                  for ln in range(64)]
+            tot += extra_cycles_b128(ws, write=True)
+            n += 1
+    return tot / n
+
+
+def xor_swizzle(masks):
+    def swz(x):
+        m = 0
+        for k, mk in masks.items():
+            if (x >> k) & 1:
+                m ^= mk
+        return x ^ m
+    return swz
+
+
+def bmac_swizzle(logp, sh):
+    """Search the masks (even, < 32) of the bits sh .. logp-1 for the lowest bmac4_cost; the chosen sets are in
+    hec_kernels.hip (BSwz): P = 128: {3: 6, 4: 2, 5: 10, 6: 20} -> 0.0; P = 256: {4: 8, 5: 4, 6: 26, 7: 0}."""
+    import itertools
+    bits = list(range(sh, logp))
+    best = None
+    for combo in itertools.product(range(0, 32, 2), repeat=len(bits)):
+        masks = dict(zip(bits, combo))
+        if any(m >> k for k, m in masks.items()):  # a mask may only touch bits below its source bit
+            continue
+        c = bmac4_cost(logp, xor_swizzle(masks))
+        if best is None or c < best[0]:
+            best = (c, masks)
+    return best
+
+
+if __name__ == "__main__":
+    for logp, masks in ((7, {3: 6, 4: 2, 5: 10, 6: 20}), (8, {4: 8, 5: 4, 6: 26, 7: 0})):
+        P = 1 << logp
+        pad = bmac4_cost(logp, lambda x: x + (x >> 4))  # the round-3 padded rows (P + P/8 words, pad 1 per 16)
+        print(f"P={P}: padded rows {pad:.2f}, swizzle {masks} {bmac4_cost(logp, xor_swizzle(masks)):.2f} "
+              f"extra LDS cycles per instruction")
