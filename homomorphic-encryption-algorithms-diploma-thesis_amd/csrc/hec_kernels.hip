@@ -1442,8 +1442,95 @@ void fan_divide_round(Ctx &c, const u64 *Y, u64 ysb, u64 ysk, u64 *Z, int B, int
 // Grid (R / NSEG, l + 1, B): blocks of one (chunk block, I) for different b are R/NSEG * (l+1) apart,
 // a multiple of 8 for logN >= 14, so they run on one XCD and share its L2 copy of the key chunk.
 // The integer target primes come first in Imap: their blocks are the slowest, so they start first.
-// k_bmac LDS segment stride (words): P data words + P/8 (one pad word per 16 elements, and spare)
-constexpr int bmac_ld(int logp) { return (1 << logp) + (1 << logp) / 8; }
+// k_bmac chunk rows at P = 2^7 / 2^8 (the cfg3 / cfg5 sizes): an XOR swizzle instead of padding.  Element x of
+// a chunk lives at word x ^ f(x), f linear over GF(2) in the four bits from SH up and touching bits 1..4 only, so
+// an element pair (2w, 2w + 1) stays one 16-B aligned pair and swz(xb | y) = swz(xb) ^ swz(y) for disjoint bits.
+// The masks M[j] (for bit SH + j) come from the bank model (tools/lds_banks.py, bmac_swizzle): at P = 128 every
+// round's ds_read_b64 / ds_write_b64, the 16-B staging stores and the 16-B final-round reads are conflict-free
+// (the padded layout: 4-way reads in the second round, 2-way elsewhere); at P = 256 one round's reads are 2-way.
+template <int LOGP>
+struct BSwz {
+    static constexpr bool on = false;
+    static constexpr int SH = 0;
+    static constexpr int M[4] = {0, 0, 0, 0};
+};
+template <>
+struct BSwz<7> {
+    static constexpr bool on = true;
+    static constexpr int SH = 3;
+    static constexpr int M[4] = {6, 2, 10, 20};
+};
+template <>
+struct BSwz<8> {
+    static constexpr bool on = true;
+    static constexpr int SH = 4;
+    static constexpr int M[4] = {8, 4, 26, 0};
+};
+template <int LOGP>
+__host__ __device__ constexpr int bswz_c(int x)  // compile-time form
+{
+    int f = 0;
+    for (int j = 0; j < 4; ++j)
+        if ((x >> (BSwz<LOGP>::SH + j)) & 1) f ^= BSwz<LOGP>::M[j];
+    return x ^ f;
+}
+template <int LOGP>
+__host__ __device__ constexpr u64 bswz_lut()  // f(x) >> 1 for the 16 values of bits SH .. SH + 3, 4 bits each
+{
+    u64 t = 0;
+    for (int i = 0; i < 16; ++i) t |= (u64)(bswz_c<LOGP>(i << BSwz<LOGP>::SH) ^ (i << BSwz<LOGP>::SH)) >> 1 << (4 * i);
+    return t;
+}
+template <int LOGP>
+__device__ __forceinline__ int bswz(int x)
+{
+    constexpr u64 L = bswz_lut<LOGP>();
+    return x ^ (int)(((L >> (4 * ((x >> BSwz<LOGP>::SH) & 15))) & 15) << 1);
+}
+// k_bmac LDS segment stride (words): swizzled rows are P words; otherwise P data words + P/8 (one pad word per 16
+// elements, and spare)
+constexpr int bmac_ld(int logp)
+{
+    return (logp == 7 || logp == 8) ? (1 << logp) : (1 << logp) + (1 << logp) / 8;
+}
+
+// ntt_round_g on one swizzled chunk row: the group's base word swz(xb) once, its elements by XOR with constants;
+// a final round that keeps its results in registers reads element pairs as 16-B words
+template <int LOGP, int S0, int S1, int EPT, bool INV, bool FP, bool TO_REG, class TwG>
+__device__ __forceinline__ void ntt_round_x(u64 *row, int ts, const TwG &twg, const DevPrime &pr, u64 *regs)
+{
+    constexpr int LE = EPT == 16 ? 4 : EPT == 8 ? 3 : EPT == 4 ? 2 : 1;
+    constexpr int D = S1 - S0, G = 1 << (LE - D), NQ = 1 << D;
+    static_assert(D >= 1 && D <= LE, "round covers 1..log2(EPT) stages");
+    constexpr bool PAIRS = TO_REG && S1 == LOGP;
+#pragma unroll
+    for (int gi = 0; gi < G; ++gi) {
+        const int g = ts * G + gi;
+        const int lo = g & ((1 << (LOGP - S1)) - 1);
+        const int hi = g >> (LOGP - S1);
+        const int xb = bswz<LOGP>((hi << (LOGP - S0)) | lo);
+        GroupTw<S0, D, FP> gt;
+        gt.load(hi, twg);
+        u64 v[NQ];
+        if constexpr (PAIRS) {
+#pragma unroll
+            for (int a = 0; a < NQ; a += 2) {
+                const ulonglong2 w = *(const ulonglong2 *)(row + (xb ^ bswz_c<LOGP>(a)));
+                v[a] = w.x;
+                v[a + 1] = w.y;
+            }
+        } else {
+#pragma unroll
+            for (int a = 0; a < NQ; ++a) v[a] = row[xb ^ bswz_c<LOGP>(a << (LOGP - S1))];
+        }
+        gt.template run<INV>(v, pr);
+#pragma unroll
+        for (int a = 0; a < NQ; ++a) {
+            if constexpr (TO_REG) regs[gi * NQ + a] = v[a];
+            else row[xb ^ bswz_c<LOGP>(a << (LOGP - S1))] = v[a];
+        }
+    }
+}
 
 template <int LOGP, int NSEG, int EPT, bool FP>
 __device__ __forceinline__ void bmac_body(u64 *lds, u64 *ltw, PolyArr T, const u64 *__restrict__ E, const u64 *__restrict__ key,
@@ -1520,17 +1607,27 @@ __device__ __forceinline__ void bmac_body(u64 *lds, u64 *ltw, PolyArr T, const u
             nx[2 * e + 1] = w.y;
         }
     };
+    constexpr bool SWZ = BSwz<LOGP>::on;
+    u64 *const row = lds + sg * LD;
     load_tile(0);
     for (int J = 0; J < l; ++J) {
         const bool ntt = J != I;
 #pragma unroll
-        for (int e = 0; e < EPT; ++e) {
-            const int li = 2 * (threadIdx.x + (e / 2) * THREADS) + (e & 1);
-            u64 v = nx[e];
+        for (int e = 0; e < EPT; e += 2) {
+            const int li = 2 * (threadIdx.x + (e / 2) * THREADS);
+            u64 v0 = nx[e], v1 = nx[e + 1];
             if constexpr (FP) {
-                if (!ntt) v = (u64)__double_as_longlong(u2d(v));  // canonical integer target
+                if (!ntt) {  // canonical integer target
+                    v0 = (u64)__double_as_longlong(u2d(v0));
+                    v1 = (u64)__double_as_longlong(u2d(v1));
+                }
             }
-            lds[(li / P) * LD + (li % P) + ((li % P) >> 4)] = v;
+            if constexpr (SWZ) {
+                *(ulonglong2 *)(lds + (li / P) * LD + bswz<LOGP>(li % P)) = ulonglong2{v0, v1};
+            } else {
+                lds[(li / P) * LD + (li % P) + ((li % P) >> 4)] = v0;
+                lds[(li / P) * LD + (li % P) + 1 + (((li % P) + 1) >> 4)] = v1;
+            }
         }
         if (J + 1 < l) load_tile(J + 1);
         u64 k0[EPT], k1[EPT];
@@ -1540,16 +1637,28 @@ __device__ __forceinline__ void bmac_body(u64 *lds, u64 *ltw, PolyArr T, const u
         if (ntt) {
             static_assert(LOGP >= 5 && LOGP <= 8, "pass-B sizes 2^5 .. 2^8");
             static_assert(EPT == 4, "rounds of 2 stages");
-            ntt_round_g<LOGP, 0, 2, EPT, false, FP, false>(lds, addr, ts, twg, pr, nullptr);
-            __syncthreads();
-            ntt_round_g<LOGP, 2, 4, EPT, false, FP, false>(lds, addr, ts, twg, pr, nullptr);
-            __syncthreads();
-            if constexpr (LOGP <= 6) {
-                ntt_round_g<LOGP, 4, LOGP, EPT, false, FP, true>(lds, addr, ts, twg, pr, v);
-            } else {
-                ntt_round_g<LOGP, 4, 6, EPT, false, FP, false>(lds, addr, ts, twg, pr, nullptr);
+            if constexpr (SWZ) {
+                ntt_round_x<LOGP, 0, 2, EPT, false, FP, false>(row, ts, twg, pr, nullptr);
                 __syncthreads();
-                ntt_round_g<LOGP, 6, LOGP, EPT, false, FP, true>(lds, addr, ts, twg, pr, v);
+                ntt_round_x<LOGP, 2, 4, EPT, false, FP, false>(row, ts, twg, pr, nullptr);
+                __syncthreads();
+                ntt_round_x<LOGP, 4, 6, EPT, false, FP, false>(row, ts, twg, pr, nullptr);
+                __syncthreads();
+                ntt_round_x<LOGP, 6, LOGP, EPT, false, FP, true>(row, ts, twg, pr, v);
+            } else if constexpr (LOGP <= 6) {
+                ntt_round_g<LOGP, 0, 2, EPT, false, FP, false>(lds, addr, ts, twg, pr, nullptr);
+                __syncthreads();
+                ntt_round_g<LOGP, 2, 4, EPT, false, FP, false>(lds, addr, ts, twg, pr, nullptr);
+                __syncthreads();
+                ntt_round_g<LOGP, 4, LOGP, EPT, false, FP, true>(lds, addr, ts, twg, pr, v);
+            }
+        } else if constexpr (SWZ) {
+            const int xb = bswz<LOGP>(ts * EPT);
+#pragma unroll
+            for (int e = 0; e < EPT; e += 2) {
+                const ulonglong2 w = *(const ulonglong2 *)(row + (xb ^ bswz_c<LOGP>(e)));
+                v[e] = w.x;
+                v[e + 1] = w.y;
             }
         } else {
 #pragma unroll
@@ -1592,8 +1701,8 @@ __global__ void __launch_bounds__(NSEG *(1 << LOGP) / EPT)
            const DevPrime *__restrict__ primes, const int *__restrict__ Imap, int nI, int logN, int l, int K,
            int nint, int gpad, u32 elt)
 {
-    __shared__ u64 lds[NSEG * bmac_ld(LOGP)];
-    __shared__ u64 ltw[NSEG * (2 * (1 << LOGP) + 2)];
+    __shared__ __attribute__((aligned(16))) u64 lds[NSEG * bmac_ld(LOGP)];  // 16-B pair accesses
+    __shared__ __attribute__((aligned(16))) u64 ltw[NSEG * (2 * (1 << LOGP) + 2)];  // rows of 2P + 2 words: 16-B pairs
     // 1-D grid, XCD-aware: workgroup w runs on XCD w % 8.  The B blocks of one (chunk block, I) group
     // read the same key chunk, so they get ids G8*8*B + b*8 + (G % 8): one XCD, dispatched together,
     // and the key chunk is fetched into that XCD's L2 once instead of once per b.
