@@ -1208,15 +1208,30 @@ __device__ __forceinline__ void hmacm_body(PolyArr X1, const u64 *__restrict__ E
                 if constexpr (FP) f[q][t][r] = u2d(w0);
                 else a[q][t][r] = U128{w0, 0};
             }
+    auto digit = [&](int J, int t) -> ulonglong2 {
+        const int b = b0 + t;
+        const u64 *src = J == I ? X1.p + b * X1.sb + ((u64)J << logN) : E + (((u64)((b * (l + 1) + I) * l + J)) << logN);
+        return b < B ? *(const ulonglong2 *)(src + s0) : ulonglong2{0, 0};
+    };
+    // software pipeline: digit J + 1 is loaded before digit J's products, so a wave keeps its next HBM reads in
+    // flight through its own MAC work (round 3: 1,961 vs 2,266 ms per step at cfg3)
+    ulonglong2 pf[BT];
+#pragma unroll
+    for (int t = 0; t < BT; ++t) pf[t] = digit(0, t);
+    auto keyw = [&](int J, int q, int k) -> ulonglong2 {
+        return *(const ulonglong2 *)(ch.c[q].key + (((u64)(J * 2 + k) * K + kI) << logN) + kc[q]);
+    };
+    ulonglong2 kpf[CG][2];  // and the children's key words of digit J + 1 (143 VGPRs, 3 waves/SIMD: 1,898-1,904 vs
+                            // 1,929-1,934 ms with the digits alone ahead)
+#pragma unroll
+    for (int q = 0; q < CG; ++q)
+        if (q < ch.n) kpf[q][0] = keyw(0, q, 0), kpf[q][1] = keyw(0, q, 1);
     for (int J = 0; J < l; ++J) {
         u64 ev[BT][2];
         double dv[FP ? BT : 1][2];  // FP64 class: the digits as doubles, converted once for all children
 #pragma unroll
         for (int t = 0; t < BT; ++t) {
-            const int b = b0 + t;
-            const u64 *src = J == I ? X1.p + b * X1.sb + ((u64)J << logN)
-                                    : E + (((u64)((b * (l + 1) + I) * l + J)) << logN);
-            const ulonglong2 v = b < B ? *(const ulonglong2 *)(src + s0) : ulonglong2{0, 0};
+            const ulonglong2 v = pf[t];
             ev[t][0] = v.x;
             ev[t][1] = v.y;
             if constexpr (FP) {
@@ -1224,11 +1239,15 @@ __device__ __forceinline__ void hmacm_body(PolyArr X1, const u64 *__restrict__ E
                 dv[t][1] = u2d(v.y);
             }
         }
+        if (J + 1 < l) {
+#pragma unroll
+            for (int t = 0; t < BT; ++t) pf[t] = digit(J + 1, t);
+        }
 #pragma unroll
         for (int q = 0; q < CG; ++q) {
             if (q >= ch.n) break;
-            const u64 *kp = ch.c[q].key + (((u64)(J * 2) * K + kI) << logN) + kc[q];
-            ulonglong2 k0 = *(const ulonglong2 *)kp, k1 = *(const ulonglong2 *)(kp + ((u64)K << logN));
+            ulonglong2 k0 = kpf[q][0], k1 = kpf[q][1];
+            if (J + 1 < l) kpf[q][0] = keyw(J + 1, q, 0), kpf[q][1] = keyw(J + 1, q, 1);
             if (sw[q]) {
                 k0 = ulonglong2{k0.y, k0.x};
                 k1 = ulonglong2{k1.y, k1.x};
