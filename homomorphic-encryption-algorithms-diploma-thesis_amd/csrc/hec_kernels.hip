@@ -2060,7 +2060,7 @@ void tensor_multi(Ctx &c, const TensorBatch &tb, u64 r_sb, u64 r_sk, u64 a_sk, P
 {
     const u64 total = (u64)l * c.N;
     const unsigned grid = (unsigned)((total + 255) / 256);
-    constexpr int BG = 4;
+    constexpr int BG = 2;  // batch entries per thread (round 3, r03t: 533 vs 578 ms per step for 4, 577 for 8)
     const dim3 g2(grid, (unsigned)((B + BG - 1) / BG));
     if (plain)
         k_tensor_multi2<true, BG><<<g2, 256, 0, c.stream>>>(tb, r_sb, r_sk, a_sk, ACC, B, c.logN, total, assign ? 1 : 0,
