@@ -120,6 +120,15 @@ def launcher_cmd(ngpus, argv, port):
             "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
 
 
+def bench_seeds(rank, sharded):
+    """Seeds of the synthetic inputs.  The relinearization key, the Galois keys and the matrix diagonals are the
+    state every rank replicates (one keygen shared by every diagonal, matrix_operations.cpp:1057-1068),
+    so they never depend on the rank: a sharded step sums partials that ranks computed with their own copies, and
+    rank 0's self-check recomputes them with its copy.  Only the input vectors of throughput mode are per rank
+    (each replica processes its own batch); sharded mode splits ONE batch, the same on every rank."""
+    return {"relin": 11, "galois": 1000, "diag": 10_000, "col": 90_000 + (0 if sharded else 100 * rank)}
+
+
 def cpu_baseline(N, moduli, n, sample_diags, threads):
     """The oracle (the C++ restatement of the reference's SEAL path, kind "port"), built here with
     -march=native, timed on this host:
@@ -248,10 +257,11 @@ def main():
     L = len(moduli) - 1
     ctx = hec.Context(N, moduli, device=local)
     elts = ctx.default_galois_elts()
-    rk = ctx.relin_key(seed=11 + rank)
-    gk = ctx.galois_keys(uniform_elts=elts, seed=1000 + 97 * rank)
-    scale = 2.0**40
     sharded = args.mode == "sharded"
+    seeds = bench_seeds(rank, sharded)
+    rk = ctx.relin_key(seed=seeds["relin"])
+    gk = ctx.galois_keys(uniform_elts=elts, seed=seeds["galois"])
+    scale = 2.0**40
     plan = None
     if sharded:
         import hecdna.shard as shard
@@ -268,11 +278,10 @@ def main():
         diags = ctx.encode(vals, scale, L)
         del vals
     else:
-        diags = [ctx.ciphertext().fill_uniform(2, L, scale, 10_000 + j) if j in held else None
+        diags = [ctx.ciphertext().fill_uniform(2, L, scale, seeds["diag"] + j) if j in held else None
                  for j in range(args.n)]
     # sharded: every rank sees the same input batch (same seeds); throughput: own vectors per rank
-    cseed = 90_000 + (0 if sharded else 100 * rank)
-    cols = [ctx.ciphertext().fill_uniform(2, L, scale, cseed + i) for i in range(args.batch)]
+    cols = [ctx.ciphertext().fill_uniform(2, L, scale, seeds["col"] + i) for i in range(args.batch)]
     outs = [hec.Ciphertext(ctx) for _ in range(args.batch)]
     ctx.synchronize()
 
@@ -321,7 +330,7 @@ def main():
         (every diagonal; the ones rank 0 does not hold are regenerated from their seeds).  Local, no collective."""
         mine, fin = res
         k = min(2, len(mine))
-        full = [d if d is not None else ctx.ciphertext().fill_uniform(2, L, scale, 10_000 + j)
+        full = [d if d is not None else ctx.ciphertext().fill_uniform(2, L, scale, seeds["diag"] + j)
                 for j, d in enumerate(diags)]
         ref = ctx.matmul_diag_col(full, [cols_used[i] for i in mine[:k]], rk, gk)
         ok = all(np.array_equal(a.download(), b.download()) and a.info() == b.info() for a, b in zip(fin[:k], ref))
@@ -334,7 +343,8 @@ def main():
     if not sharded and not ctpt and nsh > 0:
         import hecdna.shard as shard
         splan = shard.plan_diagonal_shards(N, args.n, world)
-        scols = cols if rank == 0 else [ctx.ciphertext().fill_uniform(2, L, scale, 90_000 + i)
+        s0 = bench_seeds(0, False)["col"]
+        scols = cols if rank == 0 else [ctx.ciphertext().fill_uniform(2, L, scale, s0 + i)
                                         for i in range(args.batch)]  # rank 0's batch on every rank
         res = shard.sharded_matvec(ctx, diags, scols, rk, gk, rank, world, plan=splan)  # warmup
         ctx.synchronize()
@@ -454,6 +464,10 @@ def main():
         print(json.dumps(line))
     if dist is not None:
         dist.destroy_process_group()
+    if sharded_extra is not None and "self_check" in sharded_extra and not sharded_extra["self_check"]["bitexact"]:
+        # a sharded step whose outputs differ from the 1-rank matvec is no valid measurement: fail the run
+        print("bench.py: sharded self-check is NOT bit-exact against the 1-rank matvec", file=sys.stderr)
+        sys.exit(1)
 
 
 if __name__ == "__main__":

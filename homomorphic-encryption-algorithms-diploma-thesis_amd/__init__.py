@@ -139,6 +139,9 @@ def lib():
             "hec_seal_kswitch_keys_save": [C.c_uint64, u64p, C.c_uint64, C.POINTER(u64p), u64p, C.c_uint64, C.c_int,
                                            vp, C.c_uint64, u64p],
             "hec_seal_kswitch_keys_foreach": [vp, C.c_uint64, KEYLIST_VISIT, vp, u64p, u64p],
+            "hec_seal_kswitch_keys_load_ex": [vp, C.c_uint64, C.c_uint64, C.c_uint64, u64p, u64p, C.c_uint64, u64p,
+                                              u64p],
+            "hec_seal_kswitch_keys_foreach_ex": [vp, C.c_uint64, C.c_uint64, KEYLIST_VISIT, vp, u64p, u64p],
             "hec_ciphertext_load_seal": [vp, vp, C.c_uint64, u64p],
             "hec_ciphertext_save_seal": [vp, C.c_int, vp, C.c_uint64, u64p],
             "hec_kswitch_key_load_seal": [vp, vp, C.c_uint64, C.POINTER(vp), u64p],
@@ -300,28 +303,33 @@ def seal_kswitch_keys_save(N, moduli, key_lists, compr=COMPR_NONE) -> bytes:
 KEYLIST_VISIT = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_uint64, u64p, C.c_uint64)
 
 
-def seal_kswitch_keys_lists(b: bytes):
-    """hec_seal_kswitch_keys_foreach: every non-empty key list in one pass -> ({index: u64 words}, list count,
-    bytes consumed)"""
+def seal_kswitch_keys_lists(b: bytes, max_bytes=0, visit_status=0):
+    """hec_seal_kswitch_keys_foreach[_ex]: every non-empty key list in one pass -> ({index: u64 words}, list count,
+    bytes consumed).  max_bytes bounds the decompressed object (0: the library's default); a non-zero visit_status
+    is what the visitor returns for the first list (the walk stops with that status)."""
     got = {}
 
     def visit(_user, index, words, nwords):
         got[int(index)] = np.ctypeslib.as_array(words, shape=(int(nwords),)).copy()
-        return 0
+        return visit_status
     cb = KEYLIST_VISIT(visit)
     lists, used = C.c_uint64(), C.c_uint64()
     src, n = _bytes_in(b)
-    _seal_check(lib().hec_seal_kswitch_keys_foreach(src, n, cb, None, C.byref(lists), C.byref(used)))
+    rc = lib().hec_seal_kswitch_keys_foreach_ex(src, n, max_bytes, cb, None, C.byref(lists), C.byref(used))
+    if rc != 0 and rc == visit_status:
+        raise HecError(rc, lib().hec_seal_last_error().decode())
+    _seal_check(rc)
     return got, lists.value, used.value
 
 
-def seal_kswitch_keys_load(b: bytes, index):
+def seal_kswitch_keys_load(b: bytes, index, max_bytes=0):
     """key list `index` as u64 words (u64[L][2][K][N] flattened), and the object's list count"""
     lists, words, used = C.c_uint64(), C.c_uint64(), C.c_uint64()
     src, n = _bytes_in(b)
-    _seal_check(lib().hec_seal_kswitch_keys_load(src, n, index, C.byref(lists), None, 0, C.byref(words), C.byref(used)))
+    _seal_check(lib().hec_seal_kswitch_keys_load_ex(src, n, index, max_bytes, C.byref(lists), None, 0, C.byref(words),
+                                                    C.byref(used)))
     out = np.zeros(words.value, dtype=np.uint64)
-    _seal_check(lib().hec_seal_kswitch_keys_load(src, n, index, None, _p(out), out.size, None, None))
+    _seal_check(lib().hec_seal_kswitch_keys_load_ex(src, n, index, max_bytes, None, _p(out), out.size, None, None))
     return out, lists.value, used.value
 
 

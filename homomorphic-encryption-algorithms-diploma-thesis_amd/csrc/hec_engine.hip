@@ -1918,6 +1918,18 @@ int hec_ciphertext_save_seal(const hec_ciphertext *ct, int compr_mode, void *out
     });
 }
 
+// Decompressed-size limit of a KSwitchKeys object loaded into this context (the bytes come from a client socket,
+// server.cpp:110-122): `lists` key lists of L PublicKeys of u64[2][K][N], the object's N list-length words, and at
+// most 256 B of SEALHeader / parms_id / ciphertext metadata per PublicKey.  GaloisKeys are accepted with up to
+// kMaxGaloisLists non-empty lists: SEAL's default set (create_galois_keys(), the reference's only form:
+// matrix_operations.cpp:771,872,1064) holds 2 log2(N) - 1; a caller with more keys loads them with
+// hec_seal_kswitch_keys_foreach_ex and an explicit limit.
+static constexpr uint64_t kMaxGaloisLists = 64;
+static uint64_t seal_keys_max_bytes(const Ctx &c, uint64_t lists)
+{
+    return lists * c.L * (2 * c.K * c.N * 8 + 256) + c.N * 8 + 4096;
+}
+
 int hec_kswitch_key_load_seal(hec_context *ctx, const void *bytes, uint64_t nbytes, hec_kswitch_key **out,
                               uint64_t *consumed)
 {
@@ -1925,10 +1937,11 @@ int hec_kswitch_key_load_seal(hec_context *ctx, const void *bytes, uint64_t nbyt
         need(ctx && bytes && out, "null argument");
         const Ctx &c = ctx->c;
         uint64_t words = 0, used = 0, lists = 0;
-        seal_rc(hec_seal_kswitch_keys_load(bytes, nbytes, 0, &lists, nullptr, 0, &words, &used));
+        const uint64_t cap = seal_keys_max_bytes(c, 1);
+        seal_rc(hec_seal_kswitch_keys_load_ex(bytes, nbytes, 0, cap, &lists, nullptr, 0, &words, &used));
         need(lists >= 1 && words == c.L * 2 * c.K * c.N, "relin_keys is not valid for encryption parameters");
         std::vector<u64> host(words);
-        seal_rc(hec_seal_kswitch_keys_load(bytes, nbytes, 0, nullptr, host.data(), words, nullptr, nullptr));
+        seal_rc(hec_seal_kswitch_keys_load_ex(bytes, nbytes, 0, cap, nullptr, host.data(), words, nullptr, nullptr));
         const int rc = hec_kswitch_key_upload(ctx, host.data(), out);
         if (rc != HEC_OK) throw std::logic_error(hec_last_error());
         if (consumed) *consumed = used;
@@ -1958,7 +1971,8 @@ int hec_galois_keys_load_seal(hec_galois_keys *gk, const void *bytes, uint64_t n
             return st->rc = rc;
         };
         uint64_t used = 0;
-        const int rc = hec_seal_kswitch_keys_foreach(bytes, nbytes, cb, &v, nullptr, &used);
+        const int rc = hec_seal_kswitch_keys_foreach_ex(bytes, nbytes, seal_keys_max_bytes(gk->ctx->c, kMaxGaloisLists),
+                                                        cb, &v, nullptr, &used);
         if (v.rc != HEC_OK) {
             if (v.rc == HEC_EINVAL) throw std::invalid_argument(v.err);
             throw std::logic_error(v.err);

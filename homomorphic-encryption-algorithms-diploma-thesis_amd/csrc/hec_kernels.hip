@@ -1556,10 +1556,13 @@ __device__ __forceinline__ void bmac_body(u64 *lds, u64 *ltw, PolyArr T, const u
                                           u64 *__restrict__ ACC, const TwTables &tt, const DevPrime &pr, int I, int kI,
                                           int b, int xb, int logN, int l, int K, u32 elt)
 {
-    // segment-major lane layout: the P / EPT threads of one chunk are consecutive lanes, rows of P + P/8 words
-    // with one pad word per 16 elements.  The staging writes and the rounds' reads and writes then take about
-    // half the LDS bank-conflict cycles of the chunk-interleaved layout (tools/lds_banks.py; -7 % kernel time)
+    // segment-major lane layout: the P / EPT threads of one chunk are consecutive lanes.  At P = 128 and 256 (the
+    // cfg3 / cfg5 sizes) a chunk row is exactly P words with the XOR swizzle of BSwz (element x at word x ^ f(x),
+    // element pairs stay 16-B aligned); at P <= 64 a row is P + P/8 words with one pad word per 16 elements.  The
+    // swizzled rows take 0.275 bank-conflict cycles per LDS instruction (tools/lds_banks.py, bmac_swizzle)
     constexpr int P = 1 << LOGP, THREADS = NSEG * P / EPT, LD = bmac_ld(LOGP), TWS = 2 * P + 2;
+    static_assert(BSwz<LOGP>::on || LOGP <= 6, "P = 128 / 256 chunk rows are swizzled: the padded rounds stop at P = 64");
+    static_assert(BSwz<LOGP>::on == (LD == P), "bmac_ld must match the row layout");
     const u64 N = 1ull << logN;
     const int seg0 = xb * NSEG;
     const u64 base = (u64)seg0 << LOGP;

@@ -369,10 +369,13 @@ const Zlib &zlib()
 
 // Decompressed member bytes are bounded: a client's bytes arrive over the socket (server.cpp:110-122), so a small
 // compressed payload must not expand without limit.  kMaxCtObject covers a ciphertext object (size <= 16 polys,
-// N <= 2^17, <= 64 limbs of u64: 1 GiB of words); kMaxKeysObject a KSwitchKeys object (GaloisKeys at N = 2^17,
-// every rotation key).
+// N <= 2^17, <= 64 limbs of u64: 1 GiB of words).  A KSwitchKeys object is bounded by its caller: the device
+// loaders know N, K and L and pass the exact size of the key lists they accept (hec_engine.hip); the context-free
+// entry points use kMaxKeysObjectDefault (4 GiB: SEAL's default GaloisKeys at N = 2^15, L = 10 take 1.67 GB), and
+// the *_ex forms take an explicit limit.  The output buffer doubles from a small start, so a rejected payload has
+// cost at most twice the limit.
 constexpr std::size_t kMaxCtObject = (std::size_t)1 << 31;
-constexpr std::size_t kMaxKeysObject = (std::size_t)1 << 40;
+constexpr std::size_t kMaxKeysObjectDefault = (std::size_t)1 << 32;
 void check_growth(std::size_t want, std::size_t max_out)
 {
     if (want > max_out) throw std::invalid_argument("decompressed SEAL object exceeds the size limit");
@@ -390,7 +393,10 @@ std::vector<u8> inflate_zlib(const u8 *src, std::size_t n, std::size_t max_out)
         int rc = Z_OK;
         while (rc == Z_OK) {
             if (s.total_out == out.size()) {
-                check_growth(s.total_out, max_out);
+                if (s.total_out > max_out) {
+                    z.inflate_end(&s);  // the stream state is released before the rejection
+                    check_growth(s.total_out, max_out);
+                }
                 out.resize(std::min(2 * out.size(), max_out + 1));
             }
             s.next_out = out.data() + s.total_out;
@@ -419,7 +425,10 @@ std::vector<u8> inflate_zstd(const u8 *src, std::size_t n, std::size_t max_out)
     std::size_t rc = 1;
     while (in.pos < in.size || rc != 0) {
         if (ob.pos == ob.size) {
-            if (ob.pos > max_out) { z.free_d(ds); check_growth(ob.pos, max_out); }
+            if (ob.pos > max_out) {
+                z.free_d(ds);
+                check_growth(ob.pos, max_out);
+            }
             out.resize(std::min(2 * out.size(), max_out + 1));
             ob.dst = out.data();
             ob.size = out.size();
@@ -441,6 +450,15 @@ std::vector<u8> inflate_zstd(const u8 *src, std::size_t n, std::size_t max_out)
 
 // One SEAL object: its header, then the members (decompressed when needed, at most max_out bytes).  Returns the
 // member bytes and advances r past the whole object.
+// Decompression budget of the object being loaded: every compressed payload nested in it (a KSwitchKeys object's
+// PublicKeys, their DynArrays) draws from it, so nested compressed members cannot multiply the caller's limit.
+thread_local std::size_t t_inflate_budget = SIZE_MAX;
+struct InflateBudget {
+    std::size_t saved;
+    explicit InflateBudget(std::size_t b) : saved(t_inflate_budget) { t_inflate_budget = b; }
+    ~InflateBudget() { t_inflate_budget = saved; }
+};
+
 std::vector<u8> open_object(Reader &r, std::size_t max_out = kMaxCtObject)
 {
     const Header h = r.get<Header>();
@@ -451,12 +469,12 @@ std::vector<u8> open_object(Reader &r, std::size_t max_out = kMaxCtObject)
     r.need(n);
     const u8 *payload = r.p;
     r.p += n;
-    switch (h.compr) {
-    case 0: return std::vector<u8>(payload, payload + n);
-    case 1: return inflate_zlib(payload, n, max_out);
-    case 2: return inflate_zstd(payload, n, max_out);
-    default: throw std::invalid_argument("unsupported compression mode");
-    }
+    if (h.compr == 0) return std::vector<u8>(payload, payload + n);
+    if (h.compr != 1 && h.compr != 2) throw std::invalid_argument("unsupported compression mode");
+    std::vector<u8> out = h.compr == 1 ? inflate_zlib(payload, n, std::min(max_out, t_inflate_budget))
+                                       : inflate_zstd(payload, n, std::min(max_out, t_inflate_budget));
+    if (t_inflate_budget != SIZE_MAX) t_inflate_budget -= out.size();
+    return out;
 }
 // wrap members into a SEAL object with the given compression
 void close_object(Writer &w, const std::vector<u8> &members, int compr)
@@ -579,12 +597,21 @@ void expand_seed(CtData &c, const u64 *q, u64 count)
     c.seeded = false;
 }
 
+// a status chosen by a caller's callback (hec_seal_kswitch_keys_foreach's visit), returned unchanged by io_guard
+struct CallerStatus : std::runtime_error {
+    int rc;
+    explicit CallerStatus(int r) : std::runtime_error("key list rejected by the caller"), rc(r) {}
+};
+
 template <class F>
 int io_guard(F &&f)
 {
     try {
         f();
         return HEC_OK;
+    } catch (const CallerStatus &e) {
+        g_io_err = e.what();
+        return e.rc;
     } catch (const std::invalid_argument &e) {
         g_io_err = e.what();
         return HEC_EINVAL;
@@ -606,13 +633,15 @@ void copy_out(const std::vector<u8> &b, void *out, uint64_t cap, uint64_t *writt
 // (KeyGenerator::create_galois_keys resizes the list array to the ring degree), so a per-list reparse would cost
 // N full parses.
 template <class F>
-void walk_kswitch_keys(const void *bytes, uint64_t nbytes, uint64_t *lists, uint64_t *consumed, F &&visit)
+void walk_kswitch_keys(const void *bytes, uint64_t nbytes, uint64_t max_bytes, uint64_t *lists, uint64_t *consumed,
+                       F &&visit)
 {
     if (!bytes) throw std::invalid_argument("invalid argument");
     Reader outer{static_cast<const u8 *>(bytes), static_cast<const u8 *>(bytes) + nbytes};
     Header h;
     std::memcpy(&h, bytes, std::min<uint64_t>(nbytes, sizeof(h)));
-    std::vector<u8> m = open_object(outer, kMaxKeysObject);
+    InflateBudget budget(max_bytes ? (std::size_t)max_bytes : kMaxKeysObjectDefault);
+    std::vector<u8> m = open_object(outer, t_inflate_budget);
     Reader r{m.data(), m.data() + m.size()};
     u64 pid[4];
     r.bytes(pid, 32);
@@ -785,12 +814,13 @@ int hec_seal_parms_save(uint64_t N, const uint64_t *coeff_modulus, uint64_t coun
 // KSwitchKeys key list `index` (RelinKeys: 0; GaloisKeys: (galois_elt - 1) / 2) as the engine's key layout
 // u64[L][2][K][N].  With index = UINT64_MAX only *lists (dim1) is reported; *words = the list's word count (0 when
 // that list is empty).
-int hec_seal_kswitch_keys_load(const void *bytes, uint64_t nbytes, uint64_t index, uint64_t *lists, uint64_t *out,
-                               uint64_t cap_words, uint64_t *words, uint64_t *consumed)
+int hec_seal_kswitch_keys_load_ex(const void *bytes, uint64_t nbytes, uint64_t index, uint64_t max_bytes,
+                                  uint64_t *lists, uint64_t *out, uint64_t cap_words, uint64_t *words,
+                                  uint64_t *consumed)
 {
     return io_guard([&] {
         std::vector<u64> got;
-        walk_kswitch_keys(bytes, nbytes, lists, consumed, [&](u64 i, const std::vector<u64> &w) {
+        walk_kswitch_keys(bytes, nbytes, max_bytes, lists, consumed, [&](u64 i, const std::vector<u64> &w) {
             if (i == index) got = w;
         });
         if (words) *words = got.size();
@@ -801,18 +831,30 @@ int hec_seal_kswitch_keys_load(const void *bytes, uint64_t nbytes, uint64_t inde
     });
 }
 
+int hec_seal_kswitch_keys_load(const void *bytes, uint64_t nbytes, uint64_t index, uint64_t *lists, uint64_t *out,
+                               uint64_t cap_words, uint64_t *words, uint64_t *consumed)
+{
+    return hec_seal_kswitch_keys_load_ex(bytes, nbytes, index, 0, lists, out, cap_words, words, consumed);
+}
+
+int hec_seal_kswitch_keys_foreach_ex(const void *bytes, uint64_t nbytes, uint64_t max_bytes,
+                                     int (*visit)(void *user, uint64_t index, const uint64_t *words, uint64_t nwords),
+                                     void *user, uint64_t *lists, uint64_t *consumed)
+{
+    return io_guard([&] {
+        if (!visit) throw std::invalid_argument("invalid argument");
+        walk_kswitch_keys(bytes, nbytes, max_bytes, lists, consumed, [&](u64 i, const std::vector<u64> &w) {
+            const int rc = visit(user, i, w.data(), w.size());
+            if (rc != HEC_OK) throw CallerStatus(rc);
+        });
+    });
+}
+
 int hec_seal_kswitch_keys_foreach(const void *bytes, uint64_t nbytes,
                                   int (*visit)(void *user, uint64_t index, const uint64_t *words, uint64_t nwords),
                                   void *user, uint64_t *lists, uint64_t *consumed)
 {
-    return io_guard([&] {
-        if (!visit) throw std::invalid_argument("invalid argument");
-        walk_kswitch_keys(bytes, nbytes, lists, consumed, [&](u64 i, const std::vector<u64> &w) {
-            const int rc = visit(user, i, w.data(), w.size());
-            if (rc == HEC_EINVAL) throw std::invalid_argument("key list rejected by the caller");
-            if (rc != HEC_OK) throw std::logic_error("key list rejected by the caller");
-        });
-    });
+    return hec_seal_kswitch_keys_foreach_ex(bytes, nbytes, 0, visit, user, lists, consumed);
 }
 
 // KSwitchKeys::save of nlists key lists; list i has digits[i] PublicKeys of u64[2][K][N] (keys[i] = u64[L][2][K][N],

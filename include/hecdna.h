@@ -208,8 +208,11 @@ int hec_matmul_diag_col_sharded(hec_context *ctx, const hec_ciphertext *const *d
  * input ("loaded SEALHeader is invalid", ...); hec_seal_last_error() holds the message.  Seeded ciphertexts
  * (encrypt_symmetric().save(), client.cpp:113-114) are expanded by hec_seal_ciphertext_load_ex and by the device
  * loader hec_ciphertext_load_seal (Ciphertext::expand_seed); hec_seal_ciphertext_load, which has no moduli,
- * rejects them (HEC_EINVAL).  Decompressed objects are bounded (2 GiB per ciphertext, 1 TiB per key object) and a
- * payload must hold the words it announces, since the bytes come from a client socket (server.cpp:110-122). */
+ * rejects them (HEC_EINVAL).  Decompressed objects are bounded, since the bytes come from a client socket
+ * (server.cpp:110-122): 2 GiB per ciphertext; a key object (with every compressed member nested in it) by the
+ * caller's max_bytes in the *_ex forms, by 4 GiB in the others, and by the size of the key lists the context
+ * accepts in the device loaders.  A payload over its limit is HEC_EINVAL ("decompressed SEAL object exceeds the
+ * size limit"); a payload must also hold the words it announces. */
 #define HEC_COMPR_NONE 0
 #define HEC_COMPR_ZLIB 1
 #define HEC_COMPR_ZSTD 2
@@ -246,12 +249,21 @@ int hec_seal_parms_save(uint64_t poly_modulus_degree, const uint64_t *coeff_modu
  * in the engine's key layout u64[L][2][K][N]; *lists = the object's list count, *words = that list's words */
 int hec_seal_kswitch_keys_load(const void *bytes, uint64_t nbytes, uint64_t index, uint64_t *lists, uint64_t *out,
                                uint64_t cap_words, uint64_t *words, uint64_t *consumed);
+/* ... with at most max_bytes decompressed (0: the 4 GiB default) */
+int hec_seal_kswitch_keys_load_ex(const void *bytes, uint64_t nbytes, uint64_t index, uint64_t max_bytes,
+                                  uint64_t *lists, uint64_t *out, uint64_t cap_words, uint64_t *words,
+                                  uint64_t *consumed);
 /* The same object in ONE pass: visit(user, index, words, nwords) is called for every non-empty key list in order
  * (GaloisKeys hold N lists, almost all empty, so a per-index hec_seal_kswitch_keys_load would reparse the object N
- * times).  A non-zero return from visit stops the walk with that status.  *lists = the object's list count. */
+ * times).  A non-zero return from visit stops the walk, and the function returns that status unchanged (with
+ * hec_seal_last_error() = "key list rejected by the caller").  *lists = the object's list count. */
 int hec_seal_kswitch_keys_foreach(const void *bytes, uint64_t nbytes,
                                   int (*visit)(void *user, uint64_t index, const uint64_t *words, uint64_t nwords),
                                   void *user, uint64_t *lists, uint64_t *consumed);
+/* ... with at most max_bytes decompressed (0: the 4 GiB default) */
+int hec_seal_kswitch_keys_foreach_ex(const void *bytes, uint64_t nbytes, uint64_t max_bytes,
+                                     int (*visit)(void *user, uint64_t index, const uint64_t *words, uint64_t nwords),
+                                     void *user, uint64_t *lists, uint64_t *consumed);
 int hec_seal_kswitch_keys_save(uint64_t poly_modulus_degree, const uint64_t *coeff_modulus, uint64_t K,
                                const uint64_t *const *keys, const uint64_t *digits, uint64_t nlists, int compr_mode,
                                void *out, uint64_t cap, uint64_t *written);

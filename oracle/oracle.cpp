@@ -555,7 +555,12 @@ Plaintext encode(const Context &ctx, const std::vector<cd> &values, double scale
     const double fix = scale / (double)N;
     seal_transform_from_rev(v.data(), __builtin_ctzll(N), inv_roots.data(), &fix);
     double max_coeff = 0;  // over the unrounded real parts, as SEAL
-    for (std::size_t k = 0; k < N; ++k) max_coeff = std::max(max_coeff, std::fabs(v[k].real()));
+    for (std::size_t k = 0; k < N; ++k) {
+        // a NaN or infinite coefficient (from a non-finite input) is rejected as too large, as the GPU encoder
+        // rejects it; SEAL's std::max would skip a NaN and then cast it to an integer (undefined behaviour)
+        if (!std::isfinite(v[k].real())) throw std::invalid_argument("encoded values are too large");
+        max_coeff = std::max(max_coeff, std::fabs(v[k].real()));
+    }
     const int max_bits = (int)std::ceil(std::log2(std::max(max_coeff, 1.0))) + 1;
     if (max_bits >= ctx.total_bits(level)) throw std::invalid_argument("encoded values are too large");
     Plaintext pt;

@@ -55,6 +55,19 @@ def test_gpus_n_launches_n_ranks_one_line(gpus):
     assert r["n_gpus"] == gpus and r["rccl_world"] == gpus and r["dry_run"] and r["steps"] == 2
 
 
+def test_replicated_seeds_do_not_depend_on_rank(bench):
+    """The keys and the matrix diagonals are the replicated state of every rank: their seeds must be the
+    same on every rank, or a sharded step sums partials computed under different keys.  Throughput mode gives each rank
+    its own input vectors; sharded mode splits one batch, the same on every rank."""
+    for sharded in (False, True):
+        s0 = bench.bench_seeds(0, sharded)
+        for r in range(1, 8):
+            s = bench.bench_seeds(r, sharded)
+            assert (s["relin"], s["galois"], s["diag"]) == (s0["relin"], s0["galois"], s0["diag"])
+            assert (s["col"] == s0["col"]) == sharded
+    assert bench.bench_seeds(3, True)["col"] == bench.bench_seeds(0, False)["col"]  # the sharded leg's batch = rank 0's
+
+
 def test_cpu_leg_sizing(bench, monkeypatch):
     monkeypatch.setattr(bench, "cgroup_cpu_quota", lambda: None)
     monkeypatch.setenv("OMP_NUM_THREADS", "1")

@@ -69,6 +69,13 @@ def test_encode_errors_follow_oracle(orc, hecdna):
     for vals, scale, level in [(np.zeros((1 << 10) + 1), 2.0**30, 3), (np.full(8, 1e30), 2.0**40, 3)]:
         with pytest.raises(orc.OracleError):
             e.o.encode(vals, scale, level)
+    for bad in (np.nan, np.inf, -np.inf):          # non-finite input: both sides raise the same error
+        v = np.zeros((1, 8))
+        v[0, 5] = bad
+        with pytest.raises(hecdna.HecError, match="encoded values are too large"):
+            e.ctx.encode(v, 2.0**40, 3)
+        with pytest.raises(orc.OracleError, match="encoded values are too large"):
+            e.o.encode(v[0], 2.0**40, 3)
 
 
 @pytest.mark.parametrize("which,n", [("env11", 9), ("env15", 4)])

@@ -149,3 +149,15 @@ def test_encode_too_large_uses_unrounded_maximum(orc):
     with pytest.raises(orc.OracleError, match="encoded values are too large"):
         o.encode(np.full(8, 2.0**40), 2.0**20, 2)
     o.encode(np.full(8, 2.0**10), 2.0**20, 2)
+
+
+@pytest.mark.parametrize("bad", [np.nan, np.inf, -np.inf, complex(0.5, np.nan)])
+def test_encode_rejects_non_finite(orc, bad):
+    """A NaN or infinite slot value is "encoded values are too large", as the GPU encoder reports it (no cast of a
+    non-finite double to an integer)."""
+    N = 1 << 10
+    o = orc.Oracle(N, orc.Oracle.create_coeff_modulus(N, [30, 20, 30]))
+    v = np.zeros(8, dtype=complex)
+    v[3] = bad
+    with pytest.raises(orc.OracleError, match="encoded values are too large"):
+        o.encode(v, 2.0**20, 2)

@@ -207,3 +207,46 @@ def test_truncated_dynarray_is_rejected_before_allocation(hecdna):
     b[8:16] = len(b).to_bytes(8, "little")
     with pytest.raises(hecdna.InvalidArgument, match="truncated"):
         hecdna.seal_ciphertext_load(bytes(b))
+
+
+@pytest.mark.parametrize("compr", ["zlib", "zstd"])
+def test_key_object_decompression_bomb_is_rejected(hecdna, compr):
+    """A small compressed KSwitchKeys payload that inflates past the caller's limit is HEC_EINVAL (the bytes come from
+    a client socket, server.cpp:110-122), with no allocation beyond about twice the limit; the same object loads
+    under a limit that holds it."""
+    lists = [np.zeros((3, 2, 4, N), dtype=np.uint64) for _ in range(8)]   # 3 MiB of zeros: ~1000:1 compressible
+    mode = hecdna.COMPR_ZLIB if compr == "zlib" else hecdna.COMPR_ZSTD
+    b = hecdna.seal_kswitch_keys_save(N, MOD, lists, compr=mode)
+    assert len(b) < 64 * 1024
+    for fn in (lambda lim: hecdna.seal_kswitch_keys_lists(b, max_bytes=lim),
+               lambda lim: hecdna.seal_kswitch_keys_load(b, 3, max_bytes=lim)):
+        with pytest.raises(hecdna.InvalidArgument, match="exceeds the size limit"):
+            fn(1 << 20)
+    got, nl, used = hecdna.seal_kswitch_keys_lists(b, max_bytes=8 << 20)
+    assert nl == 8 and used == len(b) and sorted(got) == list(range(8))
+
+
+def test_nested_compressed_members_share_the_limit(hecdna):
+    """A raw KSwitchKeys object whose PublicKeys are each zlib-compressed: every nested payload draws from the one
+    limit of the object, so many small bombs cannot multiply it."""
+    pid = sf.parms_id(N, MOD)
+    k = np.zeros((2, 4, N), dtype=np.uint64)                    # one PublicKey: 128 KiB of words at N = 2^11
+    pk = sf.obj(sf.ciphertext(k, 1.0, MOD, pid=pid), compr=1)   # zlib-compressed PublicKey wrapper
+    import struct
+    m = pid.astype(np.uint64).tobytes() + struct.pack("<QQ", 1, 16) + pk * 16   # 1 list of 16 digits: 2 MiB inflated
+    b = sf.obj(m)
+    assert len(b) < 64 * 1024
+    with pytest.raises(hecdna.InvalidArgument, match="exceeds the size limit"):
+        hecdna.seal_kswitch_keys_lists(b, max_bytes=1 << 20)
+    got, nl, _ = hecdna.seal_kswitch_keys_lists(b, max_bytes=4 << 20)
+    assert nl == 1 and got[0].size == 16 * 2 * 4 * N
+
+
+def test_foreach_returns_the_visitors_status(hecdna):
+    """hec_seal_kswitch_keys_foreach stops the walk and returns the visitor's status unchanged (hecdna.h)"""
+    lists = [np.zeros((1, 2, 4, N), dtype=np.uint64), np.ones((1, 2, 4, N), dtype=np.uint64)]
+    b = hecdna.seal_kswitch_keys_save(N, MOD, lists)
+    for status in (1, 2, 3, 7):
+        with pytest.raises(hecdna.HecError) as e:
+            hecdna.seal_kswitch_keys_lists(b, visit_status=status)
+        assert e.value.code == status and "rejected by the caller" in str(e.value)
