@@ -98,6 +98,7 @@ def lib():
             "hec_plaintext_info": [vp, u64p, C.POINTER(C.c_double)],
             "hec_encode": [vp, C.POINTER(C.c_double), C.POINTER(C.c_double), C.c_uint64, C.c_uint64, C.c_double,
                            C.c_uint64, vp],
+            "hec_encode_scalar": [vp, C.c_double, C.c_double, C.c_uint64, vp],
             "hec_matmul_diag_col_partial": [vp, vp, C.c_uint64, C.c_uint64, C.c_uint64, vp, C.c_uint64, vp, vp],
             "hec_matmul_diag_col_partial_set": [vp, vp, C.c_uint64, vp, C.c_uint64, vp, C.c_uint64, vp, vp],
             "hec_matmul_finish": [vp, vp, C.c_uint64, vp, vp],
@@ -408,6 +409,14 @@ class Context:
         _check(lib().hec_encode(self.h, re.ctypes.data_as(dp), im.ctypes.data_as(dp) if im is not None else None,
                                 v.shape[1], v.shape[0], float(scale), level, arr))
         return pts[0] if single else pts
+
+    def encode_scalar(self, value, scale, level=None):
+        """seal::CKKSEncoder::encode(double value, parms_id, scale, pt) (hec_encode_scalar): the constant plaintext
+        he::util::drop_chain_levels and he::math multiply by (he_util.h:33)"""
+        level = level or (self.K - 1)
+        pt = Plaintext(self, None, scale)
+        _check(lib().hec_encode_scalar(self.h, float(value), float(scale), level, pt.h))
+        return pt
 
     def relin_key(self, data=None, seed=None):
         return KSwitchKey(self, data, seed)

@@ -15,6 +15,12 @@
 //          encode         (the demo's plaintexts: CKKSEncoder::encode of mat1's columns, the data of
 //                          matrix_operations.cpp:1079-1087 at dim = #ciphertexts in the input, scale 2^40,
 //                          matrix_operations.cpp:1106-1108; written as size-1 entries)
+//          math:<iter>    (he::math on the he_math.h drop-in: signed_inv(c0, 1.0), inv_sqrt_twice(c0, 0.7),
+//                          sqrt(c0, 1.0), abs(c1, 1.0) with <iter> iterations, src/core/he_math.cpp:22-269)
+//          util           (he::util: drop_chain_levels(c0, 2), then reach_chain_level of {c1, c2} to c0's level,
+//                          include/he_util.h:27-77; the chain indices of every output are printed)
+//          least_squares  (src/demos/matrix_operations.cpp:915-1003 on x = c0, y = c1 of 5 data slots: the sums,
+//                          the denominator, signed_inv(denom, 0.05, 6), the numerators, a and b)
 #include <cmath>
 #include <complex>
 #include <cstdio>
@@ -27,7 +33,9 @@
 #include <vector>
 
 #include "he_linalg.h"
+#include "he_math.h"
 #include "he_operators.h"
+#include "he_util.h"
 
 using namespace he::operators;
 using namespace he::linalg;
@@ -110,7 +118,8 @@ void write_output(const char *path, const std::vector<const Ciphertext *> &cts)
 int main(int argc, char **argv)
 {
     if (argc != 4) {
-        std::cout << "usage: he_demo <batched_diag|batched_col|ops|matrix|encode|sum_elems:<dim>> <in.bin> <out.bin>\n";
+        std::cout << "usage: he_demo <batched_diag|batched_col|ops|matrix|matrix_family|encode|sum_elems:<dim>|math:<iter>|"
+                     "util|least_squares|server> <in.bin> <out.bin>\n";
         return 1;
     }
     const std::string mode = argv[1];
@@ -218,6 +227,85 @@ int main(int argc, char **argv)
             threw = std::string(e.what()).find("mismatch") != std::string::npos;
         }
         keep.push_back(threw ? cts[0] : cts[1]);
+    } else if (mode.rfind("math:", 0) == 0) {
+        const std::size_t iter = std::stoul(mode.substr(5));
+        hecdna::CKKSEncoder cencd(ctx);
+        keep.push_back(he::math::signed_inv(cencd, eval, rk, cts[0], 1.0, iter));
+        keep.push_back(he::math::inv_sqrt_twice(cencd, eval, rk, cts[0], 0.7, iter));
+        keep.push_back(he::math::sqrt(ctx, cencd, eval, rk, cts[0], 1.0, iter));
+        keep.push_back(he::math::abs(ctx, cencd, eval, rk, cts[1], 1.0, iter));
+    } else if (mode == "util") {
+        hecdna::CKKSEncoder cencd(ctx);
+        Ciphertext d0 = cts[0];
+        he::util::drop_chain_levels(ctx, cencd, eval, d0, 2);
+        Ciphertext d1 = cts[1], d2 = cts[2];
+        hecdna::Plaintext one_pt;
+        he::util::reach_chain_level(ctx, cencd, eval, one_pt, std::vector<Ciphertext *>{&d1, &d2}, d0);
+        for (const Ciphertext *c : {&d0, &d1, &d2})
+            std::cout << "chain_index " << he::util::get_chain_index(ctx, *c) << " "
+                      << he::util::get_chain_index(hecdna::EncryptionParameters(in.N, in.moduli), *c) << " "
+                      << he::util::uint64_to_hex_string(c->parms_id()[0]) << "\n";
+        keep.push_back(d0);
+        keep.push_back(d1);
+        keep.push_back(d2);
+    } else if (mode == "least_squares") {
+        // bench_he_least_squares_2d after encryption (matrix_operations.cpp:915-1003), x_ct = c0, y_ct = c1
+        hecdna::CKKSEncoder cencd(ctx);
+        const std::size_t n = 5;
+        BatchedVector x_ctv(n, cts[0]);
+        BatchedVector y_ctv(n, cts[1]);
+        Ciphertext sum_x_ct = x_ctv.sum_elems(eval, gk).get_bvec();
+        Ciphertext sum_y_ct = y_ctv.sum_elems(eval, gk).get_bvec();
+        Ciphertext sum_xx_ct = x_ctv.square(eval, rk).sum_elems(eval, gk).get_bvec();
+        Ciphertext sum_xy_ct = (eval % rk % x_ctv * y_ctv).sum_elems(eval, gk).get_bvec();
+        hecdna::Plaintext n_pt;
+        cencd.encode(n, sum_xx_ct.parms_id(), sum_xx_ct.scale(), n_pt);
+        Ciphertext n_sum_xx_ct = eval % sum_xx_ct * n_pt;
+        n_sum_xx_ct ^= eval;
+        Ciphertext sum_x_sqr_ct;
+        eval.square(sum_x_ct, sum_x_sqr_ct);
+        sum_x_sqr_ct &= eval % rk;
+        sum_x_sqr_ct ^= eval;
+        hecdna::Plaintext one_pt;
+        cencd.encode(1, sum_x_sqr_ct.parms_id(), sum_x_sqr_ct.scale(), one_pt);
+        sum_x_sqr_ct *= eval % one_pt;
+        sum_x_sqr_ct ^= eval;
+        Ciphertext denom_ct = eval % n_sum_xx_ct - sum_x_sqr_ct;
+        hecdna::Plaintext one_pt_;
+        cencd.encode(std::vector<double>{1}, denom_ct.parms_id(), denom_ct.scale(), one_pt_);
+        denom_ct *= eval % one_pt_;
+        denom_ct ^= eval;
+        Ciphertext denom_inv_ct = he::math::signed_inv(cencd, eval, rk, denom_ct, 0.05, 6);
+        Ciphertext n_sum_xy_ct = eval % sum_xy_ct * n_pt;
+        n_sum_xy_ct ^= eval;
+        Ciphertext sum_x_sum_y_ct = eval % sum_x_ct * sum_y_ct;
+        sum_x_sum_y_ct &= eval % rk;
+        sum_x_sum_y_ct ^= eval;
+        sum_x_sum_y_ct *= eval % one_pt;
+        sum_x_sum_y_ct ^= eval;
+        Ciphertext a_num_ct = eval % n_sum_xy_ct - sum_x_sum_y_ct;
+        cencd.encode(1, sum_y_ct.parms_id(), sum_y_ct.scale(), one_pt);
+        Ciphertext sum_y_sum_xx_ct = sum_y_ct;
+        sum_y_sum_xx_ct *= eval % one_pt;
+        sum_y_sum_xx_ct ^= eval;
+        sum_y_sum_xx_ct *= eval % sum_xx_ct;
+        sum_y_sum_xx_ct &= eval % rk;
+        sum_y_sum_xx_ct ^= eval;
+        Ciphertext sum_x_sum_xy_ct = sum_x_ct;
+        sum_x_sum_xy_ct *= eval % one_pt;
+        sum_x_sum_xy_ct ^= eval;
+        sum_x_sum_xy_ct *= eval % sum_xy_ct;
+        sum_x_sum_xy_ct &= eval % rk;
+        sum_x_sum_xy_ct ^= eval;
+        Ciphertext b_num_ct = eval % sum_y_sum_xx_ct - sum_x_sum_xy_ct;
+        he::util::reach_chain_level(ctx, cencd, eval, one_pt, std::vector{&a_num_ct, &b_num_ct}, denom_inv_ct);
+        Ciphertext a_ct = eval % a_num_ct * denom_inv_ct;
+        a_ct &= eval % rk;
+        a_ct ^= eval;
+        Ciphertext b_ct = eval % b_num_ct * denom_inv_ct;
+        b_ct &= eval % rk;
+        b_ct ^= eval;
+        for (Ciphertext *c : {&denom_ct, &denom_inv_ct, &a_num_ct, &b_num_ct, &a_ct, &b_ct}) keep.push_back(*c);
     } else if (mode == "matrix") {
         // Matrix::matmul on 2x2 element-wise ciphertext matrices (column-major elems)
         Matrix A(2, 2, std::vector<Ciphertext>(cts.begin(), cts.begin() + 4));

@@ -8,17 +8,21 @@
 //                                                copy = deep device copy, like SEAL)
 //   seal::RelinKeys / GaloisKeys              -> hecdna::RelinKeys / GaloisKeys
 //   seal::CoeffModulus::Create                -> hecdna::CoeffModulus::Create
-//   seal::CKKSEncoder::encode                 -> hecdna::CKKSEncoder::encode (on the GPU, hec_encode;
-//                                                SEAL's parms_id argument is the level here)
+//   seal::CKKSEncoder::encode                 -> hecdna::CKKSEncoder::encode (on the GPU, hec_encode /
+//                                                hec_encode_scalar; a parms_id or a level selects the level)
+//   seal::parms_id_type, get_context_data(...) -> hecdna::parms_id_type (BLAKE2b-256 of {scheme, N, the level's
+//      ->chain_index()                            moduli}, SEAL's parms_id), hecdna::ContextData
 //
 // Errors are rethrown with SEAL's exception types and messages (std::invalid_argument,
 // std::logic_error); HIP failures as std::runtime_error.  Objects live on the context's GPU.
 #pragma once
 
+#include <array>
 #include <complex>
 #include <cstddef>
 #include <cstdint>
 #include <ios>
+#include <map>
 #include <memory>
 #include <ostream>
 #include <stdexcept>
@@ -91,6 +95,44 @@ private:
     std::vector<std::uint64_t> q_;
 };
 
+// seal::parms_id_type: the BLAKE2b-256 hash of a level's EncryptionParameters (EncryptionParameters::compute_parms_id
+// over {scheme, N, the level's coeff_modulus, plain modulus}); the same words SEAL writes in a ciphertext's header
+using parms_id_type = std::array<std::uint64_t, 4>;
+inline parms_id_type compute_parms_id(std::size_t N, const std::uint64_t *moduli, std::size_t count)
+{
+    parms_id_type id{};
+    seal_check(hec_seal_parms_id(N, moduli, count, id.data()));
+    return id;
+}
+
+// seal::SEALContext::ContextData of one level of the modulus switching chain.  A level keeps its first
+// `coeff_modulus_size` primes; chain_index() counts the levels below it (the key level, all K primes, has the
+// largest index K - 1; the last data level, one prime, has 0), as SEAL numbers its chain.
+class ContextData {
+public:
+    ContextData(std::size_t level, std::size_t N, std::vector<std::uint64_t> moduli, parms_id_type id,
+                std::shared_ptr<const ContextData> next)
+        : level_(level), parms_(N, std::move(moduli)), id_(id), next_(std::move(next)) {}
+    std::size_t chain_index() const { return level_ - 1; }
+    const parms_id_type &parms_id() const { return id_; }
+    const EncryptionParameters &parms() const { return parms_; }
+    std::size_t coeff_modulus_size() const { return level_; }
+    int total_coeff_modulus_bit_count() const
+    {
+        int bits = 0;
+        for (std::uint64_t q : parms_.coeff_modulus()) bits += 64 - __builtin_clzll(q);
+        return bits;
+    }
+    // the next level down the chain (nullptr below the last one), as SEAL's next_context_data()
+    std::shared_ptr<const ContextData> next_context_data() const { return next_; }
+
+private:
+    std::size_t level_;
+    EncryptionParameters parms_;
+    parms_id_type id_;
+    std::shared_ptr<const ContextData> next_;
+};
+
 class Context {
 public:
     // SEALContext ctx(parms) (server.cpp:112)
@@ -102,8 +144,44 @@ public:
         check(hec_context_create(poly_modulus_degree, coeff_modulus.data(), coeff_modulus.size(), device, &c));
         h_.reset(c, [](hec_context *p) { hec_context_destroy(p); });
         moduli_ = coeff_modulus;
+        // the modulus switching chain, last level first: level l holds q_0 .. q_{l-1}; the key level all K primes
+        std::shared_ptr<const ContextData> next;
+        levels_.resize(coeff_modulus.size() + 1);
+        for (std::size_t l = 1; l <= coeff_modulus.size(); ++l) {
+            std::vector<std::uint64_t> q(coeff_modulus.begin(), coeff_modulus.begin() + (std::ptrdiff_t)l);
+            const parms_id_type id = compute_parms_id(poly_modulus_degree, q.data(), l);
+            auto cd = std::make_shared<const ContextData>(l, poly_modulus_degree, std::move(q), id,
+                                                          l == coeff_modulus.size() ? nullptr : next);
+            by_id_[id] = l;
+            levels_[l] = cd;
+            next = cd;
+        }
     }
     hec_context *get() const { return h_.get(); }
+    // SEALContext::get_context_data(parms_id): nullptr for an unknown parms_id (SEAL returns an empty pointer)
+    std::shared_ptr<const ContextData> get_context_data(const parms_id_type &id) const
+    {
+        const auto it = by_id_.find(id);
+        return it == by_id_.end() ? nullptr : levels_[it->second];
+    }
+    std::shared_ptr<const ContextData> key_context_data() const { return levels_.back(); }
+    std::shared_ptr<const ContextData> first_context_data() const { return levels_[moduli_.size() - 1]; }
+    std::shared_ptr<const ContextData> last_context_data() const { return levels_[1]; }
+    const parms_id_type &key_parms_id() const { return levels_.back()->parms_id(); }
+    const parms_id_type &first_parms_id() const { return first_context_data()->parms_id(); }
+    const parms_id_type &last_parms_id() const { return levels_[1]->parms_id(); }
+    // the level (number of primes) of a parms_id; invalid_argument for one outside this context's chain
+    std::size_t level_of(const parms_id_type &id) const
+    {
+        const auto it = by_id_.find(id);
+        if (it == by_id_.end()) throw std::invalid_argument("parms_id is not valid for encryption parameters");
+        return it->second;
+    }
+    const parms_id_type &parms_id_of(std::size_t level) const
+    {
+        if (level < 1 || level >= levels_.size()) throw std::invalid_argument("parms_id is not valid for encryption parameters");
+        return levels_[level]->parms_id();
+    }
     std::size_t poly_modulus_degree() const { return hec_context_poly_degree(h_.get()); }
     std::size_t slot_count() const { return poly_modulus_degree() / 2; }
     const std::vector<std::uint64_t> &coeff_modulus() const { return moduli_; }
@@ -138,6 +216,8 @@ public:
 private:
     std::shared_ptr<hec_context> h_;
     std::vector<std::uint64_t> moduli_;
+    std::vector<std::shared_ptr<const ContextData>> levels_;  // [level], index 0 unused
+    std::map<parms_id_type, std::size_t> by_id_;
 };
 
 class Ciphertext {
@@ -188,6 +268,14 @@ public:
     std::size_t level() const { return info().level; }
     double scale() const { return info().scale; }
     const Context &context() const { return *ctx_; }
+    // seal::Ciphertext::parms_id(): the parms_id of the ciphertext's level; coeff_modulus_size() = that level
+    parms_id_type parms_id() const
+    {
+        if (!ctx_ || !h_) return parms_id_type{};  // SEAL's parms_id_zero for an empty ciphertext
+        return ctx_->parms_id_of(level());
+    }
+    std::size_t coeff_modulus_size() const { return level(); }
+    bool is_ntt_form() const { return true; }
     // SEAL wire format: Ciphertext::load(context, in, size) (server.cpp:120-121) returns the bytes read;
     // save(stream, compr_mode) (server.cpp:140-141; SEAL's default compression is zstd)
     std::streamoff load(const Context &ctx, const seal_byte *in, std::size_t size)
@@ -261,6 +349,8 @@ public:
     }
     std::size_t level() const { std::uint64_t l = 0; check(hec_plaintext_info(h_.get(), &l, nullptr)); return l; }
     double scale() const { double s = 0; check(hec_plaintext_info(h_.get(), nullptr, &s)); return s; }
+    parms_id_type parms_id() const { return h_ && level() ? ctx_->parms_id_of(level()) : parms_id_type{}; }
+    bool is_ntt_form() const { return true; }
     // SEAL layout u64[level][N] (seal::Plaintext::data() of an NTT-form CKKS plaintext)
     std::vector<std::uint64_t> download() const
     {
@@ -300,11 +390,35 @@ public:
     }
     void encode(const std::vector<std::complex<double>> &values, double scale, Plaintext &destination) const
     {
-        std::vector<double> re(values.size()), im(values.size());
-        for (std::size_t i = 0; i < values.size(); ++i) { re[i] = values[i].real(); im[i] = values[i].imag(); }
+        encode_complex(values, top(), scale, destination);
+    }
+    // the parms_id overloads of SEAL (encode(values, parms_id, scale, destination)), including the scalar forms
+    // he_util.h:33 and he_math.cpp:32-53 call: encode(double value, parms_id, scale, destination) puts the constant
+    // round(value scale) in every coefficient (hec_encode_scalar); a complex scalar fills every slot (SEAL's
+    // encode_internal(complex, ...) does the same through the vector encoder)
+    void encode(const std::vector<double> &values, const parms_id_type &parms_id, double scale, Plaintext &destination) const
+    {
+        encode(values, ctx_->level_of(parms_id), scale, destination);
+    }
+    void encode(const std::vector<std::complex<double>> &values, const parms_id_type &parms_id, double scale,
+                Plaintext &destination) const
+    {
+        encode_complex(values, ctx_->level_of(parms_id), scale, destination);
+    }
+    void encode(double value, const parms_id_type &parms_id, double scale, Plaintext &destination) const
+    {
+        const std::size_t level = ctx_->level_of(parms_id);
         destination.bind(*ctx_);
-        hec_plaintext *p = destination.get();
-        check(hec_encode(ctx_->get(), re.data(), im.data(), values.size(), 1, scale, top(), &p));
+        check(hec_encode_scalar(ctx_->get(), value, scale, level, destination.get()));
+    }
+    void encode(double value, double scale, Plaintext &destination) const
+    {
+        encode(value, ctx_->first_parms_id(), scale, destination);
+    }
+    void encode(std::complex<double> value, const parms_id_type &parms_id, double scale, Plaintext &destination) const
+    {
+        encode_complex(std::vector<std::complex<double>>(slot_count(), value), ctx_->level_of(parms_id), scale,
+                       destination);
     }
     // every row must have the same length (at most slot_count())
     void encode_batch(const std::vector<std::vector<double>> &rows, double scale, std::vector<Plaintext> &destination) const
@@ -324,6 +438,15 @@ public:
 
 private:
     std::size_t top() const { return ctx_->coeff_modulus().size() - 1; }
+    void encode_complex(const std::vector<std::complex<double>> &values, std::size_t level, double scale,
+                        Plaintext &destination) const
+    {
+        std::vector<double> re(values.size()), im(values.size());
+        for (std::size_t i = 0; i < values.size(); ++i) { re[i] = values[i].real(); im[i] = values[i].imag(); }
+        destination.bind(*ctx_);
+        hec_plaintext *p = destination.get();
+        check(hec_encode(ctx_->get(), re.data(), im.data(), values.size(), 1, scale, level, &p));
+    }
     const Context *ctx_;
 };
 
@@ -408,6 +531,16 @@ public:
     {
         check(hec_apply_galois_inplace(c(), a.get(), elt, gk.get()));
     }
+    // Evaluator::mod_switch_to_inplace / rescale_to_inplace (encrypted, parms_id): one step at a time down the chain
+    // until the ciphertext is at parms_id; SEAL's errors for an unknown parms_id and for a higher level
+    void mod_switch_to_inplace(Ciphertext &a, const parms_id_type &parms_id) const
+    {
+        for (std::size_t n = steps_to(a, parms_id); n > 0; --n) mod_switch_to_next_inplace(a);
+    }
+    void rescale_to_inplace(Ciphertext &a, const parms_id_type &parms_id) const
+    {
+        for (std::size_t n = steps_to(a, parms_id); n > 0; --n) rescale_to_next_inplace(a);
+    }
 
     // out-of-place forms: destination = copy, then the in-place operation (SEAL's own pattern)
     void negate(const Ciphertext &a, Ciphertext &d) const { d = a; negate_inplace(d); }
@@ -430,9 +563,27 @@ public:
         d = a;
         rotate_vector_inplace(d, steps, gk);
     }
+    void mod_switch_to(const Ciphertext &a, const parms_id_type &parms_id, Ciphertext &d) const
+    {
+        d = a;
+        mod_switch_to_inplace(d, parms_id);
+    }
+    void rescale_to(const Ciphertext &a, const parms_id_type &parms_id, Ciphertext &d) const
+    {
+        d = a;
+        rescale_to_inplace(d, parms_id);
+    }
 
 private:
     hec_context *c() const { return ctx_->get(); }
+    std::size_t steps_to(const Ciphertext &a, const parms_id_type &parms_id) const
+    {
+        if (!ctx_->get_context_data(a.parms_id())) throw std::invalid_argument("encrypted is not valid for encryption parameters");
+        if (!ctx_->get_context_data(parms_id)) throw std::invalid_argument("parms_id is not valid for encryption parameters");
+        const std::size_t from = a.level(), to = ctx_->level_of(parms_id);
+        if (from < to) throw std::invalid_argument("cannot switch to higher level modulus");
+        return from - to;
+    }
     const Context *ctx_;
 };
 

@@ -1780,6 +1780,59 @@ int hec_encode(hec_context *ctx, const double *re, const double *im, uint64_t n_
     });
 }
 
+// the residue mod q of a non-negative integer-valued double a (exactly the integer a, as SEAL's 64-bit, 128-bit
+// (fmod / division by 2^64) and multi-word decompositions give it)
+static u64 exact_residue(double a, u64 q)
+{
+    if (a < 18446744073709551616.0) return (u64)a % q;
+    int e = 0;
+    const double f = std::frexp(a, &e);  // a = f 2^e, 0.5 <= f < 1, e > 64
+    u64 r = (u64)std::ldexp(f, 53) % q, pw = 2 % q;
+    for (int k = e - 53; k > 0; k >>= 1) {  // r *= 2^(e - 53) mod q
+        if (k & 1) r = (u64)((unsigned __int128)r * pw % q);
+        pw = (u64)((unsigned __int128)pw * pw % q);
+    }
+    return r;
+}
+
+int hec_encode_scalar(hec_context *ctx, double value, double scale, uint64_t level, hec_plaintext *out)
+{
+    return guard([&] {
+        need(ctx && out, "null argument");
+        Ctx &c = ctx->c;
+        set_device(ctx);
+        // SEAL 4.1 CKKSEncoder::encode_internal(double value, parms_id, scale, destination), in its order
+        if (level < 1 || level > c.L) throw std::invalid_argument("parms_id is not valid for encryption parameters");
+        need(out->ctx == ctx, "plain is not valid for encryption parameters");
+        const int total = c.total_bits(level);
+        if (scale <= 0 || (int)std::log2(scale) >= total) throw std::invalid_argument("scale out of bounds");
+        value *= scale;
+        // coeff_bit_count = int(log2 |value|) + 2; a zero value passes (SEAL's cast of -inf), a non-finite one is
+        // rejected (SEAL would cast NaN / inf to int: undefined behaviour)
+        if (!std::isfinite(value)) throw std::invalid_argument("encoded value is too large");
+        if (value != 0.0 && (int)std::log2(std::fabs(value)) + 2 >= total)
+            throw std::invalid_argument("encoded value is too large");
+        const double cd = std::round(value);
+        const bool neg = std::signbit(cd);
+        const double a = std::fabs(cd);
+        u64 words[HEC_MAXL + 1];
+        for (std::size_t j = 0; j < level; ++j) {
+            const u64 q = c.q[j], r = exact_residue(a, q);
+            words[j] = neg && r ? q - r : r;  // negate_uint_mod
+        }
+        // the constant polynomial in NTT form: every coefficient of limb j is the residue (SEAL's fill_n)
+        const std::size_t w = level * c.N;
+        if (out->cap < w) {
+            if (out->d) HEC_HIP(hipFree(out->d));
+            out->d = dalloc(w);
+            out->cap = w;
+        }
+        fill_limbs(c, out->d, (int)level, words);
+        out->level = level;
+        out->scale = scale;
+    });
+}
+
 // ------------------------------------------------------------------ keys ------------------
 static std::size_t key_words(const Ctx &c) { return c.L * 2 * c.K * c.N; }
 

@@ -185,6 +185,8 @@ void ew_dyadic(Ctx &c, const u64 *a, const u64 *b, u64 *out, int limb0, int nl, 
 void ct_multiply(Ctx &c, const u64 *a, int sa, const u64 *b, int sb, u64 *out, int nl);
 void ew_reduce(Ctx &c, u64 *p, int npoly, int nl);
 void fill_uniform(Ctx &c, u64 *p, int npoly, int nl, int limb_prime0, int special_last, u64 seed);
+// p[i][*] = words[i] for the nl limbs (a scalar plaintext in NTT form)
+void fill_limbs(Ctx &c, u64 *p, int nl, const u64 *words);
 // CKKS encode of `count` slot vectors (hec_encode.hip): re/im device [count][nv] (im may be null), work
 // device doubles [count][2N], out [count][level][N] NTT form, maxabs[count] = max |coefficient| (bits
 // of a double)

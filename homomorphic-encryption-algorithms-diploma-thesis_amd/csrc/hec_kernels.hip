@@ -2255,4 +2255,25 @@ void fill_uniform(Ctx &c, u64 *p, int npoly, int nl, int limb_prime0, int, u64 s
     HEC_HIP(hipGetLastError());
 }
 
+// every word of limb i = v.w[i] (the NTT form of a constant polynomial: CKKSEncoder::encode of a scalar)
+struct LimbWords {
+    u64 w[HEC_MAXL + 1];
+};
+__global__ void __launch_bounds__(256) k_fill_limbs(u64 *p, int logN, u64 total, LimbWords v)
+{
+    const u64 idx = (u64)blockIdx.x * 256 + threadIdx.x;
+    if (idx >= total) return;
+    p[idx] = v.w[idx >> logN];
+}
+
+void fill_limbs(Ctx &c, u64 *p, int nl, const u64 *words)
+{
+    if (nl > HEC_MAXL + 1) throw std::invalid_argument("too many limbs");
+    LimbWords v{};
+    for (int i = 0; i < nl; ++i) v.w[i] = words[i];
+    const u64 total = (u64)nl * c.N;
+    k_fill_limbs<<<(unsigned)((total + 255) / 256), 256, 0, c.stream>>>(p, c.logN, total, v);
+    HEC_HIP(hipGetLastError());
+}
+
 }  // namespace hec

@@ -100,6 +100,13 @@ int hec_plaintext_info(const hec_plaintext *pt, uint64_t *level, double *scale);
  * "encoded values are too large". */
 int hec_encode(hec_context *ctx, const double *re, const double *im, uint64_t n_values, uint64_t count, double scale,
                uint64_t level, hec_plaintext *const *out);
+/* seal::CKKSEncoder::encode(double value, parms_id, scale, destination) (SEAL 4.1 encode_internal(double, ...)), the
+ * scalar form he::util::drop_chain_levels and he::math use (include/he_util.h:33, src/core/he_math.cpp:32,40,53):
+ * round(value * scale) as an exact integer, its residue mod every prime of `level` (negated for a negative value),
+ * written to every word of that limb (the NTT form of a constant polynomial); no transform runs.  Errors as SEAL:
+ * "parms_id is not valid for encryption parameters", "scale out of bounds", "encoded value is too large" (also for a
+ * non-finite value). */
+int hec_encode_scalar(hec_context *ctx, double value, double scale, uint64_t level, hec_plaintext *out);
 
 /* ---------------------------------------------------------------- keys -------------------- */
 /* RelinKeys (KeyGenerator::create_relin_keys, matrix_operations.cpp:1061-1062): data u64[L][2][K][N] */

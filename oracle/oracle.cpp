@@ -580,6 +580,51 @@ Plaintext encode(const Context &ctx, const std::vector<cd> &values, double scale
     return pt;
 }
 
+// CKKSEncoder::encode(double value, parms_id, scale, destination): SEAL 4.1 encode_internal(double, ...) restated
+// in its own three cases (a different route to the exact residue than encode_residue's mantissa / exponent split,
+// so the GPU's scalar encoder is checked against an independent reduction):
+//   coeff_bit_count = int(log2 |value scale|) + 2 <= 64:  (u64) |round| mod q       (barrett_reduce_64)
+//                                                 <= 128: {fmod(c, 2^64), c / 2^64} mod q  (barrett_reduce_128)
+//   otherwise: base-2^64 digits by repeated fmod / division, then reduced mod q    (RNSBase::decompose)
+// negated for a negative value (negate_uint_mod), and written to every coefficient of the NTT-form limb (fill_n):
+// the NTT of a constant polynomial.  A non-finite value is rejected as too large (SEAL would cast it to int).
+Plaintext encode_scalar(const Context &ctx, double value, double scale, std::size_t level)
+{
+    if (level < 1 || level > ctx.L()) throw std::invalid_argument("parms_id is not valid for encryption parameters");
+    const int total = ctx.total_bits(level);
+    if (scale <= 0 || (int)std::log2(scale) >= total) throw std::invalid_argument("scale out of bounds");
+    value *= scale;
+    if (!std::isfinite(value)) throw std::invalid_argument("encoded value is too large");
+    const int bits = value == 0.0 ? INT32_MIN + 2 : (int)std::log2(std::fabs(value)) + 2;
+    if (bits >= total) throw std::invalid_argument("encoded value is too large");
+    const double two64 = std::pow(2.0, 64);
+    double cd = std::round(value);
+    const bool neg = std::signbit(cd);
+    cd = std::fabs(cd);
+    Plaintext pt;
+    pt.level = level;
+    pt.scale = scale;
+    pt.data.assign(level * ctx.N(), 0);
+    for (std::size_t j = 0; j < level; ++j) {
+        const u64 q = ctx.mod(j).value;
+        u64 r;
+        if (bits <= 64) {
+            r = (u64)cd % q;
+        } else if (bits <= 128) {
+            const u128 w = ((u128)(u64)(cd / two64) << 64) | (u64)std::fmod(cd, two64);
+            r = (u64)(w % q);
+        } else {
+            std::vector<u64> digits;
+            for (double t = cd; t >= 1; t /= two64) digits.push_back((u64)std::fmod(t, two64));
+            r = 0;
+            for (std::size_t k = digits.size(); k-- > 0;) r = (u64)((((u128)r << 64) | digits[k]) % q);
+        }
+        if (neg && r) r = q - r;
+        std::fill(pt.data.begin() + j * ctx.N(), pt.data.begin() + (j + 1) * ctx.N(), r);
+    }
+    return pt;
+}
+
 // little-endian multi-word unsigned helpers for CRT composition
 using Big = std::vector<u64>;
 static void big_mul_add(Big &acc, const Big &x, u64 s)  // acc += x * s

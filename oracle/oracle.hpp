@@ -193,6 +193,8 @@ KSwitchKey gen_galois_key(const Context &ctx, const SecretKey &sk, u32 elt, u64 
 // CKKS encoder (slot i <-> evaluation at zeta^(3^i mod 2N), zeta = exp(i*pi/N); SEAL CKKSEncoder)
 Plaintext encode(const Context &ctx, const std::vector<std::complex<double>> &values, double scale,
                  std::size_t level);
+// CKKSEncoder::encode(double, parms_id, scale, destination): the scalar form (no transform)
+Plaintext encode_scalar(const Context &ctx, double value, double scale, std::size_t level);
 std::vector<std::complex<double>> decode(const Context &ctx, const Plaintext &pt);
 Ciphertext encrypt_symmetric(const Context &ctx, const SecretKey &sk, const Plaintext &pt, u64 seed);
 Plaintext decrypt(const Context &ctx, const SecretKey &sk, const Ciphertext &ct);

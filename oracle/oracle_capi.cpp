@@ -135,6 +135,13 @@ int orc_encode(void *c, const double *re, const double *im, u64 n, double scale,
         std::memcpy(out, pt.data.data(), pt.data.size() * sizeof(u64));
     });
 }
+int orc_encode_scalar(void *c, double value, double scale, u64 level, u64 *out)
+{
+    return guard([&] {
+        auto pt = encode_scalar(*static_cast<Context *>(c), value, scale, level);
+        std::memcpy(out, pt.data.data(), pt.data.size() * sizeof(u64));
+    });
+}
 int orc_decode(void *c, const u64 *pt, u64 level, double scale, double *re, double *im)
 {
     return guard([&] {

@@ -193,6 +193,12 @@ class Oracle:
                                 C.c_double(scale), C.c_uint64(level), _p(out)))
         return out
 
+    def encode_scalar(self, value, scale, level):
+        """CKKSEncoder::encode(double, parms_id, scale, pt): u64[level][N], every word of limb j the residue"""
+        out = np.zeros((level, self.N), dtype=np.uint64)
+        _check(lib().orc_encode_scalar(self.h, C.c_double(value), C.c_double(scale), C.c_uint64(level), _p(out)))
+        return out
+
     def decode(self, pt, scale):
         pt = np.ascontiguousarray(pt, dtype=np.uint64)
         re = np.zeros(self.N // 2)

@@ -161,3 +161,49 @@ def test_encode_rejects_non_finite(orc, bad):
     v[3] = bad
     with pytest.raises(orc.OracleError, match="encoded values are too large"):
         o.encode(v, 2.0**20, 2)
+
+
+def _scalar_reference(value, scale, moduli, level, N):
+    """SEAL 4.1 CKKSEncoder::encode_internal(double, ...) in Python integers: round(value * scale) as the exact integer
+    the double holds, its residue per prime (negated when negative), every coefficient of the NTT-form limb."""
+    import math
+    v = value * scale
+    c = round(v) if abs(v - math.trunc(v)) != 0.5 else (math.trunc(v) + (1 if v > 0 else -1))  # std::round: half away
+    out = np.zeros((level, N), dtype=np.uint64)
+    for j in range(level):
+        out[j] = c % moduli[j]
+    return out
+
+
+@pytest.mark.parametrize("value,scale", [(1.0, 2.0**40), (-0.05**2, 2.0**40), (2 * 0.05, 2.0**30), (3.0 / 2, 2.0**40),
+                                         (0.0, 2.0**40), (-1.0, 2.0**40), (5.0, 2.0**40), (1.4142135623730951, 2.0**40),
+                                         (-3.7e9, 2.0**40), (1e20, 2.0**62), (-7.5e22, 2.0**62), (0.5, 1.0),
+                                         (-2.5, 1.0)])
+def test_encode_scalar_matches_integer_restatement(orc, value, scale):
+    """encode_scalar: the 64-bit, 128-bit and multi-word cases (|value scale| up to 2^138 at 17 primes) against Python's
+    exact integers; std::round rounds halves away from zero"""
+    N = 1 << 10
+    m = orc.Oracle.create_coeff_modulus(N, [60] + [40] * 15 + [60])
+    o = orc.Oracle(N, m)
+    L = len(m) - 1
+    for level in (L, 3, 1):
+        if abs(value * scale) >= 2.0 ** (sum(q.bit_length() for q in m[:level]) - 2):
+            continue
+        assert np.array_equal(o.encode_scalar(value, scale, level), _scalar_reference(value, scale, m, level, N))
+
+
+def test_encode_scalar_decodes_to_constant_and_errors(orc):
+    N = 1 << 10
+    m = orc.Oracle.create_coeff_modulus(N, [50, 36, 36, 50])
+    o = orc.Oracle(N, m)
+    pt = o.encode_scalar(-0.3125, 2.0**30, 3)
+    d = o.decode(pt, 2.0**30)
+    assert np.max(np.abs(d - (-0.3125))) < 2.0**-25
+    with pytest.raises(orc.OracleError, match="encoded value is too large"):
+        o.encode_scalar(2.0**100, 2.0**30, 3)
+    with pytest.raises(orc.OracleError, match="encoded value is too large"):
+        o.encode_scalar(float("nan"), 2.0**30, 3)
+    with pytest.raises(orc.OracleError, match="scale out of bounds"):
+        o.encode_scalar(1.0, 2.0**125, 3)
+    with pytest.raises(orc.OracleError, match="parms_id is not valid"):
+        o.encode_scalar(1.0, 2.0**30, 4)
