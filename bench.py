@@ -168,6 +168,89 @@ def cpu_baseline(N, moduli, n, sample_diags, threads):
     return {"full_s": full, "one_core_s": one * ks_total(N, n) / ks_sample, "ks_sample": ks_sample}
 
 
+def run_cfg2(args, hec, world, rank, local, barrier, max_over_ranks):
+    """BASELINE configs[1]: batched forward NTT + dyadic multiply + inverse NTT at N = 2^15 over the 10 data primes of
+    the cfg2-4 chain {60, 40 x 9, 60} (the primitives of math_operations.cpp:316-354's per-primitive
+    timing).  One step = forward NTT of --batch polynomials x 10 limbs in place, their dyadic product with a second
+    NTT-form batch, inverse NTT of the product.  value = limb-NTTs per second (forward + inverse); the roofline uses
+    SURVEY §8(d)'s 524,288 B (2 N 8) per limb and pass."""
+    N = 1 << 15
+    moduli = hec.create_coeff_modulus(N, [60] + [40] * 9 + [60])
+    nl, npolys = 10, args.batch
+    ctx = hec.Context(N, moduli, device=local)
+    rng = np.random.default_rng(2 + rank)
+    words = npolys * nl * N
+    bufs = [hec.DeviceBuffer(ctx, words * 8) for _ in range(3)]
+    for b in bufs[:2]:
+        host = np.stack([rng.integers(0, moduli[i], (npolys, N), dtype=np.uint64) for i in range(nl)], axis=1)
+        b.upload(host)
+        del host
+    ctx.synchronize()
+
+    def step():
+        ctx.ntt_device(bufs[0], nl, npolys)
+        ctx.dyadic_device(bufs[0], bufs[1], bufs[2], nl, npolys)
+        ctx.ntt_device(bufs[2], nl, npolys, inverse=True)
+
+    for _ in range(args.warmup):
+        step()
+    ctx.synchronize()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    ctx.synchronize()
+    barrier()
+    dt = max_over_ranks(time.perf_counter() - t0)
+    limb_ntts = 2 * nl * npolys * args.steps * world
+    kernels, roof = {}, None
+    if not args.no_profile:
+        ctx.profile(2)
+        step()
+        ctx.synchronize()
+        for cls in ctx.profile_classes():
+            if not cls.startswith("k:"):
+                continue
+            ms, _, nbytes, kl = ctx.profile_read_ex(cls)
+            kernels[cls[2:]] = {"ms": round(ms, 4), "launches": kl, "bytes_per_launch": int(nbytes / max(1, kl)),
+                                "GBps": round(nbytes / (ms * 1e-3) / 1e9, 1) if ms else None}
+        ctx.profile(0)
+        ntt = [v for k, v in kernels.items() if k.startswith("k_ntt/")]
+        ms = sum(v["ms"] for v in ntt)
+        nb = sum(v["bytes_per_launch"] * v["launches"] for v in ntt)
+        nlaunch = sum(v["launches"] for v in ntt)
+        gbs = nb / (ms * 1e-3) / 1e9
+        roof = {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None, "kernel": "k_ntt", "avg_ms": round(ms / nlaunch, 4),
+                "algorithmic_bytes_per_launch": int(nb / nlaunch), "launches_per_step": nlaunch,
+                "us_per_limb_ntt": round(ms * 1e3 / (2 * nl * npolys), 4),
+                "note": "per pass: every limb read and written once (2 N 8 = 524,288 B per limb and pass)"}
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle_py as orc
+        o = orc.Oracle(N, moduli)
+        sample = 200  # limbs per direction, about 0.5 s of scalar CPU work
+        data = [rng.integers(0, moduli[i % nl], N, dtype=np.uint64) for i in range(sample)]
+        t1 = time.perf_counter()
+        for i, a in enumerate(data):
+            o.ntt_inv(i % nl, o.ntt_fwd(i % nl, a))
+        cs = time.perf_counter() - t1
+        cpu = {"value": round(2 * sample / cs, 2), "unit": "limb-NTT/s", "cores": 1, "kind": "port",
+               "sample": f"{sample} forward + {sample} inverse limb-NTTs at N=2^15 (the oracle's Harvey NTT, SEAL's "
+                         f"ntt_negacyclic_harvey restated, one thread, via ctypes)"}
+    if rank == 0:
+        print(json.dumps({
+            "metric": "batched negacyclic NTT limb-transforms/sec (N=2^15, 10 primes), forward + dyadic + inverse",
+            "value": round(limb_ntts / dt, 1), "unit": "limb-NTT/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u64", "data": "synthetic",
+            "config": {"workload": f"cfg2: forward NTT + dyadic + inverse NTT of {npolys} polys x {nl} limbs, N=2^15, "
+                                   f"primes {{60, 40 x 9}}", "batch_per_gpu": npolys,
+                       "parallelism": f"replicas, dp{world}"},
+            "roofline": roof, "kernels_one_step": kernels, "cpu_baseline": cpu}))
+
+
 def dry_run(args, world, rank):
     """--dry-run: the launcher, the process group, the max-over-ranks timing and the rank-0 line over gloo,
     with no GPU and no engine (tests/test_bench_measurement.py runs it at world size 2 on the CPU)."""
@@ -212,8 +295,10 @@ def main():
                     help="throughput: replicas, own vectors per rank (the metric, weak scaling); sharded: one "
                          "batch split over ranks by trie subtrees of the diagonals + one RCCL reduce-scatter "
                          "(cfg4 curve, strong scaling)")
-    ap.add_argument("--config", choices=["cfg3", "cfg5"], default="cfg3",
-                    help="cfg3: the BASELINE metric (4096x4096 matvec, N=2^15, L=10); cfg5: BASELINE configs[4], "
+    ap.add_argument("--config", choices=["cfg2", "cfg3", "cfg5"], default="cfg3",
+                    help="cfg3: the BASELINE metric (4096x4096 matvec, N=2^15, L=10); cfg2: BASELINE configs[1], "
+                         "batched forward NTT + dyadic + inverse NTT over --batch polys x 10 limbs at N=2^15 "
+                         "(limb-NTTs per second; default batch 64); cfg5: BASELINE configs[4], "
                          "the 1024x1024x1024 ct x ct matmul at N=2^16, L=16, measured as output columns per second "
                          "(a step = --batch columns of the product; not the metric)")
     ap.add_argument("--sharded-steps", type=int, default=None,
@@ -226,6 +311,8 @@ def main():
         args.logn, args.n = 16, 1024
         if args.batch == ap.get_default("batch"):
             args.batch = 32
+    if args.config == "cfg2" and args.batch == ap.get_default("batch"):
+        args.batch = 64
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # one process per GPU: start the N ranks as a child launcher before anything touches a GPU, relay its
@@ -251,6 +338,24 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     hec = load_hecdna()
+
+    def barrier():
+        if dist is not None:
+            torch.cuda.synchronize(local)
+            dist.barrier()
+
+    def max_over_ranks(dt):
+        if dist is None:
+            return dt
+        t = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    if args.config == "cfg2":
+        run_cfg2(args, hec, world, rank, local, barrier, max_over_ranks)
+        if dist is not None:
+            dist.destroy_process_group()
+        return
     N = 1 << args.logn
     bits = [60] + [40] * (15 if args.config == "cfg5" else 9) + [60]
     moduli = hec.create_coeff_modulus(N, bits)
@@ -284,20 +389,6 @@ def main():
     cols = [ctx.ciphertext().fill_uniform(2, L, scale, seeds["col"] + i) for i in range(args.batch)]
     outs = [hec.Ciphertext(ctx) for _ in range(args.batch)]
     ctx.synchronize()
-
-    def barrier():
-        if dist is not None:
-            import torch
-            torch.cuda.synchronize(local)
-            dist.barrier()
-
-    def max_over_ranks(dt):
-        if dist is None:
-            return dt
-        import torch
-        t = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local}")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        return float(t.item())
 
     last_sharded = [None]
 

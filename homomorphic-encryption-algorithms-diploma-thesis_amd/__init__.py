@@ -546,6 +546,15 @@ class Context:
         _check(fn(self.h, buf.p, limb0, nl, npolys))
         return buf.download(a.shape)
 
+    def ntt_device(self, buf, nl, npolys, limb0=0, inverse=False):
+        """in place on device words u64[npolys][nl][N] (hec_ntt_forward / hec_ntt_inverse, stream ordered)"""
+        fn = lib().hec_ntt_inverse if inverse else lib().hec_ntt_forward
+        _check(fn(self.h, buf.p, limb0, nl, npolys))
+
+    def dyadic_device(self, a, b, out, nl, npolys, limb0=0):
+        """out = a (*) b on device words u64[npolys][nl][N] (hec_dyadic_multiply, stream ordered)"""
+        _check(lib().hec_dyadic_multiply(self.h, a.p, b.p, out.p, limb0, nl, npolys))
+
     def dyadic_multiply(self, a: np.ndarray, b: np.ndarray, limb0=0):
         """a, b host u64[npolys][nlimbs][N] -> (a * b) mod q_(limb0 + limb) (device round trip)."""
         a = np.ascontiguousarray(a, dtype=np.uint64)

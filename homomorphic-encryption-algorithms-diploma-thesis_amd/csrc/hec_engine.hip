@@ -2591,7 +2591,13 @@ int hec_ntt_forward(hec_context *ctx, uint64_t *d, uint64_t limb0, uint64_t nl, 
         need(d && nl >= 1 && limb0 + nl <= ctx->c.K && nl <= HEC_MAXL + 1, "invalid limb range");
         int pm[HEC_MAXL + 1];
         for (uint64_t i = 0; i < nl; ++i) pm[i] = (int)(limb0 + i);
-        ntt_strided(ctx->c, false, d, nl * ctx->c.N, d, nl * ctx->c.N, (int)nl, pm, (int)(nl * np));
+        // one scope per pass: each reads and writes every limb once (SURVEY 8(d)'s 2 N 8 B per limb-NTT)
+        {
+            ProfScope k(ctx->c, "k:k_ntt/fwd_a", 2.0 * nl * np);
+            ntt_strided(ctx->c, false, d, nl * ctx->c.N, d, nl * ctx->c.N, (int)nl, pm, (int)(nl * np), 1, 1);
+        }
+        ProfScope k(ctx->c, "k:k_ntt/fwd_b", 2.0 * nl * np);
+        ntt_strided(ctx->c, false, d, nl * ctx->c.N, d, nl * ctx->c.N, (int)nl, pm, (int)(nl * np), 1, 2);
     });
 }
 int hec_ntt_inverse(hec_context *ctx, uint64_t *d, uint64_t limb0, uint64_t nl, uint64_t np)
@@ -2601,7 +2607,12 @@ int hec_ntt_inverse(hec_context *ctx, uint64_t *d, uint64_t limb0, uint64_t nl, 
         need(d && nl >= 1 && limb0 + nl <= ctx->c.K && nl <= HEC_MAXL + 1, "invalid limb range");
         int pm[HEC_MAXL + 1];
         for (uint64_t i = 0; i < nl; ++i) pm[i] = (int)(limb0 + i);
-        ntt_strided(ctx->c, true, d, nl * ctx->c.N, d, nl * ctx->c.N, (int)nl, pm, (int)(nl * np));
+        {
+            ProfScope k(ctx->c, "k:k_ntt/inv_b", 2.0 * nl * np);
+            ntt_strided(ctx->c, true, d, nl * ctx->c.N, d, nl * ctx->c.N, (int)nl, pm, (int)(nl * np), 1, 1);
+        }
+        ProfScope k(ctx->c, "k:k_ntt/inv_a", 2.0 * nl * np);
+        ntt_strided(ctx->c, true, d, nl * ctx->c.N, d, nl * ctx->c.N, (int)nl, pm, (int)(nl * np), 1, 2);
     });
 }
 int hec_dyadic_multiply(hec_context *ctx, const uint64_t *a, const uint64_t *b, uint64_t *out, uint64_t limb0,
@@ -2610,6 +2621,7 @@ int hec_dyadic_multiply(hec_context *ctx, const uint64_t *a, const uint64_t *b, 
     return guard([&] {
         set_device(ctx);
         need(a && b && out && limb0 + nl <= ctx->c.K, "invalid limb range");
+        ProfScope k(ctx->c, "k:k_dyadic", 3.0 * nl * np);
         ew_dyadic(ctx->c, a, b, out, (int)limb0, (int)nl, (int)np);
     });
 }
