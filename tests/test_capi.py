@@ -56,7 +56,7 @@ def test_cpp_facade_links_against_boundary(hecdna, tmp_path):
                            "-I" + os.path.join(pkg, "..", "include"),
                            os.path.join(pkg, "cpp", "demo", "he_demo.cpp"),
                            os.path.join(pkg, "cpp", "src", "he_operators.cpp"),
-                           os.path.join(pkg, "cpp", "src", "he_linalg.cpp"),
+                           os.path.join(pkg, "cpp", "src", "he_linalg.cpp"), os.path.join(pkg, "cpp", "src", "he_math.cpp"),
                            "-L" + pkg, "-lhecdna", "-o", exe])
     out = subprocess.run([exe], capture_output=True, text=True, env=dict(os.environ, LD_LIBRARY_PATH=pkg))
     assert out.returncode == 1 and "usage" in out.stdout
