@@ -238,6 +238,21 @@ struct GlobalTw {
     __device__ double f(int s, int i) const { return twf[idx(s, i)]; }
     __device__ ulonglong2 w(int s, int i) const { return tw[idx(s, i)]; }
 };
+// SEAL-ordered table read through the constant address space: with a block-uniform index the loads are scalar
+// (s_load, counted by lgkmcnt, so they never wait behind the wave's outstanding vector loads)
+struct ConstTw {
+    typedef __attribute__((address_space(4))) const double cdouble;
+    typedef __attribute__((address_space(4))) const u64 cword;
+    const ulonglong2 *tw;
+    const double *twf;
+    __device__ double f(int s, int i) const { return ((cdouble *)twf)[(1u << s) + (unsigned)i]; }
+    __device__ ulonglong2 w(int s, int i) const
+    {
+        const unsigned k = 2 * ((1u << s) + (unsigned)i);
+        const u64 a = ((cword *)tw)[k], b = ((cword *)tw)[k + 1];
+        return ulonglong2{a, b};
+    }
+};
 struct LdsTw {  // entry k = 2^s - 1 + i of this segment; FP: one word (double bits), integer: {w, w_shoup}
     const u64 *row;
     __device__ double f(int s, int i) const { return __longlong_as_double((long long)row[(1 << s) - 1 + i]); }
@@ -897,6 +912,7 @@ __global__ void __launch_bounds__(NSEG *(1 << LOGP) / 16, OCC)
 #pragma unroll
         for (int k = 0; k < 16; ++k) v[k] = src.in[gblock(k)];
         const GlobalTw<decltype(twidx)> tg{twidx, inv.a + ((u64)src.prime << logN), inv.fa + ((u64)src.prime << logN)};
+        const ConstTw ctg{inv.a + ((u64)src.prime << logN), inv.fa + ((u64)src.prime << logN)};
         if (ps.fp) ntt_round_r<LOGP, 4, LOGP, true, true, decltype(tg), false, LEAN>(v, ts, tg, ps);
         else ntt_round_r<LOGP, 4, LOGP, true, false, decltype(tg), false, LEAN>(v, ts, tg, ps);
 #pragma unroll
@@ -906,12 +922,14 @@ __global__ void __launch_bounds__(NSEG *(1 << LOGP) / 16, OCC)
         for (int k = 0; k < 16; ++k) v[k] = lds[lstride(k)];
         buf = 1;
         if (ps.fp) {
-            ntt_round_r<LOGP, 0, 4, true, true, decltype(tg), LEAN, LEAN>(v, ts, tg, ps);
+            if constexpr (LEAN) ntt_round_r<LOGP, 0, 4, true, true, ConstTw, true, true>(v, ts, ctg, ps);
+            else ntt_round_r<LOGP, 0, 4, true, true>(v, ts, tg, ps);
 #pragma unroll
             for (int k = 0; k < 16; ++k)
                 d[k] = fp_canon(fp_mulmod(__longlong_as_double((long long)v[k]), ps.ninv_d, ps.qd, ps.qinv), ps.qd, ps.qinv);
         } else {
-            ntt_round_r<LOGP, 0, 4, true, false, decltype(tg), LEAN, LEAN>(v, ts, tg, ps);
+            if constexpr (LEAN) ntt_round_r<LOGP, 0, 4, true, false, ConstTw, true, true>(v, ts, ctg, ps);
+            else ntt_round_r<LOGP, 0, 4, true, false>(v, ts, tg, ps);
 #pragma unroll
             for (int k = 0; k < 16; ++k) d[k] = shoup(v[k], ps.ninv, ps.ninv_q, ps.q);
         }
@@ -931,16 +949,19 @@ __global__ void __launch_bounds__(NSEG *(1 << LOGP) / 16, OCC)
         if (!tgt.valid) continue;
         const DevPrime pt = primes[tgt.prime];
         const GlobalTw<decltype(twidx)> tw{twidx, fwd.a + ((u64)tgt.prime << logN), fwd.fa + ((u64)tgt.prime << logN)};
+        const ConstTw ctw{fwd.a + ((u64)tgt.prime << logN), fwd.fa + ((u64)tgt.prime << logN)};
         u64 *tile = lds + (DB ? buf * TILE : 0);
         buf ^= 1;
         if (!DB) __syncthreads();  // the previous exchange's reads are done
         u64 v[16];
         if (pt.fp) {
             fan.xf16(tgt, true, d, v);
-            ntt_round_r<LOGP, 0, 4, false, true, decltype(tw), LEAN, LEAN>(v, ts, tw, pt);
+            if constexpr (LEAN) ntt_round_r<LOGP, 0, 4, false, true, ConstTw, true, true>(v, ts, ctw, pt);
+            else ntt_round_r<LOGP, 0, 4, false, true>(v, ts, tw, pt);
         } else {
             fan.xf16(tgt, false, d, v);
-            ntt_round_r<LOGP, 0, 4, false, false, decltype(tw), LEAN, LEAN>(v, ts, tw, pt);
+            if constexpr (LEAN) ntt_round_r<LOGP, 0, 4, false, false, ConstTw, true, true>(v, ts, ctw, pt);
+            else ntt_round_r<LOGP, 0, 4, false, false>(v, ts, tw, pt);
         }
 #pragma unroll
         for (int k = 0; k < 16; ++k) tile[lstride(k)] = v[k];
