@@ -1252,9 +1252,6 @@ int hec_context_create(uint64_t N, const uint64_t *mod, uint64_t K, int device, 
         if (const char *f = std::getenv("HEC_FUSED_MODUP_MAC")) c.fused_modup_mac = f[0] != '0';
         if (const char *f = std::getenv("HEC_FUSE_GALOIS")) c.fuse_galois = f[0] != '0';
         if (const char *f = std::getenv("HEC_FAN")) c.fan_out = f[0] != '0';
-        if (const char *f = std::getenv("HEC_FAN_OCC")) c.fan_occ = std::atoi(f);
-        if (const char *f = std::getenv("HEC_TENSOR_XCD")) c.tensor_xcd = std::atoi(f);
-        if (const char *f = std::getenv("HEC_PRE_EARLY")) c.pre_early = std::atoi(f);
         if (const char *f = std::getenv("HEC_HOIST_SCAN")) c.hoist_scan = std::atoi(f);
         if (const char *f = std::getenv("HEC_LANES")) c.lanes = std::max(1, std::atoi(f));
         if (const char *f = std::getenv("HEC_HOIST")) c.hoist = f[0] != '0';

@@ -93,9 +93,6 @@ struct Ctx {
                                    // (1: INTT pass B, then the fan-out finishes the INTT and lists the zeros)
     int hmac_odd3 = 1;             // HEC_HMAC_ODD3=0: an odd sibling group ends in a pair and a single-child launch
     bool fan_out = true;           // HEC_FAN=0: separate INTT pass A (fan-out fuses it into the forward passes A)
-    int pre_early = 1;             // HEC_PRE_EARLY=0: forward pass B issues its post-op loads after the staging barrier
-    int tensor_xcd = 1;            // HEC_TENSOR_XCD=0: k_tensor_multi2 on a 2-D grid (batch groups far apart in time)
-    int fan_occ = 2;               // HEC_FAN_OCC=3: the fan-out at 3 waves per SIMD (one LDS tile, lean twiddle loads)
     int lanes = 3;                 // HEC_LANES: concurrent batch lanes of a matvec (hec_engine.hip matvec_lanes)
     int lane_min_batch = 16;       // input vectors per lane at least
     bool fuse_galois = true;       // HEC_FUSE_GALOIS=0: materialise apply_galois before the key switch

@@ -238,21 +238,6 @@ struct GlobalTw {
     __device__ double f(int s, int i) const { return twf[idx(s, i)]; }
     __device__ ulonglong2 w(int s, int i) const { return tw[idx(s, i)]; }
 };
-// SEAL-ordered table read through the constant address space: with a block-uniform index the loads are scalar
-// (s_load, counted by lgkmcnt, so they never wait behind the wave's outstanding vector loads)
-struct ConstTw {
-    typedef __attribute__((address_space(4))) const double cdouble;
-    typedef __attribute__((address_space(4))) const u64 cword;
-    const ulonglong2 *tw;
-    const double *twf;
-    __device__ double f(int s, int i) const { return ((cdouble *)twf)[(1u << s) + (unsigned)i]; }
-    __device__ ulonglong2 w(int s, int i) const
-    {
-        const unsigned k = 2 * ((1u << s) + (unsigned)i);
-        const u64 a = ((cword *)tw)[k], b = ((cword *)tw)[k + 1];
-        return ulonglong2{a, b};
-    }
-};
 struct LdsTw {  // entry k = 2^s - 1 + i of this segment; FP: one word (double bits), integer: {w, w_shoup}
     const u64 *row;
     __device__ double f(int s, int i) const { return __longlong_as_double((long long)row[(1 << s) - 1 + i]); }
@@ -352,7 +337,7 @@ __device__ __forceinline__ void ntt_round(u64 *lds, const AddrF &addr, int ts, c
 
 template <int LOGP, int NSEG, bool INV, bool PASS_A, bool FINAL, bool FP, class Bound>
 __device__ __forceinline__ void ntt_pass_body(u64 *lds, const Bound &bio, const DevPrime &pr, const TwTables &tt,
-                                              int logN, bool pre_early)
+                                              int logN)
 {
     constexpr int P = 1 << LOGP, TPS = P / 16, THREADS = NSEG * TPS;
     constexpr int LD = PASS_A ? (NSEG + 1) : (P + 1);
@@ -364,21 +349,24 @@ __device__ __forceinline__ void ntt_pass_body(u64 *lds, const Bound &bio, const 
     const ulonglong2 *tw = (PASS_A ? tt.a : tt.b) + ((u64)bio.prime << logN);
     const double *twf = (PASS_A ? tt.fa : tt.fb) + ((u64)bio.prime << logN);
 
-    constexpr int ITS = P * NSEG / THREADS;
-    u64 tv[ITS];
 #pragma unroll
-    for (int it = 0; it < ITS; ++it) {
+    for (int it = 0; it < P * NSEG / THREADS; ++it) {
         const int li = threadIdx.x + it * THREADS;
+        int x, sg;
         u64 g;
-        if constexpr (PASS_A) g = ((u64)(li / NSEG) << lc) + seg0 + li % NSEG;
-        else g = ((u64)(seg0 + li / P) << LOGP) + li % P;
-        tv[it] = bio.load(g);
+        if constexpr (PASS_A) { x = li / NSEG; sg = li % NSEG; g = ((u64)x << lc) + seg0 + sg; }
+        else { sg = li / P; x = li % P; g = ((u64)(seg0 + sg) << LOGP) + x; }
+        u64 v = bio.load(g);
+        if constexpr (FP && FIRST) v = (u64)__double_as_longlong(u2d(v));  // integer input -> double bits
+        lds[PASS_A ? x * LD + sg : sg * LD + x] = v;
     }
-    // post-op operands of this thread's output words: their loads are issued right behind the tile's (pre_early), so
-    // both latencies overlap, or after the staging barrier; either way before the rounds
+    __syncthreads();
+
+    // post-op operands of this thread's output words: issue their loads now so they overlap the rounds
+    constexpr int ITS = P * NSEG / THREADS;
     // (loading them at the store instead frees 64+ VGPRs but measured slower: 1313 vs 1271 ms/step)
     typename Bound::Pre pre[FINAL ? ITS : 1];
-    auto load_pre = [&] {
+    if constexpr (FINAL) {
 #pragma unroll
         for (int it = 0; it < ITS; ++it) {
             const int li = threadIdx.x + it * THREADS;
@@ -387,22 +375,7 @@ __device__ __forceinline__ void ntt_pass_body(u64 *lds, const Bound &bio, const 
             else g = ((u64)(seg0 + li / P) << LOGP) + li % P;
             pre[it] = bio.pre(g);
         }
-    };
-    if constexpr (FINAL)
-        if (pre_early) load_pre();
-#pragma unroll
-    for (int it = 0; it < ITS; ++it) {
-        const int li = threadIdx.x + it * THREADS;
-        int x, sg;
-        if constexpr (PASS_A) { x = li / NSEG; sg = li % NSEG; }
-        else { sg = li / P; x = li % P; }
-        u64 v = tv[it];
-        if constexpr (FP && FIRST) v = (u64)__double_as_longlong(u2d(v));  // integer input -> double bits
-        lds[PASS_A ? x * LD + sg : sg * LD + x] = v;
     }
-    __syncthreads();
-    if constexpr (FINAL)
-        if (!pre_early) load_pre();
     const int ts = threadIdx.x / NSEG, sg = threadIdx.x % NSEG;
     auto addr = [sg](int x) { return PASS_A ? x * LD + sg : sg * LD + x; };
     // pass A: SEAL table index 2^s + i (shared by all columns: broadcast reads).
@@ -594,7 +567,7 @@ __device__ __forceinline__ void ntt_pass_body_rd(u64 *lds, const Bound &bio, con
 // every round through LDS (ntt_pass_body: the forward pass B, where register-direct measured slower)
 template <int LOGP, int NSEG, bool INV, bool PASS_A, bool FINAL, class IO, bool RD = false>
 __global__ void __launch_bounds__(NSEG *(1 << LOGP) / 16)
-    k_ntt(const IO io, TwTables tt, const DevPrime *__restrict__ primes, int logN, int pre_early = 1)
+    k_ntt(const IO io, TwTables tt, const DevPrime *__restrict__ primes, int logN)
 {
     static_assert(LOGP >= 5 && LOGP <= 8, "two rounds of 4 stages");
     constexpr int WORDS = !RD ? (PASS_A ? (1 << LOGP) * (NSEG + 1) : NSEG * ((1 << LOGP) + 1))
@@ -606,8 +579,8 @@ __global__ void __launch_bounds__(NSEG *(1 << LOGP) / 16)
     if constexpr (RD) {
         if (pr.fp) ntt_pass_body_rd<LOGP, NSEG, INV, PASS_A, FINAL, true>(lds, bio, pr, tt, logN);
         else ntt_pass_body_rd<LOGP, NSEG, INV, PASS_A, FINAL, false>(lds, bio, pr, tt, logN);
-    } else if (pr.fp) ntt_pass_body<LOGP, NSEG, INV, PASS_A, FINAL, true>(lds, bio, pr, tt, logN, pre_early != 0);
-    else ntt_pass_body<LOGP, NSEG, INV, PASS_A, FINAL, false>(lds, bio, pr, tt, logN, pre_early != 0);
+    } else if (pr.fp) ntt_pass_body<LOGP, NSEG, INV, PASS_A, FINAL, true>(lds, bio, pr, tt, logN);
+    else ntt_pass_body<LOGP, NSEG, INV, PASS_A, FINAL, false>(lds, bio, pr, tt, logN);
 }
 
 template <int LOGR, int LOGC, int NA, int NB, bool INV, class IO1, class IO2>
@@ -622,8 +595,7 @@ static void run_ntt2(Ctx &c, int njobs, const IO1 &first, const IO2 &second, int
                            // SQ counters: a third fewer LDS and VMEM instructions, no bank conflicts either way,
                            // but 2.2x the cycles waiting on load dependencies and 15 % more wave cycles)
         if (stages & 1) k_ntt<LOGR, NA, false, true, false, IO1, true><<<gA, TA, 0, c.stream>>>(first, fwd, c.primes, c.logN);
-        if (stages & 2)
-            k_ntt<LOGC, NB, false, false, true><<<gB, TB, 0, c.stream>>>(second, fwd, c.primes, c.logN, c.pre_early);
+        if (stages & 2) k_ntt<LOGC, NB, false, false, true><<<gB, TB, 0, c.stream>>>(second, fwd, c.primes, c.logN);
     } else {
         if (stages & 1) k_ntt<LOGC, NB, true, false, false, IO1, true><<<gB, TB, 0, c.stream>>>(first, inv, c.primes, c.logN);
         if (stages & 2) k_ntt<LOGR, NA, true, true, true, IO2, true><<<gA, TA, 0, c.stream>>>(second, inv, c.primes, c.logN);
@@ -836,11 +808,7 @@ struct FanDivRound {  // source (b, k) = last limb (inverse pass-B domain) -> Z[
 // elements ntt_round_g gives it for stages [S0, S1): v[gi 2^D + a] <-> x = xb(ts G + gi) | (a << (LOGP - S1)).
 // Round 0 (stages 0..3) owns x = ts + k TPS ("stride set"), round 1 (stages 4..LOGP-1) x = 16 ts + k ("block
 // set"), k = 0..15, TPS = P / 16.
-// UNI: the round's groups all have hi = 0 (round 0 of a column transform: ts < 2^(LOGP - 4)), so every twiddle
-// index is a compile-time offset from a block-uniform table base and the loads are scalar (SMEM, lgkmcnt).
-// STAGED: a compiler fence before every stage keeps each stage's twiddle loads next to the stage instead of all
-// 15 hoisted to the round's start (VGPR pressure of the 3-waves-per-SIMD fan-out).
-template <int LOGP, int S0, int S1, bool INV, bool FP, class TwG, bool UNI = false, bool STAGED = false>
+template <int LOGP, int S0, int S1, bool INV, bool FP, class TwG>
 __device__ __forceinline__ void ntt_round_r(u64 *v, int ts, const TwG &twg, const DevPrime &pr)
 {
     constexpr int D = S1 - S0, G = 1 << (4 - D), NQ = 1 << D;
@@ -849,10 +817,9 @@ __device__ __forceinline__ void ntt_round_r(u64 *v, int ts, const TwG &twg, cons
 #pragma unroll
     for (int gi = 0; gi < G; ++gi) {
         const int g = ts * G + gi;
-        const int hi = UNI ? 0 : g >> (LOGP - S1);
+        const int hi = g >> (LOGP - S1);
 #pragma unroll
         for (int k = 0; k < D; ++k) {
-            if constexpr (STAGED) asm volatile("" ::: "memory");
             const int st = INV ? D - 1 - k : k;
             const int bit = 1 << (D - 1 - st);
 #pragma unroll
@@ -884,13 +851,10 @@ __device__ __forceinline__ void ntt_round_r(u64 *v, int ts, const TwG &twg, cons
 // DB: two alternating LDS tiles and one barrier per exchange (2 blocks per CU at N = 2^15); DB = false: one
 // tile and a second barrier per target.  (One tile with 3 waves per SIMD forced, 168 VGPRs and 20-30 spilled,
 // measured slower: k_fan 3,565 vs 2,601 ms per step.)
-// OCC = 3 (HEC_FAN_OCC=3): one LDS tile (two barriers per target) and <= 168 VGPRs for 3 waves per SIMD: the
-// forward round 0's twiddles are block-uniform scalar loads and every other stage loads its own twiddles.
-template <int LOGP, int NSEG, class FAN, bool DB = true, int OCC = 2>
-__global__ void __launch_bounds__(NSEG *(1 << LOGP) / 16, OCC)
+template <int LOGP, int NSEG, class FAN, bool DB = true>
+__global__ void __launch_bounds__(NSEG *(1 << LOGP) / 16)
     k_fan2(const FAN fan, TwTables inv, TwTables fwd, const DevPrime *__restrict__ primes, int logN)
 {
-    constexpr bool LEAN = OCC > 2;
     constexpr int P = 1 << LOGP, TPS = P / 16, LD = NSEG + 1, TILE = P * LD;
     __shared__ u64 lds[(DB ? 2 : 1) * TILE];
     const int seg0 = blockIdx.x * NSEG, lc = logN - LOGP;
@@ -912,9 +876,8 @@ __global__ void __launch_bounds__(NSEG *(1 << LOGP) / 16, OCC)
 #pragma unroll
         for (int k = 0; k < 16; ++k) v[k] = src.in[gblock(k)];
         const GlobalTw<decltype(twidx)> tg{twidx, inv.a + ((u64)src.prime << logN), inv.fa + ((u64)src.prime << logN)};
-        const ConstTw ctg{inv.a + ((u64)src.prime << logN), inv.fa + ((u64)src.prime << logN)};
-        if (ps.fp) ntt_round_r<LOGP, 4, LOGP, true, true, decltype(tg), false, LEAN>(v, ts, tg, ps);
-        else ntt_round_r<LOGP, 4, LOGP, true, false, decltype(tg), false, LEAN>(v, ts, tg, ps);
+        if (ps.fp) ntt_round_r<LOGP, 4, LOGP, true, true>(v, ts, tg, ps);
+        else ntt_round_r<LOGP, 4, LOGP, true, false>(v, ts, tg, ps);
 #pragma unroll
         for (int k = 0; k < 16; ++k) lds[lblock(k)] = v[k];
         __syncthreads();
@@ -922,14 +885,12 @@ __global__ void __launch_bounds__(NSEG *(1 << LOGP) / 16, OCC)
         for (int k = 0; k < 16; ++k) v[k] = lds[lstride(k)];
         buf = 1;
         if (ps.fp) {
-            if constexpr (LEAN) ntt_round_r<LOGP, 0, 4, true, true, ConstTw, true, true>(v, ts, ctg, ps);
-            else ntt_round_r<LOGP, 0, 4, true, true>(v, ts, tg, ps);
+            ntt_round_r<LOGP, 0, 4, true, true>(v, ts, tg, ps);
 #pragma unroll
             for (int k = 0; k < 16; ++k)
                 d[k] = fp_canon(fp_mulmod(__longlong_as_double((long long)v[k]), ps.ninv_d, ps.qd, ps.qinv), ps.qd, ps.qinv);
         } else {
-            if constexpr (LEAN) ntt_round_r<LOGP, 0, 4, true, false, ConstTw, true, true>(v, ts, ctg, ps);
-            else ntt_round_r<LOGP, 0, 4, true, false>(v, ts, tg, ps);
+            ntt_round_r<LOGP, 0, 4, true, false>(v, ts, tg, ps);
 #pragma unroll
             for (int k = 0; k < 16; ++k) d[k] = shoup(v[k], ps.ninv, ps.ninv_q, ps.q);
         }
@@ -949,27 +910,24 @@ __global__ void __launch_bounds__(NSEG *(1 << LOGP) / 16, OCC)
         if (!tgt.valid) continue;
         const DevPrime pt = primes[tgt.prime];
         const GlobalTw<decltype(twidx)> tw{twidx, fwd.a + ((u64)tgt.prime << logN), fwd.fa + ((u64)tgt.prime << logN)};
-        const ConstTw ctw{fwd.a + ((u64)tgt.prime << logN), fwd.fa + ((u64)tgt.prime << logN)};
         u64 *tile = lds + (DB ? buf * TILE : 0);
         buf ^= 1;
         if (!DB) __syncthreads();  // the previous exchange's reads are done
         u64 v[16];
         if (pt.fp) {
             fan.xf16(tgt, true, d, v);
-            if constexpr (LEAN) ntt_round_r<LOGP, 0, 4, false, true, ConstTw, true, true>(v, ts, ctw, pt);
-            else ntt_round_r<LOGP, 0, 4, false, true>(v, ts, tw, pt);
+            ntt_round_r<LOGP, 0, 4, false, true>(v, ts, tw, pt);
         } else {
             fan.xf16(tgt, false, d, v);
-            if constexpr (LEAN) ntt_round_r<LOGP, 0, 4, false, false, ConstTw, true, true>(v, ts, ctw, pt);
-            else ntt_round_r<LOGP, 0, 4, false, false>(v, ts, tw, pt);
+            ntt_round_r<LOGP, 0, 4, false, false>(v, ts, tw, pt);
         }
 #pragma unroll
         for (int k = 0; k < 16; ++k) tile[lstride(k)] = v[k];
         __syncthreads();
 #pragma unroll
         for (int k = 0; k < 16; ++k) v[k] = tile[lblock(k)];
-        if (pt.fp) ntt_round_r<LOGP, 4, LOGP, false, true, decltype(tw), false, LEAN>(v, ts, tw, pt);
-        else ntt_round_r<LOGP, 4, LOGP, false, false, decltype(tw), false, LEAN>(v, ts, tw, pt);
+        if (pt.fp) ntt_round_r<LOGP, 4, LOGP, false, true>(v, ts, tw, pt);
+        else ntt_round_r<LOGP, 4, LOGP, false, false>(v, ts, tw, pt);
 #pragma unroll
         for (int k = 0; k < 16; ++k) tgt.out[gblock(k)] = v[k];
     }
@@ -980,11 +938,7 @@ static void run_fan(Ctx &c, int njobs, const FAN &fan, int groups)
 {
     constexpr int R = 1 << LOGR, C = 1 << LOGC;
     const TwTables fwd{c.tw, c.twb, c.twf, c.twbf}, inv{c.itw, c.itwb, c.itwf, c.itwbf};
-    const dim3 grid(C / NA, njobs, groups);
-    if (c.fan_occ >= 3 && LOGR >= 5)
-        k_fan2<LOGR, NA, FAN, false, 3><<<grid, NA * R / 16, 0, c.stream>>>(fan, inv, fwd, c.primes, c.logN);
-    else
-        k_fan2<LOGR, NA><<<grid, NA * R / 16, 0, c.stream>>>(fan, inv, fwd, c.primes, c.logN);
+    k_fan2<LOGR, NA><<<dim3(C / NA, njobs, groups), NA * R / 16, 0, c.stream>>>(fan, inv, fwd, c.primes, c.logN);
     HEC_HIP(hipGetLastError());
 }
 template <class FAN>
@@ -2028,25 +1982,14 @@ void tensor_acc(Ctx &c, PolyArr R, const u64 *A, u64 a_sk, PolyArr ACC, int B, i
 // accumulators, so a wave has BG rotated-input loads in flight per diagonal and the diagonals are re-read
 // B / BG times (from L2) instead of B times.  Products are reduced as SEAL reduces them; sums are exact
 // (FP64: |sum| < 12 x 0.53 q; 60-bit primes: 128-bit sums of < 2^120 products) and canonicalised once.
-// XCD (nxg > 0): a 1-D grid in which the ny batch groups of one coefficient block get consecutive ids of one residue
-// mod 8, i.e. run back to back on one XCD, so that block's diagonal words come from that XCD's L2 after the first
-// group (id w: XCD w % 8, rest = w / 8: group rest % ny, coefficient block (rest / ny) 8 + w % 8); nxg = the padded
-// number of coefficient blocks.  Otherwise grid (coefficient blocks, batch groups).
 template <bool PT, int BG>
 __global__ void __launch_bounds__(256)
     k_tensor_multi2(TensorBatch tb, u64 r_sb, u64 r_sk, u64 a_sk, PolyArr ACC, int B, int logN, u64 total, int assign,
-                    const DevPrime *__restrict__ primes, int nxg)
+                    const DevPrime *__restrict__ primes)
 {
-    int bx = blockIdx.x, by = blockIdx.y;
-    if (nxg > 0) {
-        const int ny = (B + BG - 1) / BG, w = blockIdx.x, rest = w >> 3;
-        by = rest % ny;
-        bx = (rest / ny) * 8 + (w & 7);
-        if (bx >= nxg) return;
-    }
-    const u64 idx = (u64)bx * 256 + threadIdx.x;
+    const u64 idx = (u64)blockIdx.x * 256 + threadIdx.x;
     if (idx >= total) return;
-    const int b0 = by * BG;
+    const int b0 = blockIdx.y * BG;
     const int nb = min(BG, B - b0);
     const DevPrime pr = primes[idx >> logN];
     u64 d0[BG], d1[BG], d2[BG];
@@ -2121,15 +2064,13 @@ void tensor_multi(Ctx &c, const TensorBatch &tb, u64 r_sb, u64 r_sk, u64 a_sk, P
     const u64 total = (u64)l * c.N;
     const unsigned grid = (unsigned)((total + 255) / 256);
     constexpr int BG = 2;  // batch entries per thread (round 3, r03t: 533 vs 578 ms per step for 4, 577 for 8)
-    const unsigned ny = (unsigned)((B + BG - 1) / BG);
-    const int nxg = c.tensor_xcd ? (int)grid : 0;
-    const dim3 g2 = c.tensor_xcd ? dim3((grid + 7) / 8 * 8 * ny) : dim3(grid, ny);
+    const dim3 g2(grid, (unsigned)((B + BG - 1) / BG));
     if (plain)
         k_tensor_multi2<true, BG><<<g2, 256, 0, c.stream>>>(tb, r_sb, r_sk, a_sk, ACC, B, c.logN, total, assign ? 1 : 0,
-                                                           c.primes, nxg);
+                                                           c.primes);
     else
         k_tensor_multi2<false, BG><<<g2, 256, 0, c.stream>>>(tb, r_sb, r_sk, a_sk, ACC, B, c.logN, total,
-                                                            assign ? 1 : 0, c.primes, nxg);
+                                                            assign ? 1 : 0, c.primes);
     HEC_HIP(hipGetLastError());
 }
 
