@@ -686,6 +686,8 @@ template <bool DIRECT>
 struct FanModUpT {  // source (b, J) = D[b][J] (inverse pass-B domain) -> E[b][I][J], I != J, mod q_I
     static constexpr bool kDirect = DIRECT;
     static constexpr bool kScan = !DIRECT;
+    static constexpr bool kSplit = false;
+    static constexpr bool kSrcDouble = !DIRECT;  // an FP64-class source stays a double (xf16's sdbl)
     const u64 *D;
     u64 *E;
     int l, logN, kP;
@@ -714,8 +716,23 @@ struct FanModUpT {  // source (b, J) = D[b][J] (inverse pass-B domain) -> E[b][I
     // targets take any congruent integer-valued double with |x| < 2 q_I (their forward butterflies stay below
     // 10 q_I over all stages and every output is canonicalised): a digit with q_J <= 2 q_I needs no
     // reduction at all, only the conversion
-    __device__ void xf16(const Tgt &t, bool fp, const u64 *d, u64 *v) const
+    // sdbl: the source (an FP64-class digit, q_J < 2^42) is held as the bits of its canonical integer-valued double,
+    // converted once per block instead of once per FP64 target; the two integer targets convert it back
+    __device__ void xf16(const Tgt &t, bool fp, const u64 *d, const u32 *, u64 *v, bool sdbl = false) const
     {
+        if (sdbl) {
+            if (fp) {
+#pragma unroll
+                for (int k = 0; k < 16; ++k) v[k] = d[k];  // q_J < 2 q_I: no reduction (see above)
+                return;
+            }
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                const u64 y = d2u(__longlong_as_double((long long)d[k]));
+                v[k] = t.red == 1 ? csub(y, t.q) : y;  // red == 2 needs q_J > 2 q_I: only the 60-bit digit J = 0
+            }
+            return;
+        }
         if (t.red == 2 && fp && t.q > (1ull << 32)) {  // the 60-bit digit at an FP64 target: hi 2^30 + lo as above
             const DevPrime &p = primes[t.prime];
 #pragma unroll
@@ -747,6 +764,11 @@ using FanModUp = FanModUpT<false>;
 struct FanDivRound {  // source (b, k) = last limb (inverse pass-B domain) -> Z[b][k][i] for i < nl
     static constexpr bool kDirect = false;
     static constexpr bool kScan = false;
+    // the source value y < P < 2^60 is split once per block into hs = (y >> 30) 2^30 (an exact double, kept in d's
+    // bits) and lo = y & (2^30 - 1) (u32), so an FP64 target only reduces hs (one FMA) and adds lo: 6 FP64 operations
+    // per value and target instead of 13 mixed ones
+    static constexpr bool kSplit = true;
+    static constexpr bool kSrcDouble = false;
     int *zl = nullptr, *zflag = nullptr;
     const u64 *Y;
     u64 ysb, ysk;
@@ -778,24 +800,37 @@ struct FanDivRound {  // source (b, k) = last limb (inverse pass-B domain) -> Z[
     // an exact double and its reduction r = hi 2^30 - rint(hi 2^30 / q_i) q_i is exact in one FMA (|r| <= 0.5 q_i),
     // so the value is an integer-valued double in (-0.51 q_i, 1.51 q_i + 2^30), within the FP64 forward NTT's
     // |x| < 2 q_i input range
-    // (no 64-bit Barrett: ~8 FP64 operations per value instead of 7 integer multiplies).  Smaller FP64 primes
-    // and the integer targets keep Barrett.
-    __device__ void xf16(const Tgt &t, bool fp, const u64 *d, u64 *v) const
+    // (no 64-bit Barrett: ~6 FP64 operations per value instead of 7 integer multiplies).  Smaller FP64 primes
+    // and the integer targets keep Barrett on y rebuilt from its halves.
+    __device__ static void split(u64 *d, u32 *lo)  // once per block: d[k] = y -> bits of (y >> 30) 2^30, lo[k]
+    {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            lo[k] = (u32)(d[k] & 0x3fffffffull);
+            d[k] = (u64)__double_as_longlong(u2d(d[k] >> 30) * 1073741824.0);
+        }
+    }
+    __device__ static u64 join(u64 hs, u32 lo)
+    {
+        return (d2u(__longlong_as_double((long long)hs) * (1.0 / 1073741824.0)) << 30) | lo;
+    }
+    __device__ void xf16(const Tgt &t, bool fp, const u64 *d, const u32 *lo, u64 *v, bool = false) const
     {
         if (fp && t.c30 != 0.0) {
             const double fx = (double)t.fix;
 #pragma unroll
             for (int k = 0; k < 16; ++k) {
-                u64 y = d[k];
-                asm volatile("" : "+v"(y));  // per target: hoisting the 32 split doubles out of the target loop
-                                             // would keep them live beside d (274 VGPRs, one wave per SIMD)
-                const double hi = u2d(y >> 30) * 1073741824.0, lo = u2d(y & 0x3fffffffull);  // hi: exact, < 2^60
-                v[k] = (u64)__double_as_longlong(fp_reduce(hi, t.qd, t.qinv) + (lo + fx));
+                u64 h = d[k];
+                u32 l = lo[k];
+                asm volatile("" : "+v"(h), "+v"(l));  // per target: the conversions are not hoisted out of the target
+                                                      // loop (32 more live doubles: 256 VGPRs, one wave per SIMD)
+                const double hs = __longlong_as_double((long long)h);
+                v[k] = (u64)__double_as_longlong(fp_reduce(hs, t.qd, t.qinv) + ((double)l + fx));
             }
             return;
         }
 #pragma unroll
-        for (int k = 0; k < 16; ++k) v[k] = xf(t, d[k]);
+        for (int k = 0; k < 16; ++k) v[k] = xf(t, join(d[k], lo[k]));
         if (fp) {
 #pragma unroll
             for (int k = 0; k < 16; ++k) v[k] = (u64)__double_as_longlong(u2d(v[k]));
@@ -868,6 +903,7 @@ __global__ void __launch_bounds__(NSEG *(1 << LOGP) / 16)
     const DevPrime ps = primes[src.prime];
     int buf = 0;
     u64 d[16];  // canonical coefficient-form values of the source, stride set
+    u32 lo[FAN::kSplit ? 16 : 1];  // kSplit: the low 30 bits (d then holds the high part as a double)
     if constexpr (FAN::kDirect) {
 #pragma unroll
         for (int k = 0; k < 16; ++k) d[k] = src.in[gstride(k)];
@@ -887,8 +923,12 @@ __global__ void __launch_bounds__(NSEG *(1 << LOGP) / 16)
         if (ps.fp) {
             ntt_round_r<LOGP, 0, 4, true, true>(v, ts, tg, ps);
 #pragma unroll
-            for (int k = 0; k < 16; ++k)
-                d[k] = fp_canon(fp_mulmod(__longlong_as_double((long long)v[k]), ps.ninv_d, ps.qd, ps.qinv), ps.qd, ps.qinv);
+            for (int k = 0; k < 16; ++k) {
+                const double c = fp_mulmod(__longlong_as_double((long long)v[k]), ps.ninv_d, ps.qd, ps.qinv);
+                d[k] = fp_canon(c, ps.qd, ps.qinv);
+                // the canonical residue as an exact double (its bits; +0.0 for zero, so the zero scan is unchanged)
+                if constexpr (FAN::kSrcDouble) d[k] = (u64)__double_as_longlong(u2d(d[k]));
+            }
         } else {
             ntt_round_r<LOGP, 0, 4, true, false>(v, ts, tg, ps);
 #pragma unroll
@@ -896,6 +936,7 @@ __global__ void __launch_bounds__(NSEG *(1 << LOGP) / 16)
         }
 #pragma unroll
         for (int k = 0; k < 16; ++k) d[k] = fan.src_fix(d[k]);
+        if constexpr (FAN::kSplit) FAN::split(d, lo);
         if constexpr (FAN::kScan) {
             if (fan.zl != nullptr && blockIdx.z == 0) {  // the canonical coefficient form's zeros (k_zscan)
 #pragma unroll
@@ -915,10 +956,10 @@ __global__ void __launch_bounds__(NSEG *(1 << LOGP) / 16)
         if (!DB) __syncthreads();  // the previous exchange's reads are done
         u64 v[16];
         if (pt.fp) {
-            fan.xf16(tgt, true, d, v);
+            fan.xf16(tgt, true, d, lo, v, FAN::kSrcDouble && ps.fp);
             ntt_round_r<LOGP, 0, 4, false, true>(v, ts, tw, pt);
         } else {
-            fan.xf16(tgt, false, d, v);
+            fan.xf16(tgt, false, d, lo, v, FAN::kSrcDouble && ps.fp);
             ntt_round_r<LOGP, 0, 4, false, false>(v, ts, tw, pt);
         }
 #pragma unroll
@@ -1187,10 +1228,19 @@ __device__ __forceinline__ void hmacm_body(PolyArr X1, const u64 *__restrict__ E
         const ulonglong2 w = *(const ulonglong2 *)(ch.c[q].W + ((u64)kI << logN) + kc[q]);
         const ulonglong2 m0 = *(const ulonglong2 *)(ch.c[q].KW + ((u64)I << logN) + kc[q]);
         const ulonglong2 m1 = *(const ulonglong2 *)(ch.c[q].KW + ((u64)(l + 1 + I) << logN) + kc[q]);
-        wk[q][0] = mulmod(w.x, m0.x, pr);
-        wk[q][1] = mulmod(w.y, m0.y, pr);
-        wk[q][2] = mulmod(w.x, m1.x, pr);
-        wk[q][3] = mulmod(w.y, m1.y, pr);
+        if constexpr (FP) {  // FP64 class: the exact FP64 product (a residue in [-0.53 q, 0.53 q], as bits) starts
+                             // the accumulator, instead of a 128-bit Barrett product
+            const double wx = u2d(w.x), wy = u2d(w.y);
+            wk[q][0] = (u64)__double_as_longlong(fp_mulmod(wx, u2d(m0.x), pr.qd, pr.qinv));
+            wk[q][1] = (u64)__double_as_longlong(fp_mulmod(wy, u2d(m0.y), pr.qd, pr.qinv));
+            wk[q][2] = (u64)__double_as_longlong(fp_mulmod(wx, u2d(m1.x), pr.qd, pr.qinv));
+            wk[q][3] = (u64)__double_as_longlong(fp_mulmod(wy, u2d(m1.y), pr.qd, pr.qinv));
+        } else {
+            wk[q][0] = mulmod(w.x, m0.x, pr);
+            wk[q][1] = mulmod(w.y, m0.y, pr);
+            wk[q][2] = mulmod(w.x, m1.x, pr);
+            wk[q][3] = mulmod(w.y, m1.y, pr);
+        }
         if (sw[q]) {
             u64 x = wk[q][0]; wk[q][0] = wk[q][1]; wk[q][1] = x;
             x = wk[q][2]; wk[q][2] = wk[q][3]; wk[q][3] = x;
@@ -1204,8 +1254,8 @@ __device__ __forceinline__ void hmacm_body(PolyArr X1, const u64 *__restrict__ E
         for (int t = 0; t < BT; ++t)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const u64 w0 = q < ch.n ? wk[q][r] : 0;
-                if constexpr (FP) f[q][t][r] = u2d(w0);
+                const u64 w0 = q < ch.n ? wk[q][r] : 0;  // FP64: double bits (0 is +0.0)
+                if constexpr (FP) f[q][t][r] = __longlong_as_double((long long)w0);
                 else a[q][t][r] = U128{w0, 0};
             }
     auto digit = [&](int J, int t) -> ulonglong2 {
