@@ -23,6 +23,21 @@ struct DevPrime {
     int fp;                   // 1 -> NTT kernels use the exact FP64 arithmetic below
 };
 
+// primes[i] read through the constant address space: with a block-uniform i the loads are scalar (lgkmcnt), so a
+// kernel that stores and then looks up its next prime does not wait for its stores (a vector load's vmcnt wait
+// includes every store issued before it)
+__device__ __forceinline__ DevPrime cprime(const DevPrime *primes, int i)
+{
+    typedef __attribute__((address_space(4))) const u64 cword;
+    static_assert(sizeof(DevPrime) % 8 == 0, "DevPrime is copied as words");
+    u64 w[sizeof(DevPrime) / 8];
+#pragma unroll
+    for (unsigned k = 0; k < sizeof(DevPrime) / 8; ++k) w[k] = ((cword *)(primes + i))[k];
+    DevPrime r;
+    __builtin_memcpy(&r, w, sizeof(DevPrime));
+    return r;
+}
+
 __device__ __forceinline__ u64 mulhi64(u64 a, u64 b) { return __umul64hi(a, b); }
 
 // x * w mod q in [0, 2q) for any x < 2^64, w < q, wq = floor(w * 2^64 / q)

@@ -238,6 +238,22 @@ struct GlobalTw {
     __device__ double f(int s, int i) const { return twf[idx(s, i)]; }
     __device__ ulonglong2 w(int s, int i) const { return tw[idx(s, i)]; }
 };
+// The SEAL-ordered table read through the constant address space: with a block-uniform index the loads are scalar
+// (s_load, counted by lgkmcnt), so they never wait behind the wave's outstanding vector stores and loads (on CDNA
+// a vector load's vmcnt wait also waits for every store issued before it)
+struct ConstTw {
+    typedef __attribute__((address_space(4))) const double cdouble;
+    typedef __attribute__((address_space(4))) const u64 cword;
+    const ulonglong2 *tw;
+    const double *twf;
+    __device__ double f(int s, int i) const { return ((cdouble *)twf)[(1u << s) + (unsigned)i]; }
+    __device__ ulonglong2 w(int s, int i) const
+    {
+        const unsigned k = 2 * ((1u << s) + (unsigned)i);
+        const u64 a = ((cword *)tw)[k], b = ((cword *)tw)[k + 1];
+        return ulonglong2{a, b};
+    }
+};
 struct LdsTw {  // entry k = 2^s - 1 + i of this segment; FP: one word (double bits), integer: {w, w_shoup}
     const u64 *row;
     __device__ double f(int s, int i) const { return __longlong_as_double((long long)row[(1 << s) - 1 + i]); }
@@ -703,8 +719,9 @@ struct FanModUpT {  // source (b, J) = D[b][J] (inverse pass-B domain) -> E[b][I
     __device__ Tgt tgt(int job, int I) const
     {
         const int b = job / l, J = job % l, p = I == l ? kP : I;
-        const u64 qI = primes[p].q, qJ = primes[J].q;
-        return Tgt{I != J, p, E + (((u64)((b * (l + 1) + I) * l + J)) << logN), qI, primes[p].r1,
+        const DevPrime pp = cprime(primes, p);
+        const u64 qI = pp.q, qJ = cprime(primes, J).q;
+        return Tgt{I != J, p, E + (((u64)((b * (l + 1) + I) * l + J)) << logN), qI, pp.r1,
                    qJ <= qI ? 0 : (qJ <= 2 * qI ? 1 : 2)};
     }
     __device__ u64 src_fix(u64 d) const { return d; }
@@ -734,7 +751,7 @@ struct FanModUpT {  // source (b, J) = D[b][J] (inverse pass-B domain) -> E[b][I
             return;
         }
         if (t.red == 2 && fp && t.q > (1ull << 32)) {  // the 60-bit digit at an FP64 target: hi 2^30 + lo as above
-            const DevPrime &p = primes[t.prime];
+            const DevPrime p = cprime(primes, t.prime);
 #pragma unroll
             for (int k = 0; k < 16; ++k) {
                 u64 y = d[k];
@@ -785,7 +802,7 @@ struct FanDivRound {  // source (b, k) = last limb (inverse pass-B domain) -> Z[
     __device__ Src src(int job) const { return Src{Y + (u64)(job / nk) * ysb + (u64)(job % nk) * ysk, last_idx}; }
     __device__ Tgt tgt(int job, int i) const
     {
-        const DevPrime &p = primes[i];
+        const DevPrime p = cprime(primes, i);
         return Tgt{true, i, Z + ((u64)(job * nl + i) << logN), p.q, p.r1, fix[i], p.qd, p.qinv, c30[i],
                    ((sub1 >> i) & 1u) != 0};
     }
@@ -843,7 +860,9 @@ struct FanDivRound {  // source (b, k) = last limb (inverse pass-B domain) -> Z[
 // elements ntt_round_g gives it for stages [S0, S1): v[gi 2^D + a] <-> x = xb(ts G + gi) | (a << (LOGP - S1)).
 // Round 0 (stages 0..3) owns x = ts + k TPS ("stride set"), round 1 (stages 4..LOGP-1) x = 16 ts + k ("block
 // set"), k = 0..15, TPS = P / 16.
-template <int LOGP, int S0, int S1, bool INV, bool FP, class TwG>
+// UNI: every group of the round has hi = 0 (round 0 of a column transform: ts < 2^(LOGP - 4)), so the twiddle
+// indices are compile-time offsets from a block-uniform table base (with ConstTw: scalar loads)
+template <int LOGP, int S0, int S1, bool INV, bool FP, class TwG, bool UNI = false>
 __device__ __forceinline__ void ntt_round_r(u64 *v, int ts, const TwG &twg, const DevPrime &pr)
 {
     constexpr int D = S1 - S0, G = 1 << (4 - D), NQ = 1 << D;
@@ -852,7 +871,7 @@ __device__ __forceinline__ void ntt_round_r(u64 *v, int ts, const TwG &twg, cons
 #pragma unroll
     for (int gi = 0; gi < G; ++gi) {
         const int g = ts * G + gi;
-        const int hi = g >> (LOGP - S1);
+        const int hi = UNI ? 0 : g >> (LOGP - S1);
 #pragma unroll
         for (int k = 0; k < D; ++k) {
             const int st = INV ? D - 1 - k : k;
@@ -900,7 +919,7 @@ __global__ void __launch_bounds__(NSEG *(1 << LOGP) / 16)
     auto lblock = [&](int k) { return (16 * ts + k) * LD + sg; };
     auto twidx = [](int s, int i) -> u64 { return (1ull << s) + (u64)i; };
     const auto src = fan.src(blockIdx.y);
-    const DevPrime ps = primes[src.prime];
+    const DevPrime ps = cprime(primes, src.prime);
     int buf = 0;
     u64 d[16];  // canonical coefficient-form values of the source, stride set
     u32 lo[FAN::kSplit ? 16 : 1];  // kSplit: the low 30 bits (d then holds the high part as a double)
@@ -912,6 +931,7 @@ __global__ void __launch_bounds__(NSEG *(1 << LOGP) / 16)
 #pragma unroll
         for (int k = 0; k < 16; ++k) v[k] = src.in[gblock(k)];
         const GlobalTw<decltype(twidx)> tg{twidx, inv.a + ((u64)src.prime << logN), inv.fa + ((u64)src.prime << logN)};
+        const ConstTw ctg{inv.a + ((u64)src.prime << logN), inv.fa + ((u64)src.prime << logN)};
         if (ps.fp) ntt_round_r<LOGP, 4, LOGP, true, true>(v, ts, tg, ps);
         else ntt_round_r<LOGP, 4, LOGP, true, false>(v, ts, tg, ps);
 #pragma unroll
@@ -921,7 +941,7 @@ __global__ void __launch_bounds__(NSEG *(1 << LOGP) / 16)
         for (int k = 0; k < 16; ++k) v[k] = lds[lstride(k)];
         buf = 1;
         if (ps.fp) {
-            ntt_round_r<LOGP, 0, 4, true, true>(v, ts, tg, ps);
+            ntt_round_r<LOGP, 0, 4, true, true, ConstTw, true>(v, ts, ctg, ps);
 #pragma unroll
             for (int k = 0; k < 16; ++k) {
                 const double c = fp_mulmod(__longlong_as_double((long long)v[k]), ps.ninv_d, ps.qd, ps.qinv);
@@ -930,7 +950,7 @@ __global__ void __launch_bounds__(NSEG *(1 << LOGP) / 16)
                 if constexpr (FAN::kSrcDouble) d[k] = (u64)__double_as_longlong(u2d(d[k]));
             }
         } else {
-            ntt_round_r<LOGP, 0, 4, true, false>(v, ts, tg, ps);
+            ntt_round_r<LOGP, 0, 4, true, false, ConstTw, true>(v, ts, ctg, ps);
 #pragma unroll
             for (int k = 0; k < 16; ++k) d[k] = shoup(v[k], ps.ninv, ps.ninv_q, ps.q);
         }
@@ -949,18 +969,19 @@ __global__ void __launch_bounds__(NSEG *(1 << LOGP) / 16)
     for (int t = t0; t < t1; ++t) {
         const auto tgt = fan.tgt(blockIdx.y, t);
         if (!tgt.valid) continue;
-        const DevPrime pt = primes[tgt.prime];
+        const DevPrime pt = cprime(primes, tgt.prime);
         const GlobalTw<decltype(twidx)> tw{twidx, fwd.a + ((u64)tgt.prime << logN), fwd.fa + ((u64)tgt.prime << logN)};
+        const ConstTw ctw{fwd.a + ((u64)tgt.prime << logN), fwd.fa + ((u64)tgt.prime << logN)};
         u64 *tile = lds + (DB ? buf * TILE : 0);
         buf ^= 1;
         if (!DB) __syncthreads();  // the previous exchange's reads are done
         u64 v[16];
         if (pt.fp) {
             fan.xf16(tgt, true, d, lo, v, FAN::kSrcDouble && ps.fp);
-            ntt_round_r<LOGP, 0, 4, false, true>(v, ts, tw, pt);
+            ntt_round_r<LOGP, 0, 4, false, true, ConstTw, true>(v, ts, ctw, pt);
         } else {
             fan.xf16(tgt, false, d, lo, v, FAN::kSrcDouble && ps.fp);
-            ntt_round_r<LOGP, 0, 4, false, false>(v, ts, tw, pt);
+            ntt_round_r<LOGP, 0, 4, false, false, ConstTw, true>(v, ts, ctw, pt);
         }
 #pragma unroll
         for (int k = 0; k < 16; ++k) tile[lstride(k)] = v[k];
