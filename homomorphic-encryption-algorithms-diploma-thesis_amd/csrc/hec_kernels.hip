@@ -1722,9 +1722,11 @@ __device__ __forceinline__ void bmac_body(u64 *lds, u64 *ltw, PolyArr T, const u
                 lds[(li / P) * LD + (li % P) + 1 + (((li % P) + 1) >> 4)] = v1;
             }
         }
-        if (J + 1 < l) load_tile(J + 1);
+        // the key words of digit J before the prefetch of tile J + 1: vector loads complete in issue order (one
+        // vmcnt), so the MAC's wait for its keys does not also wait for the next tile
         u64 k0[EPT], k1[EPT];
         load_keys(J, k0, k1);  // before the rounds: their latency hides behind the LDS work
+        if (J + 1 < l) load_tile(J + 1);
         __syncthreads();
         u64 v[EPT];
         if (ntt) {
