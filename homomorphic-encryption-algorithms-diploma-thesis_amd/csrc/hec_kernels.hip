@@ -340,6 +340,21 @@ __device__ __forceinline__ void ntt_round_g(u64 *lds, const AddrF &addr, int ts,
     }
 }
 
+// round 0 (stages [0, 4), one group per thread) with its twiddles already loaded (gt)
+template <int LOGP, bool INV, bool FP, class AddrF>
+__device__ __forceinline__ void ntt_round0_pre(u64 *lds, const AddrF &addr, int ts, const GroupTw<0, 4, FP> &gt,
+                                               const DevPrime &pr)
+{
+    const int lo = ts & ((1 << (LOGP - 4)) - 1), hi = ts >> (LOGP - 4);
+    const int xb = (hi << LOGP) | lo;
+    u64 v[16];
+#pragma unroll
+    for (int a = 0; a < 16; ++a) v[a] = lds[addr(xb | (a << (LOGP - 4)))];
+    gt.template run<INV>(v, pr);
+#pragma unroll
+    for (int a = 0; a < 16; ++a) lds[addr(xb | (a << (LOGP - 4)))] = v[a];
+}
+
 // the two-pass NTT's rounds: 16 elements per thread, stages [4 RND, min(4 RND + 4, LOGP))
 template <int LOGP, int RND, bool INV, bool FP, class AddrF, class TwF>
 __device__ __forceinline__ void ntt_round(u64 *lds, const AddrF &addr, int ts, const TwF &twidx, const ulonglong2 *tw,
@@ -378,6 +393,21 @@ __device__ __forceinline__ void ntt_pass_body(u64 *lds, const Bound &bio, const 
     }
     __syncthreads();
 
+    const int ts = threadIdx.x / NSEG, sg = threadIdx.x % NSEG;
+    // pass A: SEAL table index 2^s + i (shared by all columns: broadcast reads).
+    // pass B: the per-chunk index (R + r) 2^s + i is served from the re-laid table
+    //         twb[s][i][r] = tw[(R + r) 2^s + i] at R (2^s - 1) + i R + r, so lanes (consecutive
+    //         chunks r) read consecutive entries.
+    const u64 R = 1ull << (logN - LOGP), chunk = (u64)(seg0 + sg);
+    auto twidx = [=](int s, int i) -> u64 {
+        if constexpr (PASS_A) return (1ull << s) + (u64)i;
+        else return R * ((1ull << s) - 1) + (u64)i * R + chunk;
+    };
+    // a forward final pass loads round 0's twiddles before the post-op operands: vector loads complete in issue
+    // order (one vmcnt), so round 0 then waits for its twiddles only and the operands arrive under its work
+    constexpr bool TW0 = FINAL && !INV;
+    GroupTw<0, 4, FP> gt0;
+    if constexpr (TW0) gt0.load(ts >> (LOGP - 4), GlobalTw<decltype(twidx)>{twidx, tw, twf});
     // post-op operands of this thread's output words: issue their loads now so they overlap the rounds
     constexpr int ITS = P * NSEG / THREADS;
     // (loading them at the store instead frees 64+ VGPRs but measured slower: 1313 vs 1271 ms/step)
@@ -392,19 +422,10 @@ __device__ __forceinline__ void ntt_pass_body(u64 *lds, const Bound &bio, const 
             pre[it] = bio.pre(g);
         }
     }
-    const int ts = threadIdx.x / NSEG, sg = threadIdx.x % NSEG;
     auto addr = [sg](int x) { return PASS_A ? x * LD + sg : sg * LD + x; };
-    // pass A: SEAL table index 2^s + i (shared by all columns: broadcast reads).
-    // pass B: the per-chunk index (R + r) 2^s + i is served from the re-laid table
-    //         twb[s][i][r] = tw[(R + r) 2^s + i] at R (2^s - 1) + i R + r, so lanes (consecutive
-    //         chunks r) read consecutive entries.
-    const u64 R = 1ull << (logN - LOGP), chunk = (u64)(seg0 + sg);
-    auto twidx = [=](int s, int i) -> u64 {
-        if constexpr (PASS_A) return (1ull << s) + (u64)i;
-        else return R * ((1ull << s) - 1) + (u64)i * R + chunk;
-    };
     if constexpr (!INV) {
-        ntt_round<LOGP, 0, false, FP>(lds, addr, ts, twidx, tw, twf, pr);
+        if constexpr (TW0) ntt_round0_pre<LOGP, false, FP>(lds, addr, ts, gt0, pr);
+        else ntt_round<LOGP, 0, false, FP>(lds, addr, ts, twidx, tw, twf, pr);
         __syncthreads();
         ntt_round<LOGP, 1, false, FP>(lds, addr, ts, twidx, tw, twf, pr);
     } else {
@@ -2055,14 +2076,18 @@ void tensor_acc(Ctx &c, PolyArr R, const u64 *A, u64 a_sk, PolyArr ACC, int B, i
 // accumulators, so a wave has BG rotated-input loads in flight per diagonal and the diagonals are re-read
 // B / BG times (from L2) instead of B times.  Products are reduced as SEAL reduces them; sums are exact
 // (FP64: |sum| < 12 x 0.53 q; 60-bit primes: 128-bit sums of < 2^120 products) and canonicalised once.
-template <bool PT, int BG>
-__global__ void __launch_bounds__(256)
+// A block is 64 coefficients x TG batch groups, one wave per group (round 4): the TG waves read the same diagonal
+// words, so TG - 1 of every TG reads of them hit the CU's L1 and the diagonals leave HBM / L2 B / (BG TG) times
+// per pass, while consecutive blocks still stream consecutive coefficients of the same batch entries.
+template <bool PT, int BG, int TG>
+__global__ void __launch_bounds__(64 * TG)
     k_tensor_multi2(TensorBatch tb, u64 r_sb, u64 r_sk, u64 a_sk, PolyArr ACC, int B, int logN, u64 total, int assign,
                     const DevPrime *__restrict__ primes)
 {
-    const u64 idx = (u64)blockIdx.x * 256 + threadIdx.x;
+    const u64 idx = (u64)blockIdx.x * 64 + (threadIdx.x & 63);
     if (idx >= total) return;
-    const int b0 = blockIdx.y * BG;
+    const int b0 = (blockIdx.y * TG + (int)(threadIdx.x >> 6)) * BG;
+    if (b0 >= B) return;  // wave-uniform
     const int nb = min(BG, B - b0);
     const DevPrime pr = primes[idx >> logN];
     u64 d0[BG], d1[BG], d2[BG];
@@ -2135,15 +2160,16 @@ void tensor_multi(Ctx &c, const TensorBatch &tb, u64 r_sb, u64 r_sk, u64 a_sk, P
                   bool plain)
 {
     const u64 total = (u64)l * c.N;
-    const unsigned grid = (unsigned)((total + 255) / 256);
     constexpr int BG = 2;  // batch entries per thread (round 3, r03t: 533 vs 578 ms per step for 4, 577 for 8)
-    const dim3 g2(grid, (unsigned)((B + BG - 1) / BG));
+    constexpr int TG = 4;  // batch groups (waves) per block sharing the diagonal words through L1
+    const unsigned ng = (unsigned)((B + BG - 1) / BG);
+    const dim3 g2((unsigned)((total + 63) / 64), (ng + TG - 1) / TG);
     if (plain)
-        k_tensor_multi2<true, BG><<<g2, 256, 0, c.stream>>>(tb, r_sb, r_sk, a_sk, ACC, B, c.logN, total, assign ? 1 : 0,
-                                                           c.primes);
+        k_tensor_multi2<true, BG, TG><<<g2, 64 * TG, 0, c.stream>>>(tb, r_sb, r_sk, a_sk, ACC, B, c.logN, total,
+                                                                   assign ? 1 : 0, c.primes);
     else
-        k_tensor_multi2<false, BG><<<g2, 256, 0, c.stream>>>(tb, r_sb, r_sk, a_sk, ACC, B, c.logN, total,
-                                                            assign ? 1 : 0, c.primes);
+        k_tensor_multi2<false, BG, TG><<<g2, 64 * TG, 0, c.stream>>>(tb, r_sb, r_sk, a_sk, ACC, B, c.logN, total,
+                                                                    assign ? 1 : 0, c.primes);
     HEC_HIP(hipGetLastError());
 }
 
