@@ -54,11 +54,11 @@ def algorithmic_bytes_per_matvec(N, l, n, B, ks):
 
 def pmc_traffic(kernel, B, logn, level, n, variant="ctct"):
     """HBM bytes per launch of the roofline kernel from the committed rocprofv3 PMC passes
-    (profiles/r03_pmc_<kernel>_B<B>[_ctpt].json, else r02_ / r01_; written by tools/pmc_summary.py: FETCH_SIZE and
+    (profiles/r04_pmc_<kernel>_B<B>[_ctpt].json, else r03_ / r02_ / r01_; written by tools/pmc_summary.py: FETCH_SIZE and
     WRITE_SIZE in separate passes, gfx950 FETCH x2 correction for 16-B/lane reads) when they were taken on this
     configuration and matvec variant; else None."""
     sfx = "" if variant == "ctct" else f"_{variant}"
-    for tag in ("r03", "r02", "r01"):  # the newest round's pass for this kernel
+    for tag in ("r04", "r03", "r02", "r01"):  # the newest round's pass for this kernel
         path = os.path.join(ROOT, "profiles", f"{tag}_pmc_{kernel}_B{B}{sfx}.json")
         if os.path.exists(path):
             break

@@ -20,6 +20,29 @@
 namespace hec {
 
 // =============================================================================== NTT IO ====
+// 16-B accesses of the word pair (g, g + 1), g even, p 16-B aligned (engine buffers; StridedIO checks a caller's)
+typedef u64 u64x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ ulonglong2 ld2(const u64 *p, u64 g)
+{
+    const u64x2 w = *reinterpret_cast<const u64x2 *>(p + g);
+    return make_ulonglong2(w.x, w.y);
+}
+__device__ __forceinline__ void st2(u64 *p, u64 g, u64 a, u64 b)
+{
+    u64x2 w;
+    w.x = a;
+    w.y = b;
+    *reinterpret_cast<u64x2 *>(p + g) = w;
+}
+// the pair (g, g + 1) read through the Galois permutation: galois_src(g + 1) = galois_src(g) ^ 1 (hec_device.h)
+__device__ __forceinline__ ulonglong2 ld2_galois(const u64 *p, u64 g, u32 elt, int logN)
+{
+    if (elt == 1) return ld2(p, g);
+    const u32 s0 = galois_src((u32)g, elt, logN);
+    const ulonglong2 w = ld2(p, s0 & ~1u);
+    return (s0 & 1) ? make_ulonglong2(w.y, w.x) : w;
+}
+
 // job -> (poly = job / nl, limb = job % nl); src/dst may alias (in place).  elt != 1 loads through the
 // Galois permutation (apply_galois_ntt fused into the load: src[galois_src(g)]).
 struct StridedIO {
@@ -28,6 +51,7 @@ struct StridedIO {
     u64 ps_src, ps_dst;
     int nl, logN;
     u32 elt;
+    int a16;  // src, dst and the strides 16-B aligned (set on the host): pass B moves 16-B pairs
     int pmap[HEC_MAXL + 1];
     struct Bound {
         const u64 *s;
@@ -35,17 +59,29 @@ struct StridedIO {
         int prime;
         u32 elt;
         int logN;
+        bool a16;
         bool valid = true;
         struct Pre {};
         __device__ Pre pre(u64) const { return {}; }
         __device__ u64 load(u64 g) const { return s[elt == 1 ? g : galois_src((u32)g, elt, logN)]; }
         __device__ void store(u64 g, u64 v, Pre) const { d[g] = v; }
+        __device__ ulonglong2 load2(u64 g) const
+        {
+            if (a16) return ld2_galois(s, g, elt, logN);
+            return make_ulonglong2(load(g), load(g + 1));
+        }
+        __device__ void pre2(u64, Pre &, Pre &) const {}
+        __device__ void store2(u64 g, u64 a, u64 b, Pre, Pre) const
+        {
+            if (a16) st2(d, g, a, b);
+            else { d[g] = a; d[g + 1] = b; }
+        }
     };
     __device__ Bound bind(int job) const
     {
         const int poly = job / nl, limb = job % nl;
         return Bound{src + (u64)poly * ps_src + ((u64)limb << logN), dst + (u64)poly * ps_dst + ((u64)limb << logN),
-                     pmap[limb], elt, logN};
+                     pmap[limb], elt, logN, a16 != 0};
     }
 };
 
@@ -115,6 +151,9 @@ struct ModUpIO_B {
         __device__ Pre pre(u64) const { return {}; }
         __device__ u64 load(u64 g) const { return p[g]; }
         __device__ void store(u64 g, u64 v, Pre) const { p[g] = v; }
+        __device__ ulonglong2 load2(u64 g) const { return ld2(p, g); }
+        __device__ void pre2(u64, Pre &, Pre &) const {}
+        __device__ void store2(u64 g, u64 a, u64 b, Pre, Pre) const { st2(p, g, a, b); }
     };
     __device__ Bound bind(int job) const
     {
@@ -190,19 +229,34 @@ struct DivRoundIO_B {
             return Pre{x[g], in ? in[elt == 1 ? g : galois_src((u32)g, elt, logN)] : 0};
         }
         __device__ u64 load(u64 g) const { return z[g]; }
-        __device__ void store(u64 g, u64 v, Pre p) const
+        __device__ void store(u64 g, u64 v, Pre p) const { out[g] = post(v, p); }
+        __device__ u64 post(u64 v, Pre p) const
         {
             u64 r = shoup(p.x + q - v, w, wq, q);
             if (in) r = addmod(r, p.in, q);
-            out[g] = r;
+            return r;
         }
+        __device__ ulonglong2 load2(u64 g) const { return ld2(z, g); }
+        __device__ void pre2(u64 g, Pre &a, Pre &b) const
+        {
+            const ulonglong2 xv = ld2(x, g);
+            const ulonglong2 iv = in ? ld2_galois(in, g, elt, logN) : make_ulonglong2(0, 0);
+            a = Pre{xv.x, iv.x};
+            b = Pre{xv.y, iv.y};
+        }
+        __device__ void store2(u64 g, u64 a, u64 b, Pre pa, Pre pb) const { st2(out, g, post(a, pa), post(b, pb)); }
         // v: the FP64 NTT output before canonicalisation (|v| < 10 q): (x - v) P^-1 (+ in) with one exact
         // fp_mulmod (|x - v| < 11 q) and one canonicalisation, instead of Shoup on u64 plus fp_canon
-        __device__ void store_fp(u64 g, double v, Pre p, const DevPrime &pr) const
+        __device__ void store_fp(u64 g, double v, Pre p, const DevPrime &pr) const { out[g] = post_fp(v, p, pr); }
+        __device__ u64 post_fp(double v, Pre p, const DevPrime &pr) const
         {
             double r = fp_mulmod(u2d(p.x) - v, u2d(w), pr.qd, pr.qinv);
             if (in) r += u2d(p.in);
-            out[g] = fp_canon(r, pr.qd, pr.qinv);
+            return fp_canon(r, pr.qd, pr.qinv);
+        }
+        __device__ void store_fp2(u64 g, double a, double b, Pre pa, Pre pb, const DevPrime &pr) const
+        {
+            st2(out, g, post_fp(a, pa, pr), post_fp(b, pb, pr));
         }
     };
     __device__ Bound bind(int job) const
@@ -340,19 +394,25 @@ __device__ __forceinline__ void ntt_round_g(u64 *lds, const AddrF &addr, int ts,
     }
 }
 
-// round 0 (stages [0, 4), one group per thread) with its twiddles already loaded (gt)
-template <int LOGP, bool INV, bool FP, class AddrF>
-__device__ __forceinline__ void ntt_round0_pre(u64 *lds, const AddrF &addr, int ts, const GroupTw<0, 4, FP> &gt,
-                                               const DevPrime &pr)
+// a round of the 16-element LDS pass (stages [S0, S1)) with its groups' twiddles already loaded: gts[gi] is group
+// gi's GroupTw (ntt_round_g's groups: g = ts G + gi)
+template <int LOGP, int S0, int S1, bool INV, bool FP, class AddrF>
+__device__ __forceinline__ void ntt_round_pre(u64 *lds, const AddrF &addr, int ts, const GroupTw<S0, S1 - S0, FP> *gts,
+                                              const DevPrime &pr)
 {
-    const int lo = ts & ((1 << (LOGP - 4)) - 1), hi = ts >> (LOGP - 4);
-    const int xb = (hi << LOGP) | lo;
-    u64 v[16];
+    constexpr int D = S1 - S0, G = 1 << (4 - D), NQ = 1 << D;
 #pragma unroll
-    for (int a = 0; a < 16; ++a) v[a] = lds[addr(xb | (a << (LOGP - 4)))];
-    gt.template run<INV>(v, pr);
+    for (int gi = 0; gi < G; ++gi) {
+        const int g = ts * G + gi;
+        const int lo = g & ((1 << (LOGP - S1)) - 1), hi = g >> (LOGP - S1);
+        const int xb = (hi << (LOGP - S0)) | lo;
+        u64 v[NQ];
 #pragma unroll
-    for (int a = 0; a < 16; ++a) lds[addr(xb | (a << (LOGP - 4)))] = v[a];
+        for (int a = 0; a < NQ; ++a) v[a] = lds[addr(xb | (a << (LOGP - S1)))];
+        gts[gi].template run<INV>(v, pr);
+#pragma unroll
+        for (int a = 0; a < NQ; ++a) lds[addr(xb | (a << (LOGP - S1)))] = v[a];
+    }
 }
 
 // the two-pass NTT's rounds: 16 elements per thread, stages [4 RND, min(4 RND + 4, LOGP))
@@ -380,16 +440,32 @@ __device__ __forceinline__ void ntt_pass_body(u64 *lds, const Bound &bio, const 
     const ulonglong2 *tw = (PASS_A ? tt.a : tt.b) + ((u64)bio.prime << logN);
     const double *twf = (PASS_A ? tt.fa : tt.fb) + ((u64)bio.prime << logN);
 
+    // pass B moves word pairs (x, x + 1) of a chunk per lane: 16-B loads and stores (8 per thread instead of 16
+    // 8-B ones; the IO's load2 / pre2 / store2)
+    constexpr int PB2 = P / 2;
+    if constexpr (PASS_A) {
 #pragma unroll
-    for (int it = 0; it < P * NSEG / THREADS; ++it) {
-        const int li = threadIdx.x + it * THREADS;
-        int x, sg;
-        u64 g;
-        if constexpr (PASS_A) { x = li / NSEG; sg = li % NSEG; g = ((u64)x << lc) + seg0 + sg; }
-        else { sg = li / P; x = li % P; g = ((u64)(seg0 + sg) << LOGP) + x; }
-        u64 v = bio.load(g);
-        if constexpr (FP && FIRST) v = (u64)__double_as_longlong(u2d(v));  // integer input -> double bits
-        lds[PASS_A ? x * LD + sg : sg * LD + x] = v;
+        for (int it = 0; it < P * NSEG / THREADS; ++it) {
+            const int li = threadIdx.x + it * THREADS;
+            const int x = li / NSEG, sg = li % NSEG;
+            u64 v = bio.load(((u64)x << lc) + seg0 + sg);
+            if constexpr (FP && FIRST) v = (u64)__double_as_longlong(u2d(v));  // integer input -> double bits
+            lds[x * LD + sg] = v;
+        }
+    } else {
+#pragma unroll
+        for (int it = 0; it < P * NSEG / THREADS / 2; ++it) {
+            const int li = threadIdx.x + it * THREADS;
+            const int sg = li / PB2, x = 2 * (li % PB2);
+            const ulonglong2 w = bio.load2(((u64)(seg0 + sg) << LOGP) + x);
+            u64 a = w.x, b = w.y;
+            if constexpr (FP && FIRST) {
+                a = (u64)__double_as_longlong(u2d(a));
+                b = (u64)__double_as_longlong(u2d(b));
+            }
+            lds[sg * LD + x] = a;
+            lds[sg * LD + x + 1] = b;
+        }
     }
     __syncthreads();
 
@@ -403,31 +479,45 @@ __device__ __forceinline__ void ntt_pass_body(u64 *lds, const Bound &bio, const 
         if constexpr (PASS_A) return (1ull << s) + (u64)i;
         else return R * ((1ull << s) - 1) + (u64)i * R + chunk;
     };
-    // a forward final pass loads round 0's twiddles before the post-op operands: vector loads complete in issue
-    // order (one vmcnt), so round 0 then waits for its twiddles only and the operands arrive under its work
-    constexpr bool TW0 = FINAL && !INV;
-    GroupTw<0, 4, FP> gt0;
-    if constexpr (TW0) gt0.load(ts >> (LOGP - 4), GlobalTw<decltype(twidx)>{twidx, tw, twf});
+    // a forward final pass loads round 0's twiddles (and at FP64 primes round 1's too) before the post-op operands:
+    // vector loads complete in issue order (one vmcnt), so the rounds wait for their twiddles only and the operands
+    // arrive under their work (the integer class keeps round 1's loads in the round: 56 more VGPRs would cost a wave)
+    constexpr bool TW0 = FINAL && !INV, TW1 = TW0 && FP;
+    constexpr int S1R = LOGP < 8 ? LOGP : 8, D1 = S1R - 4, G1 = 1 << (4 - D1);
+    const GlobalTw<decltype(twidx)> gtw{twidx, tw, twf};
+    GroupTw<0, 4, FP> gt0[1];
+    GroupTw<4, D1, FP> gt1[TW1 ? G1 : 1];
+    if constexpr (TW0) gt0[0].load(ts >> (LOGP - 4), gtw);
+    if constexpr (TW1) {
+#pragma unroll
+        for (int gi = 0; gi < G1; ++gi) gt1[gi].load((ts * G1 + gi) >> (LOGP - S1R), gtw);
+    }
     // post-op operands of this thread's output words: issue their loads now so they overlap the rounds
     constexpr int ITS = P * NSEG / THREADS;
     // (loading them at the store instead frees 64+ VGPRs but measured slower: 1313 vs 1271 ms/step)
     typename Bound::Pre pre[FINAL ? ITS : 1];
     if constexpr (FINAL) {
+        if constexpr (PASS_A) {
 #pragma unroll
-        for (int it = 0; it < ITS; ++it) {
-            const int li = threadIdx.x + it * THREADS;
-            u64 g;
-            if constexpr (PASS_A) g = ((u64)(li / NSEG) << lc) + seg0 + li % NSEG;
-            else g = ((u64)(seg0 + li / P) << LOGP) + li % P;
-            pre[it] = bio.pre(g);
+            for (int it = 0; it < ITS; ++it) {
+                const int li = threadIdx.x + it * THREADS;
+                pre[it] = bio.pre(((u64)(li / NSEG) << lc) + seg0 + li % NSEG);
+            }
+        } else {
+#pragma unroll
+            for (int it = 0; it < ITS / 2; ++it) {
+                const int li = threadIdx.x + it * THREADS;
+                bio.pre2(((u64)(seg0 + li / PB2) << LOGP) + 2 * (li % PB2), pre[2 * it], pre[2 * it + 1]);
+            }
         }
     }
     auto addr = [sg](int x) { return PASS_A ? x * LD + sg : sg * LD + x; };
     if constexpr (!INV) {
-        if constexpr (TW0) ntt_round0_pre<LOGP, false, FP>(lds, addr, ts, gt0, pr);
+        if constexpr (TW0) ntt_round_pre<LOGP, 0, 4, false, FP>(lds, addr, ts, gt0, pr);
         else ntt_round<LOGP, 0, false, FP>(lds, addr, ts, twidx, tw, twf, pr);
         __syncthreads();
-        ntt_round<LOGP, 1, false, FP>(lds, addr, ts, twidx, tw, twf, pr);
+        if constexpr (TW1) ntt_round_pre<LOGP, 4, S1R, false, FP>(lds, addr, ts, gt1, pr);
+        else ntt_round<LOGP, 1, false, FP>(lds, addr, ts, twidx, tw, twf, pr);
     } else {
         ntt_round<LOGP, 1, true, FP>(lds, addr, ts, twidx, tw, twf, pr);
         __syncthreads();
@@ -435,19 +525,48 @@ __device__ __forceinline__ void ntt_pass_body(u64 *lds, const Bound &bio, const 
     }
     __syncthreads();
 
+    if constexpr (!PASS_A) {
+#pragma unroll
+        for (int it = 0; it < ITS / 2; ++it) {
+            const int li = threadIdx.x + it * THREADS;
+            const int s2 = li / PB2, x = 2 * (li % PB2);
+            u64 a = lds[s2 * LD + x], b = lds[s2 * LD + x + 1];
+            const u64 g = ((u64)(seg0 + s2) << LOGP) + x;
+            if constexpr (FINAL) {
+                if constexpr (FP) {
+                    double da = __longlong_as_double((long long)a), db = __longlong_as_double((long long)b);
+                    if constexpr (INV) {
+                        da = fp_mulmod(da, pr.ninv_d, pr.qd, pr.qinv);
+                        db = fp_mulmod(db, pr.ninv_d, pr.qd, pr.qinv);
+                    }
+                    if constexpr (HasFpStore<Bound>::value) {
+                        if (bio.fpstore) {
+                            bio.store_fp2(g, da, db, pre[2 * it], pre[2 * it + 1], pr);
+                            continue;
+                        }
+                    }
+                    a = fp_canon(da, pr.qd, pr.qinv);
+                    b = fp_canon(db, pr.qd, pr.qinv);
+                } else if constexpr (!INV) {
+                    a = csub(csub(a, two_q), q);
+                    b = csub(csub(b, two_q), q);
+                } else {
+                    a = shoup(a, pr.ninv, pr.ninv_q, q);
+                    b = shoup(b, pr.ninv, pr.ninv_q, q);
+                }
+                bio.store2(g, a, b, pre[2 * it], pre[2 * it + 1]);
+            } else {
+                bio.store2(g, a, b, typename Bound::Pre{}, typename Bound::Pre{});
+            }
+        }
+        return;
+    }
 #pragma unroll
     for (int it = 0; it < P * NSEG / THREADS; ++it) {
         const int li = threadIdx.x + it * THREADS;
-        u64 v, g;
-        if constexpr (PASS_A) {
-            const int x = li / NSEG, s2 = li % NSEG;
-            v = lds[x * LD + s2];
-            g = ((u64)x << lc) + seg0 + s2;
-        } else {
-            const int s2 = li / P, x = li % P;
-            v = lds[s2 * LD + x];
-            g = ((u64)(seg0 + s2) << LOGP) + x;
-        }
+        const int x = li / NSEG, s2 = li % NSEG;
+        u64 v = lds[x * LD + s2];
+        const u64 g = ((u64)x << lc) + seg0 + s2;
         if constexpr (FINAL) {
             if constexpr (FP) {
                 double d = __longlong_as_double((long long)v);
@@ -663,6 +782,7 @@ static StridedIO strided(const u64 *src, u64 *dst, u64 ps_src, u64 ps_dst, int n
 {
     StridedIO io{};
     io.src = src; io.dst = dst; io.ps_src = ps_src; io.ps_dst = ps_dst; io.nl = nl; io.logN = logN; io.elt = elt;
+    io.a16 = ((((uintptr_t)src | (uintptr_t)dst) & 15) == 0 && ((ps_src | ps_dst) & 1) == 0) ? 1 : 0;
     for (int i = 0; i < nl && i <= HEC_MAXL; ++i) io.pmap[i] = pmap[i];
     return io;
 }
@@ -877,6 +997,30 @@ struct FanDivRound {  // source (b, k) = last limb (inverse pass-B domain) -> Z[
 };
 
 // ------------------------------------------------------------------ register-direct fan-out (k_fan2)
+// the value of lane (lane ^ 1) (a quad_perm [1, 0, 3, 2] DPP move of each half)
+__device__ __forceinline__ u64 lane_xor1(u64 x)
+{
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(u32)x, 0xB1, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(u32)(x >> 32), 0xB1, 0xF, 0xF, false);
+    return ((u64)(u32)hi << 32) | (u32)lo;
+}
+
+// Store a block set (v[k] = row 16 ts + k of column sg; addr(k) its u64 index) as 16-B pieces: lanes sg and sg ^ 1
+// (adjacent columns, adjacent lanes) trade half their rows, so the even lane stores rows 2j of both columns and the
+// odd lane rows 2j + 1 -- 8 dwordx4 stores instead of 16 dwordx2 (a column-per-lane store tail is issue-bound at
+// 8 B per lane).  addr(k) of the even column must be 16-B aligned.
+template <class AddrF>
+__device__ __forceinline__ void store_block_pairs(u64 *__restrict__ out, const u64 *v, int sg, const AddrF &addr)
+{
+    const bool odd = sg & 1;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const u64 r = lane_xor1(odd ? v[2 * j] : v[2 * j + 1]);
+        const u64 lo = odd ? r : v[2 * j], hi = odd ? v[2 * j + 1] : r;
+        *reinterpret_cast<ulonglong2 *>(out + addr(2 * j + odd) - odd) = make_ulonglong2(lo, hi);
+    }
+}
+
 // The stages of one round on 16 register-resident elements: thread ts of a P = 2^LOGP point column holds the
 // elements ntt_round_g gives it for stages [S0, S1): v[gi 2^D + a] <-> x = xb(ts G + gi) | (a << (LOGP - S1)).
 // Round 0 (stages 0..3) owns x = ts + k TPS ("stride set"), round 1 (stages 4..LOGP-1) x = 16 ts + k ("block
@@ -1011,8 +1155,7 @@ __global__ void __launch_bounds__(NSEG *(1 << LOGP) / 16)
         for (int k = 0; k < 16; ++k) v[k] = tile[lblock(k)];
         if (pt.fp) ntt_round_r<LOGP, 4, LOGP, false, true>(v, ts, tw, pt);
         else ntt_round_r<LOGP, 4, LOGP, false, false>(v, ts, tw, pt);
-#pragma unroll
-        for (int k = 0; k < 16; ++k) tgt.out[gblock(k)] = v[k];
+        store_block_pairs(tgt.out, v, sg, gblock);
     }
 }
 
