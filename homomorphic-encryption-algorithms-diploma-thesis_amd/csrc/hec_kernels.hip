@@ -1009,6 +1009,21 @@ __device__ __forceinline__ u64 lane_xor1(u64 x)
 // (adjacent columns, adjacent lanes) trade half their rows, so the even lane stores rows 2j of both columns and the
 // odd lane rows 2j + 1 -- 8 dwordx4 stores instead of 16 dwordx2 (a column-per-lane store tail is issue-bound at
 // 8 B per lane).  addr(k) of the even column must be 16-B aligned.
+// The converse load: v[k] = element k of column sg from 16-B pieces (the even lane loads element 2j of both
+// columns, the odd lane element 2j + 1, and they trade)
+template <class AddrF>
+__device__ __forceinline__ void load_pairs(const u64 *__restrict__ in, u64 *v, int sg, const AddrF &addr)
+{
+    const bool odd = sg & 1;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const ulonglong2 w = ld2(in, addr(2 * j + odd) - odd);
+        const u64 r = lane_xor1(odd ? w.x : w.y);
+        v[2 * j] = odd ? r : w.x;
+        v[2 * j + 1] = odd ? w.y : r;
+    }
+}
+
 template <class AddrF>
 __device__ __forceinline__ void store_block_pairs(u64 *__restrict__ out, const u64 *v, int sg, const AddrF &addr)
 {
@@ -1089,12 +1104,10 @@ __global__ void __launch_bounds__(NSEG *(1 << LOGP) / 16)
     u64 d[16];  // canonical coefficient-form values of the source, stride set
     u32 lo[FAN::kSplit ? 16 : 1];  // kSplit: the low 30 bits (d then holds the high part as a double)
     if constexpr (FAN::kDirect) {
-#pragma unroll
-        for (int k = 0; k < 16; ++k) d[k] = src.in[gstride(k)];
+        load_pairs(src.in, d, sg, gstride);
     } else {
         u64 v[16];
-#pragma unroll
-        for (int k = 0; k < 16; ++k) v[k] = src.in[gblock(k)];
+        load_pairs(src.in, v, sg, gblock);
         const GlobalTw<decltype(twidx)> tg{twidx, inv.a + ((u64)src.prime << logN), inv.fa + ((u64)src.prime << logN)};
         const ConstTw ctg{inv.a + ((u64)src.prime << logN), inv.fa + ((u64)src.prime << logN)};
         if (ps.fp) ntt_round_r<LOGP, 4, LOGP, true, true>(v, ts, tg, ps);
