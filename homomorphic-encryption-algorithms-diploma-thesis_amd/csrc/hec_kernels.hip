@@ -61,6 +61,7 @@ struct StridedIO {
         int logN;
         bool a16;
         bool valid = true;
+        static constexpr bool kPair = true;
         struct Pre {};
         __device__ Pre pre(u64) const { return {}; }
         __device__ u64 load(u64 g) const { return s[elt == 1 ? g : galois_src((u32)g, elt, logN)]; }
@@ -147,6 +148,7 @@ struct ModUpIO_B {
         u64 *p;
         int prime;
         bool valid = true;
+        static constexpr bool kPair = true;
         struct Pre {};
         __device__ Pre pre(u64) const { return {}; }
         __device__ u64 load(u64 g) const { return p[g]; }
@@ -197,6 +199,13 @@ struct DivRoundIO_A {
         return Bound{Y + b * ysb + k * ysk, Z + ((u64)job << logN), last, half, primes[i].q, primes[i].r1, fix[i], i};
     }
 };
+// Bound types whose pass B moves word pairs (load2 / pre2 / store2; HasPair).  The divide-and-round pass B keeps
+// 8-B accesses: its pairs measured slower (2,011-2,026 vs 1,852 ms per step, round 4; the mod-up pass B gained,
+// 1,046 vs 1,088)
+template <class T, class = void>
+struct HasPair : std::false_type {};
+template <class T>
+struct HasPair<T, std::void_t<decltype(T::kPair)>> : std::bool_constant<T::kPair> {};
 // Bound types with a store_fp(g, double, Pre, prime) post-op for FP64 primes (HasFpStore)
 template <class T, class = void>
 struct HasFpStore : std::false_type {};
@@ -229,34 +238,19 @@ struct DivRoundIO_B {
             return Pre{x[g], in ? in[elt == 1 ? g : galois_src((u32)g, elt, logN)] : 0};
         }
         __device__ u64 load(u64 g) const { return z[g]; }
-        __device__ void store(u64 g, u64 v, Pre p) const { out[g] = post(v, p); }
-        __device__ u64 post(u64 v, Pre p) const
+        __device__ void store(u64 g, u64 v, Pre p) const
         {
             u64 r = shoup(p.x + q - v, w, wq, q);
             if (in) r = addmod(r, p.in, q);
-            return r;
+            out[g] = r;
         }
-        __device__ ulonglong2 load2(u64 g) const { return ld2(z, g); }
-        __device__ void pre2(u64 g, Pre &a, Pre &b) const
-        {
-            const ulonglong2 xv = ld2(x, g);
-            const ulonglong2 iv = in ? ld2_galois(in, g, elt, logN) : make_ulonglong2(0, 0);
-            a = Pre{xv.x, iv.x};
-            b = Pre{xv.y, iv.y};
-        }
-        __device__ void store2(u64 g, u64 a, u64 b, Pre pa, Pre pb) const { st2(out, g, post(a, pa), post(b, pb)); }
         // v: the FP64 NTT output before canonicalisation (|v| < 10 q): (x - v) P^-1 (+ in) with one exact
         // fp_mulmod (|x - v| < 11 q) and one canonicalisation, instead of Shoup on u64 plus fp_canon
-        __device__ void store_fp(u64 g, double v, Pre p, const DevPrime &pr) const { out[g] = post_fp(v, p, pr); }
-        __device__ u64 post_fp(double v, Pre p, const DevPrime &pr) const
+        __device__ void store_fp(u64 g, double v, Pre p, const DevPrime &pr) const
         {
             double r = fp_mulmod(u2d(p.x) - v, u2d(w), pr.qd, pr.qinv);
             if (in) r += u2d(p.in);
-            return fp_canon(r, pr.qd, pr.qinv);
-        }
-        __device__ void store_fp2(u64 g, double a, double b, Pre pa, Pre pb, const DevPrime &pr) const
-        {
-            st2(out, g, post_fp(a, pa, pr), post_fp(b, pb, pr));
+            out[g] = fp_canon(r, pr.qd, pr.qinv);
         }
     };
     __device__ Bound bind(int job) const
@@ -440,17 +434,21 @@ __device__ __forceinline__ void ntt_pass_body(u64 *lds, const Bound &bio, const 
     const ulonglong2 *tw = (PASS_A ? tt.a : tt.b) + ((u64)bio.prime << logN);
     const double *twf = (PASS_A ? tt.fa : tt.fb) + ((u64)bio.prime << logN);
 
-    // pass B moves word pairs (x, x + 1) of a chunk per lane: 16-B loads and stores (8 per thread instead of 16
-    // 8-B ones; the IO's load2 / pre2 / store2)
+    // PAIR: pass B moves word pairs (x, x + 1) of a chunk per lane: 16-B loads and stores (8 per thread instead
+    // of 16 8-B ones; the IO's load2 / pre2 / store2)
+    constexpr bool PAIR = !PASS_A && HasPair<Bound>::value;
     constexpr int PB2 = P / 2;
-    if constexpr (PASS_A) {
+    if constexpr (!PAIR) {
 #pragma unroll
         for (int it = 0; it < P * NSEG / THREADS; ++it) {
             const int li = threadIdx.x + it * THREADS;
-            const int x = li / NSEG, sg = li % NSEG;
-            u64 v = bio.load(((u64)x << lc) + seg0 + sg);
+            int x, sg;
+            u64 g;
+            if constexpr (PASS_A) { x = li / NSEG; sg = li % NSEG; g = ((u64)x << lc) + seg0 + sg; }
+            else { sg = li / P; x = li % P; g = ((u64)(seg0 + sg) << LOGP) + x; }
+            u64 v = bio.load(g);
             if constexpr (FP && FIRST) v = (u64)__double_as_longlong(u2d(v));  // integer input -> double bits
-            lds[x * LD + sg] = v;
+            lds[PASS_A ? x * LD + sg : sg * LD + x] = v;
         }
     } else {
 #pragma unroll
@@ -479,29 +477,25 @@ __device__ __forceinline__ void ntt_pass_body(u64 *lds, const Bound &bio, const 
         if constexpr (PASS_A) return (1ull << s) + (u64)i;
         else return R * ((1ull << s) - 1) + (u64)i * R + chunk;
     };
-    // a forward final pass loads round 0's twiddles (and at FP64 primes round 1's too) before the post-op operands:
-    // vector loads complete in issue order (one vmcnt), so the rounds wait for their twiddles only and the operands
-    // arrive under their work (the integer class keeps round 1's loads in the round: 56 more VGPRs would cost a wave)
-    constexpr bool TW0 = FINAL && !INV, TW1 = TW0 && FP;
-    constexpr int S1R = LOGP < 8 ? LOGP : 8, D1 = S1R - 4, G1 = 1 << (4 - D1);
-    const GlobalTw<decltype(twidx)> gtw{twidx, tw, twf};
+    // a forward final pass loads round 0's twiddles before the post-op operands: vector loads complete in issue
+    // order (one vmcnt), so round 0 then waits for its twiddles only and the operands arrive under its work
+    // (divide-and-round pass B 1,852 vs 1,886 ms per step; round 1's as well at FP64 primes measured slower, 1,890)
+    constexpr bool TW0 = FINAL && !INV;
     GroupTw<0, 4, FP> gt0[1];
-    GroupTw<4, D1, FP> gt1[TW1 ? G1 : 1];
-    if constexpr (TW0) gt0[0].load(ts >> (LOGP - 4), gtw);
-    if constexpr (TW1) {
-#pragma unroll
-        for (int gi = 0; gi < G1; ++gi) gt1[gi].load((ts * G1 + gi) >> (LOGP - S1R), gtw);
-    }
+    if constexpr (TW0) gt0[0].load(ts >> (LOGP - 4), GlobalTw<decltype(twidx)>{twidx, tw, twf});
     // post-op operands of this thread's output words: issue their loads now so they overlap the rounds
     constexpr int ITS = P * NSEG / THREADS;
     // (loading them at the store instead frees 64+ VGPRs but measured slower: 1313 vs 1271 ms/step)
     typename Bound::Pre pre[FINAL ? ITS : 1];
     if constexpr (FINAL) {
-        if constexpr (PASS_A) {
+        if constexpr (!PAIR) {
 #pragma unroll
             for (int it = 0; it < ITS; ++it) {
                 const int li = threadIdx.x + it * THREADS;
-                pre[it] = bio.pre(((u64)(li / NSEG) << lc) + seg0 + li % NSEG);
+                u64 g;
+                if constexpr (PASS_A) g = ((u64)(li / NSEG) << lc) + seg0 + li % NSEG;
+                else g = ((u64)(seg0 + li / P) << LOGP) + li % P;
+                pre[it] = bio.pre(g);
             }
         } else {
 #pragma unroll
@@ -516,8 +510,7 @@ __device__ __forceinline__ void ntt_pass_body(u64 *lds, const Bound &bio, const 
         if constexpr (TW0) ntt_round_pre<LOGP, 0, 4, false, FP>(lds, addr, ts, gt0, pr);
         else ntt_round<LOGP, 0, false, FP>(lds, addr, ts, twidx, tw, twf, pr);
         __syncthreads();
-        if constexpr (TW1) ntt_round_pre<LOGP, 4, S1R, false, FP>(lds, addr, ts, gt1, pr);
-        else ntt_round<LOGP, 1, false, FP>(lds, addr, ts, twidx, tw, twf, pr);
+        ntt_round<LOGP, 1, false, FP>(lds, addr, ts, twidx, tw, twf, pr);
     } else {
         ntt_round<LOGP, 1, true, FP>(lds, addr, ts, twidx, tw, twf, pr);
         __syncthreads();
@@ -525,7 +518,7 @@ __device__ __forceinline__ void ntt_pass_body(u64 *lds, const Bound &bio, const 
     }
     __syncthreads();
 
-    if constexpr (!PASS_A) {
+    if constexpr (PAIR) {
 #pragma unroll
         for (int it = 0; it < ITS / 2; ++it) {
             const int li = threadIdx.x + it * THREADS;
@@ -538,12 +531,6 @@ __device__ __forceinline__ void ntt_pass_body(u64 *lds, const Bound &bio, const 
                     if constexpr (INV) {
                         da = fp_mulmod(da, pr.ninv_d, pr.qd, pr.qinv);
                         db = fp_mulmod(db, pr.ninv_d, pr.qd, pr.qinv);
-                    }
-                    if constexpr (HasFpStore<Bound>::value) {
-                        if (bio.fpstore) {
-                            bio.store_fp2(g, da, db, pre[2 * it], pre[2 * it + 1], pr);
-                            continue;
-                        }
                     }
                     a = fp_canon(da, pr.qd, pr.qinv);
                     b = fp_canon(db, pr.qd, pr.qinv);
@@ -564,9 +551,16 @@ __device__ __forceinline__ void ntt_pass_body(u64 *lds, const Bound &bio, const 
 #pragma unroll
     for (int it = 0; it < P * NSEG / THREADS; ++it) {
         const int li = threadIdx.x + it * THREADS;
-        const int x = li / NSEG, s2 = li % NSEG;
-        u64 v = lds[x * LD + s2];
-        const u64 g = ((u64)x << lc) + seg0 + s2;
+        u64 v, g;
+        if constexpr (PASS_A) {
+            const int x = li / NSEG, s2 = li % NSEG;
+            v = lds[x * LD + s2];
+            g = ((u64)x << lc) + seg0 + s2;
+        } else {
+            const int s2 = li / P, x = li % P;
+            v = lds[s2 * LD + x];
+            g = ((u64)(seg0 + s2) << LOGP) + x;
+        }
         if constexpr (FINAL) {
             if constexpr (FP) {
                 double d = __longlong_as_double((long long)v);
@@ -997,45 +991,6 @@ struct FanDivRound {  // source (b, k) = last limb (inverse pass-B domain) -> Z[
 };
 
 // ------------------------------------------------------------------ register-direct fan-out (k_fan2)
-// the value of lane (lane ^ 1) (a quad_perm [1, 0, 3, 2] DPP move of each half)
-__device__ __forceinline__ u64 lane_xor1(u64 x)
-{
-    const int lo = __builtin_amdgcn_update_dpp(0, (int)(u32)x, 0xB1, 0xF, 0xF, false);
-    const int hi = __builtin_amdgcn_update_dpp(0, (int)(u32)(x >> 32), 0xB1, 0xF, 0xF, false);
-    return ((u64)(u32)hi << 32) | (u32)lo;
-}
-
-// Store a block set (v[k] = row 16 ts + k of column sg; addr(k) its u64 index) as 16-B pieces: lanes sg and sg ^ 1
-// (adjacent columns, adjacent lanes) trade half their rows, so the even lane stores rows 2j of both columns and the
-// odd lane rows 2j + 1 -- 8 dwordx4 stores instead of 16 dwordx2 (a column-per-lane store tail is issue-bound at
-// 8 B per lane).  addr(k) of the even column must be 16-B aligned.
-// The converse load: v[k] = element k of column sg from 16-B pieces (the even lane loads element 2j of both
-// columns, the odd lane element 2j + 1, and they trade)
-template <class AddrF>
-__device__ __forceinline__ void load_pairs(const u64 *__restrict__ in, u64 *v, int sg, const AddrF &addr)
-{
-    const bool odd = sg & 1;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        const ulonglong2 w = ld2(in, addr(2 * j + odd) - odd);
-        const u64 r = lane_xor1(odd ? w.x : w.y);
-        v[2 * j] = odd ? r : w.x;
-        v[2 * j + 1] = odd ? w.y : r;
-    }
-}
-
-template <class AddrF>
-__device__ __forceinline__ void store_block_pairs(u64 *__restrict__ out, const u64 *v, int sg, const AddrF &addr)
-{
-    const bool odd = sg & 1;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        const u64 r = lane_xor1(odd ? v[2 * j] : v[2 * j + 1]);
-        const u64 lo = odd ? r : v[2 * j], hi = odd ? v[2 * j + 1] : r;
-        *reinterpret_cast<ulonglong2 *>(out + addr(2 * j + odd) - odd) = make_ulonglong2(lo, hi);
-    }
-}
-
 // The stages of one round on 16 register-resident elements: thread ts of a P = 2^LOGP point column holds the
 // elements ntt_round_g gives it for stages [S0, S1): v[gi 2^D + a] <-> x = xb(ts G + gi) | (a << (LOGP - S1)).
 // Round 0 (stages 0..3) owns x = ts + k TPS ("stride set"), round 1 (stages 4..LOGP-1) x = 16 ts + k ("block
@@ -1104,10 +1059,12 @@ __global__ void __launch_bounds__(NSEG *(1 << LOGP) / 16)
     u64 d[16];  // canonical coefficient-form values of the source, stride set
     u32 lo[FAN::kSplit ? 16 : 1];  // kSplit: the low 30 bits (d then holds the high part as a double)
     if constexpr (FAN::kDirect) {
-        load_pairs(src.in, d, sg, gstride);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) d[k] = src.in[gstride(k)];
     } else {
         u64 v[16];
-        load_pairs(src.in, v, sg, gblock);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) v[k] = src.in[gblock(k)];
         const GlobalTw<decltype(twidx)> tg{twidx, inv.a + ((u64)src.prime << logN), inv.fa + ((u64)src.prime << logN)};
         const ConstTw ctg{inv.a + ((u64)src.prime << logN), inv.fa + ((u64)src.prime << logN)};
         if (ps.fp) ntt_round_r<LOGP, 4, LOGP, true, true>(v, ts, tg, ps);
@@ -1168,7 +1125,9 @@ __global__ void __launch_bounds__(NSEG *(1 << LOGP) / 16)
         for (int k = 0; k < 16; ++k) v[k] = tile[lblock(k)];
         if (pt.fp) ntt_round_r<LOGP, 4, LOGP, false, true>(v, ts, tw, pt);
         else ntt_round_r<LOGP, 4, LOGP, false, false>(v, ts, tw, pt);
-        store_block_pairs(tgt.out, v, sg, gblock);
+        // (16-B stores and loads through lane-pair trades measured slower: 2,613 vs 2,580 ms per step, round 4)
+#pragma unroll
+        for (int k = 0; k < 16; ++k) tgt.out[gblock(k)] = v[k];
     }
 }
 
@@ -2232,18 +2191,16 @@ void tensor_acc(Ctx &c, PolyArr R, const u64 *A, u64 a_sk, PolyArr ACC, int B, i
 // accumulators, so a wave has BG rotated-input loads in flight per diagonal and the diagonals are re-read
 // B / BG times (from L2) instead of B times.  Products are reduced as SEAL reduces them; sums are exact
 // (FP64: |sum| < 12 x 0.53 q; 60-bit primes: 128-bit sums of < 2^120 products) and canonicalised once.
-// A block is 64 coefficients x TG batch groups, one wave per group (round 4): the TG waves read the same diagonal
-// words, so TG - 1 of every TG reads of them hit the CU's L1 and the diagonals leave HBM / L2 B / (BG TG) times
-// per pass, while consecutive blocks still stream consecutive coefficients of the same batch entries.
-template <bool PT, int BG, int TG>
-__global__ void __launch_bounds__(64 * TG)
+// (Blocks of 4 waves on 4 batch groups sharing the diagonal words through L1 measured slower: 556 vs 522 ms per
+// step, round 4.)
+template <bool PT, int BG>
+__global__ void __launch_bounds__(256)
     k_tensor_multi2(TensorBatch tb, u64 r_sb, u64 r_sk, u64 a_sk, PolyArr ACC, int B, int logN, u64 total, int assign,
                     const DevPrime *__restrict__ primes)
 {
-    const u64 idx = (u64)blockIdx.x * 64 + (threadIdx.x & 63);
+    const u64 idx = (u64)blockIdx.x * 256 + threadIdx.x;
     if (idx >= total) return;
-    const int b0 = (blockIdx.y * TG + (int)(threadIdx.x >> 6)) * BG;
-    if (b0 >= B) return;  // wave-uniform
+    const int b0 = blockIdx.y * BG;
     const int nb = min(BG, B - b0);
     const DevPrime pr = primes[idx >> logN];
     u64 d0[BG], d1[BG], d2[BG];
@@ -2317,15 +2274,13 @@ void tensor_multi(Ctx &c, const TensorBatch &tb, u64 r_sb, u64 r_sk, u64 a_sk, P
 {
     const u64 total = (u64)l * c.N;
     constexpr int BG = 2;  // batch entries per thread (round 3, r03t: 533 vs 578 ms per step for 4, 577 for 8)
-    constexpr int TG = 4;  // batch groups (waves) per block sharing the diagonal words through L1
-    const unsigned ng = (unsigned)((B + BG - 1) / BG);
-    const dim3 g2((unsigned)((total + 63) / 64), (ng + TG - 1) / TG);
+    const dim3 g2((unsigned)((total + 255) / 256), (unsigned)((B + BG - 1) / BG));
     if (plain)
-        k_tensor_multi2<true, BG, TG><<<g2, 64 * TG, 0, c.stream>>>(tb, r_sb, r_sk, a_sk, ACC, B, c.logN, total,
-                                                                   assign ? 1 : 0, c.primes);
+        k_tensor_multi2<true, BG><<<g2, 256, 0, c.stream>>>(tb, r_sb, r_sk, a_sk, ACC, B, c.logN, total, assign ? 1 : 0,
+                                                           c.primes);
     else
-        k_tensor_multi2<false, BG, TG><<<g2, 64 * TG, 0, c.stream>>>(tb, r_sb, r_sk, a_sk, ACC, B, c.logN, total,
-                                                                    assign ? 1 : 0, c.primes);
+        k_tensor_multi2<false, BG><<<g2, 256, 0, c.stream>>>(tb, r_sb, r_sk, a_sk, ACC, B, c.logN, total,
+                                                            assign ? 1 : 0, c.primes);
     HEC_HIP(hipGetLastError());
 }
 
