@@ -20,7 +20,7 @@
 namespace hec {
 
 // =============================================================================== NTT IO ====
-// 16-B accesses of the word pair (g, g + 1), g even, p 16-B aligned (engine buffers; StridedIO checks a caller's)
+// 16-B accesses of the word pair (g, g + 1), g even, p 16-B aligned (engine buffers)
 typedef u64 u64x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ ulonglong2 ld2(const u64 *p, u64 g)
 {
@@ -34,14 +34,6 @@ __device__ __forceinline__ void st2(u64 *p, u64 g, u64 a, u64 b)
     w.y = b;
     *reinterpret_cast<u64x2 *>(p + g) = w;
 }
-// the pair (g, g + 1) read through the Galois permutation: galois_src(g + 1) = galois_src(g) ^ 1 (hec_device.h)
-__device__ __forceinline__ ulonglong2 ld2_galois(const u64 *p, u64 g, u32 elt, int logN)
-{
-    if (elt == 1) return ld2(p, g);
-    const u32 s0 = galois_src((u32)g, elt, logN);
-    const ulonglong2 w = ld2(p, s0 & ~1u);
-    return (s0 & 1) ? make_ulonglong2(w.y, w.x) : w;
-}
 
 // job -> (poly = job / nl, limb = job % nl); src/dst may alias (in place).  elt != 1 loads through the
 // Galois permutation (apply_galois_ntt fused into the load: src[galois_src(g)]).
@@ -51,7 +43,6 @@ struct StridedIO {
     u64 ps_src, ps_dst;
     int nl, logN;
     u32 elt;
-    int a16;  // src, dst and the strides 16-B aligned (set on the host): pass B moves 16-B pairs
     int pmap[HEC_MAXL + 1];
     struct Bound {
         const u64 *s;
@@ -59,30 +50,17 @@ struct StridedIO {
         int prime;
         u32 elt;
         int logN;
-        bool a16;
         bool valid = true;
-        static constexpr bool kPair = true;
         struct Pre {};
         __device__ Pre pre(u64) const { return {}; }
         __device__ u64 load(u64 g) const { return s[elt == 1 ? g : galois_src((u32)g, elt, logN)]; }
         __device__ void store(u64 g, u64 v, Pre) const { d[g] = v; }
-        __device__ ulonglong2 load2(u64 g) const
-        {
-            if (a16) return ld2_galois(s, g, elt, logN);
-            return make_ulonglong2(load(g), load(g + 1));
-        }
-        __device__ void pre2(u64, Pre &, Pre &) const {}
-        __device__ void store2(u64 g, u64 a, u64 b, Pre, Pre) const
-        {
-            if (a16) st2(d, g, a, b);
-            else { d[g] = a; d[g + 1] = b; }
-        }
     };
     __device__ Bound bind(int job) const
     {
         const int poly = job / nl, limb = job % nl;
         return Bound{src + (u64)poly * ps_src + ((u64)limb << logN), dst + (u64)poly * ps_dst + ((u64)limb << logN),
-                     pmap[limb], elt, logN, a16 != 0};
+                     pmap[limb], elt, logN};
     }
 };
 
@@ -199,9 +177,9 @@ struct DivRoundIO_A {
         return Bound{Y + b * ysb + k * ysk, Z + ((u64)job << logN), last, half, primes[i].q, primes[i].r1, fix[i], i};
     }
 };
-// Bound types whose pass B moves word pairs (load2 / pre2 / store2; HasPair).  The divide-and-round pass B keeps
-// 8-B accesses: its pairs measured slower (2,011-2,026 vs 1,852 ms per step, round 4; the mod-up pass B gained,
-// 1,046 vs 1,088)
+// Bound types whose pass B moves word pairs (load2 / pre2 / store2; HasPair).  Only the mod-up pass B (1,046-1,059
+// vs 1,088-1,095 ms per step, round 4): the divide-and-round pass B measured slower with pairs (2,011-2,026 vs
+// 1,852 ms) and so did the plain strided forward pass B (cfg2: 0.0762 vs 0.0681 ms per launch)
 template <class T, class = void>
 struct HasPair : std::false_type {};
 template <class T>
@@ -776,7 +754,6 @@ static StridedIO strided(const u64 *src, u64 *dst, u64 ps_src, u64 ps_dst, int n
 {
     StridedIO io{};
     io.src = src; io.dst = dst; io.ps_src = ps_src; io.ps_dst = ps_dst; io.nl = nl; io.logN = logN; io.elt = elt;
-    io.a16 = ((((uintptr_t)src | (uintptr_t)dst) & 15) == 0 && ((ps_src | ps_dst) & 1) == 0) ? 1 : 0;
     for (int i = 0; i < nl && i <= HEC_MAXL; ++i) io.pmap[i] = pmap[i];
     return io;
 }

@@ -99,6 +99,34 @@ def test_ntt_cfg2_golden(orc, hecdna):
     assert [sha(out[i]) for i in range(len(m))] == fx["forward_sha256"]
 
 
+def test_cfg2_device_pipeline_bitexact(orc, hecdna):
+    """bench.py --config cfg2's step on device-resident buffers (Context.ntt_device / dyadic_device: the forward NTT
+    in place, the dyadic product into a third buffer, its inverse NTT in place) equals the oracle's
+    ntt_fwd -> (a * b) mod q -> ntt_inv, limb by limb, at N = 2^15 over the 10 data primes."""
+    N, nl, npolys = 1 << 15, 10, 3
+    m = orc.Oracle.create_coeff_modulus(N, [60] + [40] * 9 + [60])
+    o = orc.Oracle(N, m)
+    ctx = hecdna.Context(N, m)
+    rng = np.random.default_rng(22)
+    a = np.stack([np.stack([rng.integers(0, q, N, dtype=np.uint64) for q in m[:nl]]) for _ in range(npolys)])
+    b = np.stack([np.stack([rng.integers(0, q, N, dtype=np.uint64) for q in m[:nl]]) for _ in range(npolys)])
+    bufs = [hecdna.DeviceBuffer(ctx, a.nbytes) for _ in range(3)]
+    bufs[0].upload(a)
+    bufs[1].upload(b)
+    ctx.ntt_device(bufs[0], nl, npolys)
+    ctx.dyadic_device(bufs[0], bufs[1], bufs[2], nl, npolys)
+    ctx.ntt_device(bufs[2], nl, npolys, inverse=True)
+    ctx.synchronize()
+    fa = bufs[0].download(a.shape)
+    out = bufs[2].download(a.shape)
+    exp_f = np.stack([np.stack([o.ntt_fwd(i, a[p, i]) for i in range(nl)]) for p in range(npolys)])
+    assert np.array_equal(fa, exp_f)
+    q = np.array(m[:nl], dtype=object).reshape(1, nl, 1)
+    prod = (exp_f.astype(object) * b.astype(object) % q).astype(np.uint64)
+    exp = np.stack([np.stack([o.ntt_inv(i, prod[p, i]) for i in range(nl)]) for p in range(npolys)])
+    assert np.array_equal(out, exp)
+
+
 def test_dyadic_multiply_cfg2(orc, hecdna):
     """BASELINE cfg2 primitive: dyadic_product_coeffmod over u64[npolys][10][2^15] (the 10 data primes of
     {60, 40 x 9, 60}) through hec_dyadic_multiply, and at a limb offset; equal to (a * b) mod q_i."""
