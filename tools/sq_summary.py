@@ -1,17 +1,22 @@
 """Summarise the two SQ-counter passes of tools/gpu_sq.sh into per-kernel totals and fractions (development tool).
 SQ_WAVE_CYCLES / SQ_WAIT_* / SQ_ACTIVE_* are in quad-cycles; the fractions divide by SQ_WAVE_CYCLES (per wave).
-usage: python tools/sq_summary.py <p1/run_counter_collection.csv> <p2/...csv> <command text> > out.json"""
+usage: [SQ_BY_INSTANCE=1] python tools/sq_summary.py <p1/run_counter_collection.csv> <p2/...csv> <command text> > out.json
+SQ_BY_INSTANCE=1: one entry per template instantiation instead of per kernel."""
 import collections
 import csv
 import json
+import os
 import sys
 
+BY_INST = os.environ.get("SQ_BY_INSTANCE") == "1"
 tot = collections.defaultdict(collections.Counter)
 disp = collections.defaultdict(set)
 for path in sys.argv[1:3]:
     for r in csv.DictReader(open(path)):
         name = r["Kernel_Name"]
         base = name[name.find("k_"):].split("<")[0].split("(")[0] if "k_" in name else name
+        if BY_INST:  # one entry per template instantiation (the IO class names the k_ntt role)
+            base = name[name.find("k_"):].split("(")[0] if "k_" in name else name
         tot[base][r["Counter_Name"]] += float(r["Counter_Value"])
         disp[base].add((path, r["Dispatch_Id"]))
 out = {"command": sys.argv[3], "kernels": {}}
