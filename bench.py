@@ -281,8 +281,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--batch", type=int, default=96,
-                    help="input vectors per GPU per step (p); the engine runs them as 3 concurrent lanes of 32")
+    ap.add_argument("--batch", type=int, default=192,
+                    help="input vectors per GPU per step (p); the engine runs them as 3 concurrent lanes of 64 "
+                         "(round 4 sweep, profiles/r04i_*, r04j_*: 10.62 matvec/s at 192 vs 10.38 at 96 and 10.64 at "
+                         "288; 384 does not fit the workspaces in 288 GB)")
     ap.add_argument("--n", type=int, default=4096, help="matrix dimension (diagonals)")
     ap.add_argument("--logn", type=int, default=15)
     ap.add_argument("--no-cpu-baseline", action="store_true")

@@ -1001,6 +1001,13 @@ void matvec_lanes(hec_context *ctx, const hec_ciphertext *const *diags, const he
     Ctx &c = ctx->c;
     const int nl = (int)std::min<std::size_t>((std::size_t)std::max(1, c.lanes), p / std::max(1, c.lane_min_batch));
     if (nl <= 1 || c.prof_mode != 0) {  // profiling: the single-stream schedule, one phase at a time
+        // a whole batch on the context's own workspace: first return the idle lanes' workspaces (at the bench's
+        // 192 vectors the lanes hold 3 x 64 vectors' worth, and the one-lane profile step needs as much again)
+        if (p > (std::size_t)std::max(1, c.lane_min_batch))
+            for (hec_context *l : ctx->lanes) {
+                HEC_HIP(hipStreamSynchronize(l->c.stream));
+                l->c.ws.release();
+            }
         matvec_core(ctx, diags, pdiags, n, js, cols, p, rk, gk, finish, out);
         return;
     }
