@@ -288,6 +288,16 @@ def test_matvec_batch_lanes_bitexact(env11):
     got2 = e.ctx.matmul_diag_col([e.up(a) for a in A], [e.up(x) for x in X[:33]], e.rk, e.gk)
     for g, c in zip(got2, exp[:33]):
         e.same(g, c)
+    # profiling runs the whole batch as one lane on the context's own workspace, after returning the idle lanes'
+    # workspaces (bench.py's profile step); the lanes then grow theirs again
+    e.ctx.profile(2)
+    got3 = e.ctx.matmul_diag_col([e.up(a) for a in A], [e.up(x) for x in X], e.rk, e.gk)
+    e.ctx.synchronize()
+    e.ctx.profile(0)
+    got4 = e.ctx.matmul_diag_col([e.up(a) for a in A], [e.up(x) for x in X], e.rk, e.gk)
+    for g3, g4, c in zip(got3, got4, exp):
+        e.same(g3, c)
+        e.same(g4, c)
 
 
 def test_lane_workspace_growth_while_lanes_run(orc, hecdna):
