@@ -302,7 +302,7 @@ def main():
                          "batched forward NTT + dyadic + inverse NTT over --batch polys x 10 limbs at N=2^15 "
                          "(limb-NTTs per second; default batch 64); cfg5: BASELINE configs[4], "
                          "the 1024x1024x1024 ct x ct matmul at N=2^16, L=16, measured as output columns per second "
-                         "(a step = --batch columns of the product; not the metric)")
+                         "(a step = --batch columns of the product, default 64; not the metric)")
     ap.add_argument("--sharded-steps", type=int, default=None,
                     help="throughput mode at N > 1: after the timed steps, also time this many row-sharded steps of "
                          "one batch (the cfg4 strong-scaling figure, reported under 'sharded'; default 1 at N > 1)")
@@ -312,9 +312,9 @@ def main():
     if args.config == "cfg5":
         args.logn, args.n = 16, 1024
         if args.batch == ap.get_default("batch"):
-            args.batch = 32
+            args.batch = 64  # 2 lanes of 32 (round 4, profiles/r04p_*: 9.93 columns/s vs 9.80 at 32, 9.92 at 48)
     if args.config == "cfg2" and args.batch == ap.get_default("batch"):
-        args.batch = 64
+        args.batch = 64  # 168 MB per buffer, inside the Infinity Cache: 3.20 M limb-NTT/s vs 2.94 M at 128 (r04p)
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # one process per GPU: start the N ranks as a child launcher before anything touches a GPU, relay its
