@@ -378,11 +378,12 @@ void moddown(Ctx &c, u64 *ACC, u64 *Z, PolyArr IN, int in_nk, PolyArr OUT, int B
 // The mod-downs of ng sibling rotations of one node at once: ACC[q] = ACC + q B 2 (l+1) N (contiguous), IN the
 // node's ciphertexts read through each child's permutation.  The P-limb INTT pass and the fan-out (small,
 // latency-bound launches) run over all ng B entries in one launch each; divide_round's pass B per child.
-void moddown_group(Ctx &c, u64 *ACC, u64 *Z, PolyArr IN, const PolyArr *OUT, const u32 *elts, int ng, int B, int l)
+void moddown_group(Ctx &c, u64 *ACC, u64 *Z, PolyArr IN, int in_nk, const PolyArr *OUT, const u32 *elts, int ng,
+                   int B, int l)
 {
     const u64 N = c.N, sacc = (u64)B * 2 * (l + 1) * N, sz = (u64)B * 2 * l * N;
     if (!c.fan_out || ng == 1) {
-        for (int q = 0; q < ng; ++q) moddown(c, ACC + q * sacc, Z, IN, 1, OUT[q], B, l, elts[q]);
+        for (int q = 0; q < ng; ++q) moddown(c, ACC + q * sacc, Z, IN, in_nk, OUT[q], B, l, elts[q]);
         return;
     }
     ProfScope ps(c, "ks_moddown");
@@ -396,9 +397,9 @@ void moddown_group(Ctx &c, u64 *ACC, u64 *Z, PolyArr IN, const PolyArr *OUT, con
         fan_divide_round(c, ACC + l * N, 2 * (l + 1) * N, (l + 1) * N, Z, B * ng, 2, l, (int)c.K - 1);
     }
     for (int q = 0; q < ng; ++q) {
-        ProfScope k(c, "k:k_ntt/divround_b", 7.0 * B * l);
+        ProfScope k(c, "k:k_ntt/divround_b", (6.0 + in_nk) * B * l);
         divide_round(c, ACC + q * sacc + l * N, 2 * (l + 1) * N, (l + 1) * N,
-                     PolyArr{ACC + q * sacc, 2 * (l + 1) * N, (l + 1) * N}, IN, 1, OUT[q], B, 2, l, (int)c.K - 1,
+                     PolyArr{ACC + q * sacc, 2 * (l + 1) * N, (l + 1) * N}, IN, in_nk, OUT[q], B, 2, l, (int)c.K - 1,
                      c.p_inv.data(), c.p_inv_q.data(), Z + q * sz, elts[q], 2);
     }
 }
@@ -728,6 +729,11 @@ void walk_trie_hoisted(Ctx &c, Scratch &s, const RotTrie &t, int node, PolyArr s
     // accumulators h.acc(q), contiguous; then the mod-downs in groups of HOIST_GROUP share their small launches
     const std::size_t grp = (std::size_t)hoisted_group(c);
     const std::size_t sup = std::max<std::size_t>(grp, HOIST_GROUP / grp * grp);
+    // the sibling-fused MAC folds the node's c0 into the children's accumulators (X0 P mod q_I), so their
+    // mod-downs take no IN term; the one-child MAC (hmac_cfg 0) does not
+    const bool fold = c.hmac_cfg != 0;
+    const PolyArr X0 = fold ? PolyArr{src.p, src.sb, src.sk} : PolyArr{};
+    const int in_nk = fold ? 0 : 1;
     for (std::size_t g0 = 0; g0 < ch.size(); g0 += sup) {
         const int ng = (int)std::min<std::size_t>(sup, ch.size() - g0);
         HChildSpec kids[HOIST_GROUP];
@@ -741,10 +747,12 @@ void walk_trie_hoisted(Ctx &c, Scratch &s, const RotTrie &t, int node, PolyArr s
             nk = std::min((int)grp, ng - q0);
             // an odd group's last three children as one 3-child launch (the digits read once, not twice)
             if (c.hmac_odd3 && grp == 2 && ng - q0 == 3) nk = 3;
-            ProfScope ps(c, "ks_hmac");  // digits E (B l^2) + c1 (B l) + per child
-            ProfScope k(c, "k:k_hmacm", (double)B * (l * l + l) + nk * (2.0 * l * K + 3.0 * K + 2.0 * B * K));
-            if (nk == 3 && grp == 2) hoisted_mac_3(c, PolyArr{src.p + src.sk, src.sb, 0}, h.E, h.zl, kids + q0, B, l);
-            else hoisted_mac_multi(c, PolyArr{src.p + src.sk, src.sb, 0}, h.E, h.zl, kids + q0, nk, B, l);
+            ProfScope ps(c, "ks_hmac");  // digits E (B l^2) + c1 (B l) [+ c0 (B l), folded] + per child
+            ProfScope k(c, "k:k_hmacm",
+                        (double)B * (l * l + l + (fold ? l : 0)) + nk * (2.0 * l * K + 3.0 * K + 2.0 * B * K));
+            if (nk == 3 && grp == 2)
+                hoisted_mac_3(c, PolyArr{src.p + src.sk, src.sb, 0}, X0, h.E, h.zl, kids + q0, B, l);
+            else hoisted_mac_multi(c, PolyArr{src.p + src.sk, src.sb, 0}, X0, h.E, h.zl, kids + q0, nk, B, l);
         }
         for (int m0 = 0; m0 < ng; m0 += HOIST_GROUP) {  // mod-downs in groups, then each child's subtree
             const int nm = std::min(HOIST_GROUP, ng - m0);
@@ -754,7 +762,7 @@ void walk_trie_hoisted(Ctx &c, Scratch &s, const RotTrie &t, int node, PolyArr s
                     before_write(dst.p);
                     const std::size_t top = s.top;
                     u64 *Z = s.take((u64)B * 2 * l * N);
-                    moddown(c, h.acc(q), Z, PolyArr{src.p, src.sb, src.sk}, 1, dst, B, l, kids[q].elt);
+                    moddown(c, h.acc(q), Z, PolyArr{src.p, src.sb, src.sk}, in_nk, dst, B, l, kids[q].elt);
                     s.top = top;
                     walk_trie_hoisted(c, s, t, ch[g0 + q], dst, depth + 1, B, l, ctx, gk, bufs, hs, stride,
                                       min_children, visit, before_write);
@@ -771,7 +779,7 @@ void walk_trie_hoisted(Ctx &c, Scratch &s, const RotTrie &t, int node, PolyArr s
             {
                 const std::size_t top = s.top;
                 u64 *Z = s.take((u64)nm * B * 2 * l * N);
-                moddown_group(c, h.acc(m0), Z, PolyArr{src.p, src.sb, src.sk}, dst, elts, nm, B, l);
+                moddown_group(c, h.acc(m0), Z, PolyArr{src.p, src.sb, src.sk}, in_nk, dst, elts, nm, B, l);
                 s.top = top;
             }
             for (int q = 0; q < nm; ++q)

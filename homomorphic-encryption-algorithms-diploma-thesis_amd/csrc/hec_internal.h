@@ -159,10 +159,10 @@ struct HChildSpec {
 constexpr int HMAC_MAX_CHILDREN = 6;  // largest hoisted_group()
 // KW[k][I] = sum_{J<l, J!=I} (q_J mod q_I) key[J][k][I] mod q_I, I in [0, l] (I == l: P), k in {0, 1}
 void key_wsum(Ctx &c, const u64 *key, u64 *KW, int l);
-void hoisted_mac_multi(Ctx &c, PolyArr X1, const u64 *E, const int *zl, const HChildSpec *kids, int nkids, int B,
-                       int l);
+void hoisted_mac_multi(Ctx &c, PolyArr X1, PolyArr X0, const u64 *E, const int *zl, const HChildSpec *kids, int nkids,
+                       int B, int l);
 // three children in one sibling-fused launch (3 x 4 FP64 / 3 x 2 integer batch entries per thread)
-void hoisted_mac_3(Ctx &c, PolyArr X1, const u64 *E, const int *zl, const HChildSpec *kids, int B, int l);
+void hoisted_mac_3(Ctx &c, PolyArr X1, PolyArr X0, const u64 *E, const int *zl, const HChildSpec *kids, int B, int l);
 int hoisted_group(const Ctx &c);  // children per hoisted_mac_multi call for c.hmac_cfg
 void fan_divide_round(Ctx &c, const u64 *Y, u64 ysb, u64 ysk, u64 *Z, int B, int nk, int nl, int last_idx);
 void galois_permute(Ctx &c, PolyArr in, PolyArr out, int B, int nk, int nl, u32 elt);

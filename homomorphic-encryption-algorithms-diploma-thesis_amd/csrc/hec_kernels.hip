@@ -190,7 +190,10 @@ struct HasFpStore : std::false_type {};
 template <class T>
 struct HasFpStore<T, std::void_t<decltype(T::kFpStore)>> : std::bool_constant<T::kFpStore> {};
 
-struct DivRoundIO_B {
+// HAS_IN = false: no IN term (the hoisted children's mod-downs, whose IN the sibling-fused MAC already folded into
+// ACC as IN P mod q_i; the post-op then holds one operand, 142 instead of 209 VGPRs: 3 waves/SIMD)
+template <bool HAS_IN>
+struct DivRoundIOB {
     u64 *Z;
     PolyArr X, IN, OUT;
     int nk, nl, logN, in_nk;  // IN is added for polys k < in_nk only
@@ -213,13 +216,14 @@ struct DivRoundIO_B {
         };
         __device__ Pre pre(u64 g) const
         {
-            return Pre{x[g], in ? in[elt == 1 ? g : galois_src((u32)g, elt, logN)] : 0};
+            if constexpr (!HAS_IN) return Pre{x[g], 0};
+            else return Pre{x[g], in ? in[elt == 1 ? g : galois_src((u32)g, elt, logN)] : 0};
         }
         __device__ u64 load(u64 g) const { return z[g]; }
         __device__ void store(u64 g, u64 v, Pre p) const
         {
             u64 r = shoup(p.x + q - v, w, wq, q);
-            if (in) r = addmod(r, p.in, q);
+            if (HAS_IN && in) r = addmod(r, p.in, q);
             out[g] = r;
         }
         // v: the FP64 NTT output before canonicalisation (|v| < 10 q): (x - v) P^-1 (+ in) with one exact
@@ -227,7 +231,7 @@ struct DivRoundIO_B {
         __device__ void store_fp(u64 g, double v, Pre p, const DevPrime &pr) const
         {
             double r = fp_mulmod(u2d(p.x) - v, u2d(w), pr.qd, pr.qinv);
-            if (in) r += u2d(p.in);
+            if (HAS_IN && in) r += u2d(p.in);
             out[g] = fp_canon(r, pr.qd, pr.qinv);
         }
     };
@@ -240,6 +244,7 @@ struct DivRoundIO_B {
                      primes[i].q, inv[i], inv_q[i], i, elt, logN, fpstore != 0};
     }
 };
+using DivRoundIO_B = DivRoundIOB<true>;
 
 // =============================================================================== NTT core ==
 // Twiddle tables per prime: integer {w, w_shoup} pairs (60-bit primes) and integer-valued doubles
@@ -784,12 +789,15 @@ void divide_round(Ctx &c, const u64 *Y, u64 ysb, u64 ysk, PolyArr X, PolyArr IN,
     a.Y = Y; a.ysb = ysb; a.ysk = ysk; a.Z = Z; a.nk = nk; a.nl = nl; a.logN = c.logN;
     a.last = c.q[last_idx]; a.half = a.last >> 1; a.primes = c.primes;
     for (int i = 0; i < nl; ++i) a.fix[i] = c.q[i] - (a.half % c.q[i]);
-    DivRoundIO_B b{};
-    b.Z = Z; b.X = X; b.IN = IN; b.OUT = OUT; b.nk = nk; b.nl = nl; b.logN = c.logN; b.in_nk = in_nk; b.elt = in_elt;
-    b.primes = c.primes;
-    b.fpstore = 1;
-    for (int i = 0; i < nl; ++i) { b.inv[i] = inv[i]; b.inv_q[i] = inv_q[i]; }
-    ntt_dispatch<false>(c, B * nk * nl, a, b, stages);
+    auto run = [&](auto b) {
+        b.Z = Z; b.X = X; b.IN = IN; b.OUT = OUT; b.nk = nk; b.nl = nl; b.logN = c.logN; b.in_nk = in_nk;
+        b.elt = in_elt; b.primes = c.primes;
+        b.fpstore = 1;
+        for (int i = 0; i < nl; ++i) { b.inv[i] = inv[i]; b.inv_q[i] = inv_q[i]; }
+        ntt_dispatch<false>(c, B * nk * nl, a, b, stages);
+    };
+    if (IN.p != nullptr && in_nk > 0) run(DivRoundIOB<true>{});
+    else run(DivRoundIOB<false>{});
 }
 
 // =============================================================== fan-out: INTT pass A -> fwd passes A ==
@@ -1342,11 +1350,15 @@ struct HChildren {
 //   ACC = sum_J key_J (E_J o gal - c_J Z_J) + W_elt KW,  KW = sum_{J != I} c_J key_J  (k_keyw, per key and level)
 // with c_J = q_J mod q_I and Z_J the (rare) zero corrections: one modular product per child and output word
 // instead of one per digit.  Every term is exact mod q_I, so the canonical result is unchanged.
+// X0.p != nullptr: the node's c0, folded into every child's c0 accumulator at the data primes as X0 (P mod q_I), so
+// the mod-down's (ACC - r) P^-1 already carries the IN term and its pass B reads one operand less (DivRoundIOB<false>).
+// The output position k of child c has source position gal_c(k) = s (hmacm's thread positions), so the term is the
+// same word X0[s] for every child.
 template <int BT, int CG, bool FP>
-__device__ __forceinline__ void hmacm_body(PolyArr X1, const u64 *__restrict__ E, const int *__restrict__ zl,
-                                           const HChildren<CG> &ch, int B, int l, int K, int logN, const DevPrime &pr,
-                                           int I, int kI, u64 s0, int b0, const u64 *__restrict__ cji,
-                                           const u64 *__restrict__ psipow)
+__device__ __forceinline__ void hmacm_body(PolyArr X1, PolyArr X0, const u64 *__restrict__ E,
+                                           const int *__restrict__ zl, const HChildren<CG> &ch, int B, int l, int K,
+                                           int logN, const DevPrime &pr, u64 Pq, int I, int kI, u64 s0, int b0,
+                                           const u64 *__restrict__ cji, const u64 *__restrict__ psipow)
 {
     const bool zeros = zl[0] != 0;
     const u64 *pp = psipow + ((u64)kI << (logN + 1));
@@ -1380,6 +1392,16 @@ __device__ __forceinline__ void hmacm_body(PolyArr X1, const u64 *__restrict__ E
             x = wk[q][2]; wk[q][2] = wk[q][3]; wk[q][3] = x;
         }
     }
+    // the folded c0 words, loaded first: their wait (for the products below) is then the oldest in issue order and
+    // does not include the digit and key prefetches issued after them
+    const bool fold = X0.p != nullptr && I < l;
+    ulonglong2 x0v[BT];
+    if (fold) {
+#pragma unroll
+        for (int t = 0; t < BT; ++t)
+            x0v[t] = b0 + t < B ? *(const ulonglong2 *)(X0.p + (b0 + t) * X0.sb + ((u64)I << logN) + s0)
+                                : ulonglong2{0, 0};
+    }
     double f[FP ? CG : 1][FP ? BT : 1][4];
     U128 a[FP ? 1 : CG][FP ? 1 : BT][4];
 #pragma unroll
@@ -1392,6 +1414,31 @@ __device__ __forceinline__ void hmacm_body(PolyArr X1, const u64 *__restrict__ E
                 if constexpr (FP) f[q][t][r] = __longlong_as_double((long long)w0);
                 else a[q][t][r] = U128{w0, 0};
             }
+    if (fold) {  // + X0 (P mod q_I) on the c0 accumulators (exact residues, as every other term)
+        const u64 pm = barrett64(Pq, pr.q, pr.r1);
+#pragma unroll
+        for (int t = 0; t < BT; ++t) {
+            if constexpr (FP) {
+                const double pmd = u2d(pm);
+                const double t0 = fp_mulmod(u2d(x0v[t].x), pmd, pr.qd, pr.qinv);
+                const double t1 = fp_mulmod(u2d(x0v[t].y), pmd, pr.qd, pr.qinv);
+#pragma unroll
+                for (int q = 0; q < CG; ++q) {
+                    f[q][t][0] += t0;
+                    f[q][t][1] += t1;
+                }
+            } else {
+                const u64 t0 = mulmod(x0v[t].x, pm, pr), t1 = mulmod(x0v[t].y, pm, pr);
+#pragma unroll
+                for (int q = 0; q < CG; ++q) {
+                    a[q][t][0].lo += t0;
+                    a[q][t][0].hi += a[q][t][0].lo < t0;
+                    a[q][t][1].lo += t1;
+                    a[q][t][1].hi += a[q][t][1].lo < t1;
+                }
+            }
+        }
+    }
     auto digit = [&](int J, int t) -> ulonglong2 {
         const int b = b0 + t;
         const u64 *src = J == I ? X1.p + b * X1.sb + ((u64)J << logN) : E + (((u64)((b * (l + 1) + I) * l + J)) << logN);
@@ -1558,9 +1605,9 @@ void key_wsum(Ctx &c, const u64 *key, u64 *KW, int l)
 // budget.  Each segment is XCD-aware: the batch groups of one (coefficient block, I) share an XCD.
 template <int BTF, int BTI, int CG, int MINW>
 __global__ void __launch_bounds__(256, MINW)  // MINW waves per SIMD: 3 -> <= 168 VGPRs, 2 -> <= 256
-    k_hmacm(PolyArr X1, const u64 *__restrict__ E, const int *__restrict__ zl, const HChildren<CG> ch, int B, int l,
-            int K, int logN, const DevPrime *__restrict__ primes, const int *__restrict__ Imap, int nI, int nint,
-            const u64 *__restrict__ cji, const u64 *__restrict__ psipow, int wsplit)
+    k_hmacm(PolyArr X1, PolyArr X0, const u64 *__restrict__ E, const int *__restrict__ zl, const HChildren<CG> ch,
+            int B, int l, int K, int logN, const DevPrime *__restrict__ primes, const int *__restrict__ Imap, int nI,
+            int nint, const u64 *__restrict__ cji, const u64 *__restrict__ psipow, int wsplit)
 {
     const u64 N = 1ull << logN;
     const int X = (int)(N / 512);
@@ -1575,15 +1622,16 @@ __global__ void __launch_bounds__(256, MINW)  // MINW waves per SIMD: 3 -> <= 16
     const int kI = I == l ? K - 1 : I;
     const DevPrime pr = primes[kI];
     const u64 s0 = (u64)xb * 512 + 2 * threadIdx.x;
+    const u64 Pq = cprime(primes, K - 1).q;
     if (!integer)
-        hmacm_body<BTF, CG, true>(X1, E, zl, ch, B, l, K, logN, pr, I, kI, s0, bg * BTF, cji, psipow);
+        hmacm_body<BTF, CG, true>(X1, X0, E, zl, ch, B, l, K, logN, pr, Pq, I, kI, s0, bg * BTF, cji, psipow);
     else
-        hmacm_body<BTI, CG, false>(X1, E, zl, ch, B, l, K, logN, pr, I, kI, s0, bg * BTI, cji, psipow);
+        hmacm_body<BTI, CG, false>(X1, X0, E, zl, ch, B, l, K, logN, pr, Pq, I, kI, s0, bg * BTI, cji, psipow);
 }
 
 template <int BTF, int BTI, int CG, int MINW = (BTF * CG <= 8 && BTI * CG <= 8) ? 3 : 2>
-static void launch_hmacm(Ctx &c, PolyArr X1, const u64 *E, const int *zl, const HChildSpec *kids, int nkids, int B,
-                         int l)
+static void launch_hmacm(Ctx &c, PolyArr X1, PolyArr X0, const u64 *E, const int *zl, const HChildSpec *kids,
+                         int nkids, int B, int l)
 {
     HChildren<CG> ch{};
     ch.n = nkids;
@@ -1592,7 +1640,7 @@ static void launch_hmacm(Ctx &c, PolyArr X1, const u64 *E, const int *zl, const 
     const int nint = c.imap_nint[l], X = (int)(c.N / 512);
     const int gI = (X * nint + 7) / 8 * 8, gF = (X * (l + 1 - nint) + 7) / 8 * 8;
     const int wsplit = gI * ((B + BTI - 1) / BTI), total = wsplit + gF * ((B + BTF - 1) / BTF);
-    k_hmacm<BTF, BTI, CG, MINW><<<dim3((unsigned)total), 256, 0, c.stream>>>(X1, E, zl, ch, B, l, (int)c.K, c.logN,
+    k_hmacm<BTF, BTI, CG, MINW><<<dim3((unsigned)total), 256, 0, c.stream>>>(X1, X0, E, zl, ch, B, l, (int)c.K, c.logN,
                                                                         c.primes, c.imap_at(l), l + 1, nint, c.cji,
                                                                         c.psipow, wsplit);
     HEC_HIP(hipGetLastError());
@@ -1600,19 +1648,20 @@ static void launch_hmacm(Ctx &c, PolyArr X1, const u64 *E, const int *zl, const 
 
 int hoisted_group(const Ctx &c) { return c.hmac_cfg ? 2 : 1; }
 
-void hoisted_mac_multi(Ctx &c, PolyArr X1, const u64 *E, const int *zl, const HChildSpec *kids, int nkids, int B,
-                       int l)
+void hoisted_mac_multi(Ctx &c, PolyArr X1, PolyArr X0, const u64 *E, const int *zl, const HChildSpec *kids, int nkids,
+                       int B, int l)
 {
     if (nkids < 1 || nkids > hoisted_group(c)) throw std::invalid_argument("hoisted_mac_multi: group size");
     // <FP64 batch entries, integer batch entries, children> per thread (the 1x4, 2x2, 3x2, 4x4 ...
     // shapes measured slower)
-    if (c.hmac_cfg) launch_hmacm<4, 2, 2>(c, X1, E, zl, kids, nkids, B, l);
+    if (c.hmac_cfg) launch_hmacm<4, 2, 2>(c, X1, X0, E, zl, kids, nkids, B, l);
+    else if (X0.p != nullptr) throw std::logic_error("hoisted_mac_multi: the one-child MAC does not fold IN");
     else hoisted_mac(c, X1, E, kids[0].W, zl, kids[0].key, kids[0].ACC, B, l, kids[0].elt);
 }
 
-void hoisted_mac_3(Ctx &c, PolyArr X1, const u64 *E, const int *zl, const HChildSpec *kids, int B, int l)
+void hoisted_mac_3(Ctx &c, PolyArr X1, PolyArr X0, const u64 *E, const int *zl, const HChildSpec *kids, int B, int l)
 {
-    launch_hmacm<4, 2, 3>(c, X1, E, zl, kids, 3, B, l);
+    launch_hmacm<4, 2, 3>(c, X1, X0, E, zl, kids, 3, B, l);
 }
 
 void fan_divide_round(Ctx &c, const u64 *Y, u64 ysb, u64 ysk, u64 *Z, int B, int nk, int nl, int last_idx)
