@@ -184,6 +184,11 @@ template <class T, class = void>
 struct HasPair : std::false_type {};
 template <class T>
 struct HasPair<T, std::void_t<decltype(T::kPair)>> : std::bool_constant<T::kPair> {};
+// Bound types whose post-op operands are loaded at the store instead of before the rounds (HasLatePre)
+template <class T, class = void>
+struct HasLatePre : std::false_type {};
+template <class T>
+struct HasLatePre<T, std::void_t<decltype(T::kLatePre)>> : std::bool_constant<T::kLatePre> {};
 // Bound types with a store_fp(g, double, Pre, prime) post-op for FP64 primes (HasFpStore)
 template <class T, class = void>
 struct HasFpStore : std::false_type {};
@@ -203,6 +208,7 @@ struct DivRoundIOB {
     u64 inv[HEC_MAXL], inv_q[HEC_MAXL];
     struct Bound {
         static constexpr bool kFpStore = true;
+        static constexpr bool kLatePre = !HAS_IN;  // the one operand is loaded at the store (4 waves/SIMD)
         const u64 *z, *x, *in;
         u64 *out;
         u64 q, w, wq;
@@ -469,8 +475,9 @@ __device__ __forceinline__ void ntt_pass_body(u64 *lds, const Bound &bio, const 
     // post-op operands of this thread's output words: issue their loads now so they overlap the rounds
     constexpr int ITS = P * NSEG / THREADS;
     // (loading them at the store instead frees 64+ VGPRs but measured slower: 1313 vs 1271 ms/step)
+    constexpr bool LATE = HasLatePre<Bound>::value;
     typename Bound::Pre pre[FINAL ? ITS : 1];
-    if constexpr (FINAL) {
+    if constexpr (FINAL && !LATE) {
         if constexpr (!PAIR) {
 #pragma unroll
             for (int it = 0; it < ITS; ++it) {
@@ -530,6 +537,14 @@ __device__ __forceinline__ void ntt_pass_body(u64 *lds, const Bound &bio, const 
             }
         }
         return;
+    }
+    if constexpr (FINAL && LATE && !PAIR) {  // the operands now, all issued before the first store
+#pragma unroll
+        for (int it = 0; it < ITS; ++it) {
+            const int li = threadIdx.x + it * THREADS;
+            if constexpr (PASS_A) pre[it] = bio.pre(((u64)(li / NSEG) << lc) + seg0 + li % NSEG);
+            else pre[it] = bio.pre(((u64)(seg0 + li / P) << LOGP) + li % P);
+        }
     }
 #pragma unroll
     for (int it = 0; it < P * NSEG / THREADS; ++it) {
