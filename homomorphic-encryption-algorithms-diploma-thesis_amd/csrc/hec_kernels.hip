@@ -196,7 +196,8 @@ template <class T>
 struct HasFpStore<T, std::void_t<decltype(T::kFpStore)>> : std::bool_constant<T::kFpStore> {};
 
 // HAS_IN = false: no IN term (the hoisted children's mod-downs, whose IN the sibling-fused MAC already folded into
-// ACC as IN P mod q_i; the post-op then holds one operand, 142 instead of 209 VGPRs: 3 waves/SIMD)
+// ACC as IN P mod q_i).  The post-op then has one operand, loaded at the store (kLatePre): 104 instead of 209 VGPRs,
+// 4 waves/SIMD (preloaded before the rounds: 142 VGPRs, 3 waves, 20-30 ms per step slower at B = 192)
 template <bool HAS_IN>
 struct DivRoundIOB {
     u64 *Z;
@@ -474,7 +475,8 @@ __device__ __forceinline__ void ntt_pass_body(u64 *lds, const Bound &bio, const 
     if constexpr (TW0) gt0[0].load(ts >> (LOGP - 4), GlobalTw<decltype(twidx)>{twidx, tw, twf});
     // post-op operands of this thread's output words: issue their loads now so they overlap the rounds
     constexpr int ITS = P * NSEG / THREADS;
-    // (loading them at the store instead frees 64+ VGPRs but measured slower: 1313 vs 1271 ms/step)
+    // (for the two-operand divide-and-round, loading them at the store instead frees 64+ VGPRs but measured slower:
+    // 1313 vs 1271 ms/step; its one-operand form without IN does load at the store, HasLatePre)
     constexpr bool LATE = HasLatePre<Bound>::value;
     typename Bound::Pre pre[FINAL ? ITS : 1];
     if constexpr (FINAL && !LATE) {
