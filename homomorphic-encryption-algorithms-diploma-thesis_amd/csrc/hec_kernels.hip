@@ -841,6 +841,7 @@ struct FanModUpT {  // source (b, J) = D[b][J] (inverse pass-B domain) -> E[b][I
     static constexpr bool kScan = !DIRECT;
     static constexpr bool kSplit = false;
     static constexpr bool kSrcDouble = !DIRECT;  // an FP64-class source stays a double (xf16's sdbl)
+    static constexpr int kJobs = 2;              // source jobs per block (k_fan2j: the next one's words prefetched)
     const u64 *D;
     u64 *E;
     int l, logN, kP;
@@ -923,6 +924,7 @@ struct FanDivRound {  // source (b, k) = last limb (inverse pass-B domain) -> Z[
     // per value and target instead of 13 mixed ones
     static constexpr bool kSplit = true;
     static constexpr bool kSrcDouble = false;
+    static constexpr int kJobs = 1;  // (2 per block: 256 VGPRs + 50 AGPRs, one wave per SIMD)
     int *zl = nullptr, *zflag = nullptr;
     const u64 *Y;
     u64 ysb, ysk;
@@ -1133,12 +1135,153 @@ __global__ void __launch_bounds__(NSEG *(1 << LOGP) / 16)
     }
 }
 
+// k_fan2 over JPB source jobs per block (FanModUpT): the next job's source words are loaded during the current
+// job's last target.  A separate kernel: folded into k_fan2, the restructured body costs the divide-and-round
+// fan-out (one job per block) 12 VGPRs and a wave.
+template <int LOGP, int NSEG, class FAN, int JPB, bool DB = true>
+__global__ void __launch_bounds__(NSEG *(1 << LOGP) / 16)
+    k_fan2j(const FAN fan, TwTables inv, TwTables fwd, const DevPrime *__restrict__ primes, int logN, int njobs)
+{
+    constexpr int P = 1 << LOGP, TPS = P / 16, LD = NSEG + 1, TILE = P * LD;
+    constexpr int S1R = LOGP, D1 = LOGP - 4, G1 = 1 << (4 - D1);
+    __shared__ u64 lds[(DB ? 2 : 1) * TILE];
+    const int seg0 = blockIdx.x * NSEG, lc = logN - LOGP;
+    const int ts = threadIdx.x / NSEG, sg = threadIdx.x % NSEG;
+    auto gstride = [&](int k) { return ((u64)(ts + k * TPS) << lc) + seg0 + sg; };
+    auto gblock = [&](int k) { return ((u64)(16 * ts + k) << lc) + seg0 + sg; };
+    auto lstride = [&](int k) { return (ts + k * TPS) * LD + sg; };
+    auto lblock = [&](int k) { return (16 * ts + k) * LD + sg; };
+    auto twidx = [](int s, int i) -> u64 { return (1ull << s) + (u64)i; };
+    // the raw source words of a job: the canonical coefficient form (direct) or the inverse pass-B domain (block set)
+    auto load_src = [&](int job, u64 *w) {
+        const auto sr = fan.src(job);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) w[k] = sr.in[FAN::kDirect ? gstride(k) : gblock(k)];
+    };
+    const int nt = fan.ntargets(), t0 = blockIdx.z * nt / gridDim.z, t1 = (blockIdx.z + 1) * nt / gridDim.z;
+    const int job0 = blockIdx.y * JPB;
+    int buf = 0;
+    u64 d[16];  // canonical coefficient-form values of the source, stride set
+    u32 lo[FAN::kSplit ? 16 : 1];  // kSplit: the low 30 bits (d then holds the high part as a double)
+    load_src(job0, d);
+    // JPB jobs per block: the next job's source words are loaded during the current job's last target (into d, dead
+    // after that target's xf16), after that target's round-1 twiddles, so no round waits for them in issue order
+    for (int jj = 0; jj < JPB; ++jj) {
+        const int job = job0 + jj;
+        if (job >= njobs) break;  // block-uniform
+        const auto src = fan.src(job);
+        const DevPrime ps = cprime(primes, src.prime);
+        if constexpr (!FAN::kDirect) {
+            u64 v[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) v[k] = d[k];
+            const GlobalTw<decltype(twidx)> tg{twidx, inv.a + ((u64)src.prime << logN), inv.fa + ((u64)src.prime << logN)};
+            const ConstTw ctg{inv.a + ((u64)src.prime << logN), inv.fa + ((u64)src.prime << logN)};
+            if (ps.fp) ntt_round_r<LOGP, 4, LOGP, true, true>(v, ts, tg, ps);
+            else ntt_round_r<LOGP, 4, LOGP, true, false>(v, ts, tg, ps);
+            u64 *tile = lds + (DB ? buf * TILE : 0);
+            if (!DB || jj > 0) __syncthreads();  // the previous job's last exchange reads are done
+#pragma unroll
+            for (int k = 0; k < 16; ++k) tile[lblock(k)] = v[k];
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < 16; ++k) v[k] = tile[lstride(k)];
+            buf ^= 1;
+            if (ps.fp) {
+                ntt_round_r<LOGP, 0, 4, true, true, ConstTw, true>(v, ts, ctg, ps);
+#pragma unroll
+                for (int k = 0; k < 16; ++k) {
+                    const double c = fp_mulmod(__longlong_as_double((long long)v[k]), ps.ninv_d, ps.qd, ps.qinv);
+                    d[k] = fp_canon(c, ps.qd, ps.qinv);
+                    // the canonical residue as an exact double (its bits; +0.0 for zero, so the zero scan is unchanged)
+                    if constexpr (FAN::kSrcDouble) d[k] = (u64)__double_as_longlong(u2d(d[k]));
+                }
+            } else {
+                ntt_round_r<LOGP, 0, 4, true, false, ConstTw, true>(v, ts, ctg, ps);
+#pragma unroll
+                for (int k = 0; k < 16; ++k) d[k] = shoup(v[k], ps.ninv, ps.ninv_q, ps.q);
+            }
+#pragma unroll
+            for (int k = 0; k < 16; ++k) d[k] = fan.src_fix(d[k]);
+            if constexpr (FAN::kSplit) FAN::split(d, lo);
+            if constexpr (FAN::kScan) {
+                if (fan.zl != nullptr && blockIdx.z == 0) {  // the canonical coefficient form's zeros (k_zscan)
+#pragma unroll
+                    for (int k = 0; k < 16; ++k)
+                        if (d[k] == 0) zero_record(fan.zl, fan.zflag, job, (int)gstride(k) & ((1 << logN) - 1));
+                }
+            }
+        }
+        int tl = -1;  // the last valid target: it loads the next job's source
+        if (jj + 1 < JPB && job + 1 < njobs)
+            for (int t = t1 - 1; t >= t0; --t)
+                if (fan.tgt(job, t).valid) {
+                    tl = t;
+                    break;
+                }
+        for (int t = t0; t < t1; ++t) {
+            const auto tgt = fan.tgt(job, t);
+            if (!tgt.valid) continue;
+            const DevPrime pt = cprime(primes, tgt.prime);
+            const GlobalTw<decltype(twidx)> tw{twidx, fwd.a + ((u64)tgt.prime << logN), fwd.fa + ((u64)tgt.prime << logN)};
+            const ConstTw ctw{fwd.a + ((u64)tgt.prime << logN), fwd.fa + ((u64)tgt.prime << logN)};
+            u64 *tile = lds + (DB ? buf * TILE : 0);
+            buf ^= 1;
+            if (!DB) __syncthreads();  // the previous exchange's reads are done
+            u64 v[16];
+            if (pt.fp) {
+                fan.xf16(tgt, true, d, lo, v, FAN::kSrcDouble && ps.fp);
+                ntt_round_r<LOGP, 0, 4, false, true, ConstTw, true>(v, ts, ctw, pt);
+            } else {
+                fan.xf16(tgt, false, d, lo, v, FAN::kSrcDouble && ps.fp);
+                ntt_round_r<LOGP, 0, 4, false, false, ConstTw, true>(v, ts, ctw, pt);
+            }
+#pragma unroll
+            for (int k = 0; k < 16; ++k) tile[lstride(k)] = v[k];
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < 16; ++k) v[k] = tile[lblock(k)];
+            if (t == tl) {  // round 1's twiddles, then the next job's source, then round 1
+                if (pt.fp) {
+                    GroupTw<4, D1, true> g1[G1];
+#pragma unroll
+                    for (int gi = 0; gi < G1; ++gi) g1[gi].load(ts * G1 + gi, tw);
+                    asm volatile("" ::: "memory");
+                    load_src(job + 1, d);
+#pragma unroll
+                    for (int gi = 0; gi < G1; ++gi) g1[gi].template run<false>(v + gi * (1 << D1), pt);
+                } else {
+                    GroupTw<4, D1, false> g1[G1];
+#pragma unroll
+                    for (int gi = 0; gi < G1; ++gi) g1[gi].load(ts * G1 + gi, tw);
+                    asm volatile("" ::: "memory");
+                    load_src(job + 1, d);
+#pragma unroll
+                    for (int gi = 0; gi < G1; ++gi) g1[gi].template run<false>(v + gi * (1 << D1), pt);
+                }
+            } else if (pt.fp) {
+                ntt_round_r<LOGP, 4, LOGP, false, true>(v, ts, tw, pt);
+            } else {
+                ntt_round_r<LOGP, 4, LOGP, false, false>(v, ts, tw, pt);
+            }
+            // (16-B stores and loads through lane-pair trades measured slower: 2,613 vs 2,580 ms per step, round 4)
+#pragma unroll
+            for (int k = 0; k < 16; ++k) tgt.out[gblock(k)] = v[k];
+        }
+    }
+}
+
 template <int LOGR, int LOGC, int NA, class FAN>
 static void run_fan(Ctx &c, int njobs, const FAN &fan, int groups)
 {
     constexpr int R = 1 << LOGR, C = 1 << LOGC;
     const TwTables fwd{c.tw, c.twb, c.twf, c.twbf}, inv{c.itw, c.itwb, c.itwf, c.itwbf};
-    k_fan2<LOGR, NA><<<dim3(C / NA, njobs, groups), NA * R / 16, 0, c.stream>>>(fan, inv, fwd, c.primes, c.logN);
+    constexpr int JPB = FAN::kJobs;
+    if constexpr (JPB > 1)
+        k_fan2j<LOGR, NA, FAN, JPB><<<dim3(C / NA, (njobs + JPB - 1) / JPB, groups), NA * R / 16, 0, c.stream>>>(
+            fan, inv, fwd, c.primes, c.logN, njobs);
+    else
+        k_fan2<LOGR, NA><<<dim3(C / NA, njobs, groups), NA * R / 16, 0, c.stream>>>(fan, inv, fwd, c.primes, c.logN);
     HEC_HIP(hipGetLastError());
 }
 template <class FAN>
