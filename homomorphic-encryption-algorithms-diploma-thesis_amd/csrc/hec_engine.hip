@@ -425,7 +425,7 @@ void keyswitch(Ctx &c, Scratch &s, PolyArr T, const u64 *key, PolyArr IN, int in
     if (c.fused_modup_mac) {  // mod-up pass A, then pass B fused with the key MAC (no E round trip)
         {
             ProfScope ps(c, "ks_modup_a");
-            ProfScope k(c, fan ? "k:k_fan2/modup" : "k:k_ntt/modup_a", (double)B * l * (l + 1), 1);
+            ProfScope k(c, fan ? "k:k_fan2j/modup" : "k:k_ntt/modup_a", (double)B * l * (l + 1), 1);
             if (fan) fan_modup(c, D, E, B, l);
             else ks_modup_mac(c, D, E, T, key, ACC, B, l, 1, elt);
         }
@@ -489,7 +489,7 @@ void hoist_node(Ctx &c, PolyArr X, int B, int l, const Hoist &h)
         }
         ProfScope ps(c, "ks_modup_h");
         {
-            ProfScope k(c, "k:k_fan2/hoist", (double)B * l * (l + 1));
+            ProfScope k(c, "k:k_fan2j/hoist", (double)B * l * (l + 1));
             fan_modup(c, h.D, h.E, B, l, false, h.zl);
         }
         ProfScope k(c, "k:k_ntt/modup_h_b", 2.0 * B * l * l);
@@ -511,7 +511,7 @@ void hoist_node(Ctx &c, PolyArr X, int B, int l, const Hoist &h)
     }
     ProfScope ps(c, "ks_modup_h");
     {
-        ProfScope k(c, "k:k_fan2/hoist", (double)B * l * (l + 1));
+        ProfScope k(c, "k:k_fan2j/hoist", (double)B * l * (l + 1));
         fan_modup(c, h.D, h.E, B, l, true);  // pass A of every NTT_I(D_J mod q_I), from the canonical D
     }
     ProfScope k(c, "k:k_ntt/modup_h_b", 2.0 * B * l * l);

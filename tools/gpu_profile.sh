@@ -32,5 +32,5 @@ timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$KRE" --out
 cd $GRAFT_REPO_ROOT
 python tools/profile_step.py $OUT/trace/run_kernel_trace.csv $OUT/trace_bench.json $OUT/profile_step.json || exit 1
 cp $OUT/pmc_fetch/run_counter_collection.csv $OUT/pmc_fetch.csv && cp $OUT/pmc_write/run_counter_collection.csv $OUT/pmc_write.csv
-python tools/pmc_summary.py $OUT/pmc_fetch.csv $OUT/pmc_write.csv $DIMS $TAG "HEC_LANES=1 rocprofv3 --pmc FETCH_SIZE (then WRITE_SIZE, separate pass) --kernel-include-regex '$KRE' -- python3 bench.py $PMCARGS" k_fan2 k_ntt k_hmacm k_bmac k_tensor_multi2 > /dev/null || exit 1
+python tools/pmc_summary.py $OUT/pmc_fetch.csv $OUT/pmc_write.csv $DIMS $TAG "HEC_LANES=1 rocprofv3 --pmc FETCH_SIZE (then WRITE_SIZE, separate pass) --kernel-include-regex '$KRE' -- python3 bench.py $PMCARGS" k_fan2 k_fan2j k_ntt k_hmacm k_bmac k_tensor_multi2 > /dev/null || exit 1
 ls $OUT
