@@ -25,6 +25,9 @@ _lib = None
 u64p = C.POINTER(C.c_uint64)
 
 
+HEC_OK, HEC_EINVAL, HEC_ELOGIC, HEC_EDEVICE = 0, 1, 2, 3  # include/hecdna.h status codes
+
+
 class HecError(Exception):
     """Mirrors SEAL's exception classes: code 1 = invalid_argument, 2 = logic_error, 3 = device."""
 
@@ -58,6 +61,7 @@ def lib():
             "hec_context_destroy": [vp],
             "hec_context_set_stream": [vp, vp],
             "hec_context_synchronize": [vp],
+            "hec_context_set_option": [vp, C.c_char_p, C.c_int64],
             "hec_ciphertext_create": [vp, C.POINTER(vp)],
             "hec_ciphertext_destroy": [vp],
             "hec_ciphertext_upload": [vp, u64p, C.c_uint64, C.c_uint64, C.c_double],
@@ -121,6 +125,9 @@ def lib():
                                          C.POINTER(C.c_int32)],
             "hec_comm_unique_id": [vp],
             "hec_comm_init": [vp, C.c_int, C.c_int, vp],
+            "hec_comm_init_ops": [vp, C.c_int, C.c_int, vp],
+            "hec_shard_agree": [vp, C.c_int, C.c_int, C.c_char_p, C.POINTER(C.c_double), C.c_uint64, C.c_char_p,
+                                C.c_uint64],
             "hec_context_comm": [vp, C.POINTER(C.c_int), C.POINTER(C.c_int)],
             "hec_matmul_diag_col_sharded": [vp, vp, C.c_uint64, vp, C.c_uint64, vp, vp, vp],
             "hec_create_coeff_modulus": [C.c_uint64, C.POINTER(C.c_int), C.c_uint64, u64p],
@@ -160,6 +167,7 @@ def lib():
         L.hec_galois_keys_has.restype = C.c_int
         L.hec_profile_classes.restype = C.c_uint64
         L.hec_seal_last_error.restype = C.c_char_p
+        L.hec_seal_kswitch_keys_default_limit.restype = C.c_uint64
         _lib = L
     return _lib
 
@@ -201,6 +209,55 @@ def comm_unique_id() -> bytes:
     buf = C.create_string_buffer(128)
     _check(lib().hec_comm_unique_id(buf))
     return buf.raw
+
+
+COMM_F64_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_double), C.c_uint64, C.c_int)
+COMM_U64_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, u64p, C.c_uint64)
+REDUCE_MIN, REDUCE_MAX = 0, 1
+
+
+class CommOps(C.Structure):
+    """include/hecdna.h hec_comm_ops"""
+    _fields_ = [("user", C.c_void_p), ("allreduce_f64", COMM_F64_FN), ("allreduce_u64_sum", COMM_U64_FN)]
+
+
+class HostComm:
+    """hec_comm_ops over torch.distributed (a backend with MIN / MAX / SUM on CPU tensors: gloo): the sharded
+    matvec's collectives on the host, for hec_comm_init_ops and hec_shard_agree.  Keeps the ctypes callbacks alive."""
+
+    def __init__(self, group=None):
+        import torch
+        import torch.distributed as dist
+
+        def f64(_user, buf, count, op):
+            try:
+                if count:
+                    t = torch.from_numpy(np.ctypeslib.as_array(buf, shape=(count,)))
+                    dist.all_reduce(t, op=dist.ReduceOp.MIN if op == REDUCE_MIN else dist.ReduceOp.MAX, group=group)
+                return 0
+            except Exception:  # noqa: BLE001 - reported to the engine as a failed collective
+                return 1
+
+        def u64(_user, buf, count):
+            try:
+                if count:  # residues < 2^60, world <= 8: the int64 sum is exact and non-negative
+                    t = torch.from_numpy(np.ctypeslib.as_array(buf, shape=(count,)).view(np.int64))
+                    dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+                return 0
+            except Exception:  # noqa: BLE001
+                return 1
+
+        self._f64, self._u64 = COMM_F64_FN(f64), COMM_U64_FN(u64)
+        self.ops = CommOps(None, self._f64, self._u64)
+
+
+def shard_agree(comm: HostComm, rank: int, status: int, reason: str, scales) -> tuple[int, str]:
+    """hec_shard_agree (host only): the sharded matvec's agreement step -> (agreed status, message)."""
+    sc = np.ascontiguousarray(scales, dtype=np.float64)
+    msg = C.create_string_buffer(512)
+    rc = lib().hec_shard_agree(C.byref(comm.ops), rank, status, reason.encode(),
+                               sc.ctypes.data_as(C.POINTER(C.c_double)), len(sc), msg, 512)
+    return rc, msg.value.decode()
 
 
 # ------------------------------------------------------------------ SEAL wire format (host side)
@@ -371,6 +428,11 @@ class Context:
     def synchronize(self):
         _check(lib().hec_context_synchronize(self.h))
 
+    def set_option(self, name: str, value: int):
+        """hec_context_set_option: an engine knob (lanes, poison, lane_serial, hoist, ...) on the context and its
+        batch lanes; every setting computes the same bits."""
+        _check(lib().hec_context_set_option(self.h, name.encode(), int(value)))
+
     def elt_from_step(self, step):
         e = lib().hec_galois_elt_from_step(self.h, int(step))
         if e == 0:
@@ -484,6 +546,11 @@ class Context:
     def comm_init(self, rank, world, unique_id: bytes | None = None):
         buf = C.create_string_buffer(unique_id, 128) if unique_id is not None else None
         _check(lib().hec_comm_init(self.h, rank, world, buf))
+
+    def comm_init_ops(self, rank, world, comm: HostComm):
+        """hec_comm_init_ops: the sharded matvec over the caller's host collectives (e.g. gloo)."""
+        self._host_comm = comm  # the engine keeps the callbacks
+        _check(lib().hec_comm_init_ops(self.h, rank, world, C.byref(comm.ops)))
 
     def matmul_diag_col_sharded(self, diags, cols, rk, gk, out=None):
         """hec_matmul_diag_col_sharded: every rank calls it; returns all p outputs on every rank."""

@@ -248,6 +248,11 @@ int main(int argc, char **argv)
         keep.push_back(d0);
         keep.push_back(d1);
         keep.push_back(d2);
+        // SEAL's chain walk (print_parameters, the chain loops of the examples): key level, then first .. last
+        std::cout << "chain";
+        for (auto cd = ctx.key_context_data(); cd; cd = cd->next_context_data()) std::cout << " " << cd->chain_index();
+        std::cout << " first " << ctx.first_context_data()->chain_index() << " key_next "
+                  << (ctx.key_context_data()->next_context_data() == ctx.first_context_data()) << "\n";
     } else if (mode == "least_squares") {
         // bench_he_least_squares_2d after encryption (matrix_operations.cpp:915-1003), x_ct = c0, y_ct = c1
         hecdna::CKKSEncoder cencd(ctx);

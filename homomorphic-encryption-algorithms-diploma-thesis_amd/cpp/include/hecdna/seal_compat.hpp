@@ -150,8 +150,9 @@ public:
         for (std::size_t l = 1; l <= coeff_modulus.size(); ++l) {
             std::vector<std::uint64_t> q(coeff_modulus.begin(), coeff_modulus.begin() + (std::ptrdiff_t)l);
             const parms_id_type id = compute_parms_id(poly_modulus_degree, q.data(), l);
-            auto cd = std::make_shared<const ContextData>(l, poly_modulus_degree, std::move(q), id,
-                                                          l == coeff_modulus.size() ? nullptr : next);
+            // every level links to the one below, the key level too: SEAL's key_context_data()->next_context_data()
+            // is first_context_data()
+            auto cd = std::make_shared<const ContextData>(l, poly_modulus_degree, std::move(q), id, next);
             by_id_[id] = l;
             levels_[l] = cd;
             next = cd;

@@ -35,6 +35,16 @@ using namespace hec;
 using u128 = unsigned __int128;
 
 // =============================================================================== objects ===
+// The communicator of the sharded matvec (one process per GPU): RCCL over xGMI (hec_comm_init) or a caller's host
+// collectives (hec_comm_init_ops).  shard_agree needs only allreduce_f64; the data exchange sums the ranks' partial
+// accumulators in u64.
+struct HecComm {
+    virtual ~HecComm() = default;
+    // in place over the world, host memory: op HEC_REDUCE_MIN / HEC_REDUCE_MAX
+    virtual void allreduce_f64(double *host, std::size_t n, int op, hipStream_t s) = 0;
+    // in place over the world, a device buffer ordered on stream s: the sum (exact: world <= 8, residues < 2^60)
+    virtual void allreduce_u64_sum(u64 *dev, std::size_t n, hipStream_t s) = 0;
+};
 struct hec_context {
     Ctx c;
     // batch lanes (matvec_lanes): contexts sharing this one's device tables, each with its own HIP
@@ -46,7 +56,7 @@ struct hec_context {
     hipEvent_t lanes_start = nullptr, lane_done = nullptr;
     // multi-GPU (hec_comm_init): this process's rank in a world of one process per GPU, RCCL communicator
     int rank = 0, world = 1;
-    void *comm = nullptr;  // ncclComm_t
+    HecComm *comm = nullptr;
 };
 struct hec_ciphertext {
     hec_context *ctx = nullptr;
@@ -244,6 +254,8 @@ void ensure(hec_ciphertext *ct, std::size_t words)
     if (ct->d) HEC_HIP(hipFree(ct->d));
     ct->d = dalloc(words);
     ct->cap = words;
+    if (ct->ctx && ct->ctx->c.poison)
+        HEC_HIP(hipMemsetAsync(ct->d, 0xFF, words * sizeof(u64), ct->ctx->c.stream));
 }
 
 // stack-style carving of the context workspace; kernels are stream ordered, so a region released
@@ -273,6 +285,7 @@ struct Scratch {
         if (top + w > c.ws.words) throw std::logic_error("workspace overflow");
         u64 *p = c.ws.base + top;
         top += w;
+        if (c.poison) HEC_HIP(hipMemsetAsync(p, 0xFF, w * sizeof(u64), c.stream));
         return p;
     }
 };
@@ -1053,13 +1066,16 @@ void matvec_lanes(hec_context *ctx, const hec_ciphertext *const *diags, const he
                 HEC_HIP(hipStreamWaitEvent(lc.stream, start, 0));
                 matvec_core(ctx, diags, pdiags, n, js, cols + b0, b1 - b0, rk, gk, finish, out + b0, &lc);
                 HEC_HIP(hipEventRecord(ctx->lanes[i]->lane_done, lc.stream));
+                if (c.lane_serial) HEC_HIP(hipStreamSynchronize(lc.stream));
                 done[i] = 1;
             } catch (...) {
                 err[i] = std::current_exception();
             }
         });
+        if (c.lane_serial) th.back().join();
     }
-    for (auto &t : th) t.join();
+    for (auto &t : th)
+        if (t.joinable()) t.join();
     for (int i = 0; i < nl; ++i)  // later work on the context sees the outputs
         if (done[i]) HEC_HIP(hipStreamWaitEvent(c.stream, ctx->lanes[i]->lane_done, 0));
     for (int i = 0; i < nl; ++i)  // outgrown lane workspaces, now that no lane thread runs (waits only after a growth)
@@ -1185,6 +1201,78 @@ void nccl_check(ncclResult_t e, const char *what)
     if (e != ncclSuccess)
         throw std::logic_error(std::string(what) + ": " + (rccl().error_string ? rccl().error_string(e) : "RCCL error"));
 }
+
+struct RcclComm final : HecComm {
+    ncclComm_t comm;
+    explicit RcclComm(ncclComm_t c) : comm(c) {}
+    ~RcclComm() override { (void)rccl().destroy(comm); }
+    void allreduce_f64(double *host, std::size_t n, int op, hipStream_t s) override
+    {
+        double *dv = nullptr;
+        HEC_HIP(hipMallocAsync((void **)&dv, n * sizeof(double), s));
+        HEC_HIP(hipMemcpyAsync(dv, host, n * sizeof(double), hipMemcpyHostToDevice, s));
+        nccl_check(rccl().all_reduce(dv, dv, n, ncclFloat64, op == HEC_REDUCE_MIN ? ncclMin : ncclMax, comm, s),
+                   "ncclAllReduce");
+        HEC_HIP(hipMemcpyAsync(host, dv, n * sizeof(double), hipMemcpyDeviceToHost, s));
+        HEC_HIP(hipFreeAsync(dv, s));
+        HEC_HIP(hipStreamSynchronize(s));
+    }
+    void allreduce_u64_sum(u64 *dev, std::size_t n, hipStream_t s) override
+    {
+        nccl_check(rccl().all_reduce(dev, dev, n, ncclUint64, ncclSum, comm, s), "ncclAllReduce");
+    }
+};
+
+// the caller's host collectives (hec_comm_ops): MPI, torch.distributed (gloo), ...
+struct OpsComm final : HecComm {
+    hec_comm_ops ops;
+    explicit OpsComm(const hec_comm_ops &o) : ops(o) {}
+    void allreduce_f64(double *host, std::size_t n, int op, hipStream_t) override
+    {
+        if (ops.allreduce_f64(ops.user, host, n, op) != 0) throw std::logic_error("hec_comm_ops allreduce_f64 failed");
+    }
+    void allreduce_u64_sum(u64 *dev, std::size_t n, hipStream_t s) override
+    {
+        std::vector<u64> h(n);
+        HEC_HIP(hipMemcpyAsync(h.data(), dev, n * sizeof(u64), hipMemcpyDeviceToHost, s));
+        HEC_HIP(hipStreamSynchronize(s));
+        if (ops.allreduce_u64_sum(ops.user, h.data(), n) != 0)
+            throw std::logic_error("hec_comm_ops allreduce_u64_sum failed");
+        HEC_HIP(hipMemcpyAsync(dev, h.data(), n * sizeof(u64), hipMemcpyHostToDevice, s));
+        HEC_HIP(hipStreamSynchronize(s));
+    }
+};
+
+// The sharded matvec's agreement step, before any data-path collective: every rank contributes its own argument
+// check (status, SEAL's message) and its p product scales; all ranks return the same verdict, so an argument error
+// on one rank is an error on every rank instead of a rank left waiting in the exchange, and SEAL's add_inplace "scale
+// mismatch" is checked over the whole sum (he_linalg.cpp:977-997 adds every rank's terms).  Two all-reduces of p + 1
+// doubles: [0] = (status << 8) | (rank + 1) of a failing rank (max, so the highest failing rank names the error),
+// [1 .. p] the scales (min and max; a failing rank contributes +inf / -inf so it never decides the comparison).
+int shard_agree(HecComm &cm, int rank, int status, std::string &msg, const double *ps, std::size_t p, hipStream_t s)
+{
+    std::vector<double> mn(1 + p), mx(1 + p);
+    mn[0] = mx[0] = status ? (double)((status << 8) | (rank + 1)) : 0.0;
+    for (std::size_t i = 0; i < p; ++i) {
+        mn[1 + i] = status ? std::numeric_limits<double>::infinity() : ps[i];
+        mx[1 + i] = status ? -std::numeric_limits<double>::infinity() : ps[i];
+    }
+    cm.allreduce_f64(mn.data(), mn.size(), HEC_REDUCE_MIN, s);
+    cm.allreduce_f64(mx.data(), mx.size(), HEC_REDUCE_MAX, s);
+    const int agreed = (int)mx[0];
+    if (!status && agreed) {
+        status = agreed >> 8;
+        msg = "matmul_diag_col_sharded: the arguments failed SEAL's checks on rank " + std::to_string((agreed & 0xff) - 1);
+    }
+    if (!status)
+        for (std::size_t i = 0; i < p; ++i)
+            if (!are_close(mn[1 + i], mx[1 + i])) {
+                status = HEC_EINVAL;
+                msg = "scale mismatch";
+                break;
+            }
+    return status;
+}
 }  // namespace
 
 // =============================================================================== workspace ==
@@ -1275,6 +1363,8 @@ int hec_context_create(uint64_t N, const uint64_t *mod, uint64_t K, int device, 
         if (const char *f = std::getenv("HEC_HOIST_MIN")) c.hoist_min_children = std::max(1, std::atoi(f));
         if (const char *f = std::getenv("HEC_TENSOR_DEFER")) c.tensor_defer_max = std::max(1, std::atoi(f));
         if (const char *f = std::getenv("HEC_TENSOR_BUFS")) c.tensor_defer_bufs = std::max(1, std::atoi(f));
+        if (const char *f = std::getenv("HEC_POISON")) c.poison = f[0] != '0';
+        if (const char *f = std::getenv("HEC_LANE_SERIAL")) c.lane_serial = f[0] != '0';
         c.N = N;
         c.logN = __builtin_ctzll(N);
         c.K = K;
@@ -1412,7 +1502,7 @@ int hec_context_destroy(hec_context *ctx)
         (void)hipStreamSynchronize(c.stream);
         for (hec_context *l : ctx->lanes) free_lane(l);
         if (ctx->lanes_start) (void)hipEventDestroy(ctx->lanes_start);
-        if (ctx->comm) (void)rccl().destroy((ncclComm_t)ctx->comm);
+        delete ctx->comm;
         c.ws.release();
         (void)hipFree(c.primes);
         (void)hipFree(c.imap);
@@ -1448,6 +1538,38 @@ int hec_context_set_stream(hec_context *ctx, void *stream)
         } else {
             HEC_HIP(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
             c.own_stream = true;
+        }
+    });
+}
+
+int hec_context_set_option(hec_context *ctx, const char *name, int64_t value)
+{
+    return guard([&] {
+        need(ctx && name, "null argument");
+        set_device(ctx);
+        const std::string n(name);
+        auto apply = [&](Ctx &c) {
+            if (n == "lanes") c.lanes = (int)std::max<int64_t>(1, value);
+            else if (n == "lane_min_batch") c.lane_min_batch = (int)std::max<int64_t>(1, value);
+            else if (n == "poison") c.poison = value != 0;
+            else if (n == "lane_serial") c.lane_serial = value != 0;
+            else if (n == "hoist") c.hoist = value != 0;
+            else if (n == "hoist_min") c.hoist_min_children = (int)std::max<int64_t>(1, value);
+            else if (n == "hmac") c.hmac_cfg = (int)value;
+            else if (n == "hmac_odd3") c.hmac_odd3 = (int)value;
+            else if (n == "hoist_scan") c.hoist_scan = (int)value;
+            else if (n == "fan") c.fan_out = value != 0;
+            else if (n == "fuse_galois") c.fuse_galois = value != 0;
+            else if (n == "fused_modup_mac") c.fused_modup_mac = value != 0;
+            else if (n == "tensor_defer") c.tensor_defer_max = (int)std::max<int64_t>(1, value);
+            else if (n == "tensor_bufs") c.tensor_defer_bufs = (int)std::max<int64_t>(1, value);
+            else throw std::invalid_argument("unknown option");
+        };
+        HEC_HIP(hipStreamSynchronize(ctx->c.stream));
+        apply(ctx->c);
+        for (hec_context *l : ctx->lanes) {  // the lanes hold copies of the knobs (make_lane)
+            HEC_HIP(hipStreamSynchronize(l->c.stream));
+            apply(l->c);
         }
     });
 }
@@ -1988,11 +2110,18 @@ int hec_ciphertext_save_seal(const hec_ciphertext *ct, int compr_mode, void *out
 
 // Decompressed-size limit of a KSwitchKeys object loaded into this context (the bytes come from a client socket,
 // server.cpp:110-122): `lists` key lists of L PublicKeys of u64[2][K][N], the object's N list-length words, and at
-// most 256 B of SEALHeader / parms_id / ciphertext metadata per PublicKey.  GaloisKeys are accepted with up to
-// kMaxGaloisLists non-empty lists: SEAL's default set (create_galois_keys(), the reference's only form:
-// matrix_operations.cpp:771,872,1064) holds 2 log2(N) - 1; a caller with more keys loads them with
-// hec_seal_kswitch_keys_foreach_ex and an explicit limit.
-static constexpr uint64_t kMaxGaloisLists = 64;
+// most 256 B of SEALHeader / parms_id / ciphertext metadata per PublicKey.  GaloisKeys are accepted with as many
+// non-empty lists as there are Galois elements (N: the odd residues mod 2N) and as fit in the device's free memory
+// at load time, the same bound whether the object is compressed (the inflate budget) or not (counted as the lists
+// are parsed).  SEAL's default set (create_galois_keys(), the reference's only form: matrix_operations.cpp:771,
+// 872,1064) holds 2 log2(N) - 1.
+static uint64_t galois_lists_that_fit(const Ctx &c)
+{
+    std::size_t free_b = 0, total_b = 0;
+    HEC_HIP(hipMemGetInfo(&free_b, &total_b));
+    const uint64_t per = c.L * 2 * c.K * c.N * 8;
+    return std::max<uint64_t>(1, std::min<uint64_t>(c.N, free_b / per));
+}
 static uint64_t seal_keys_max_bytes(const Ctx &c, uint64_t lists)
 {
     return lists * c.L * (2 * c.K * c.N * 8 + 256) + c.N * 8 + 4096;
@@ -2020,11 +2149,13 @@ int hec_galois_keys_load_seal(hec_galois_keys *gk, const void *bytes, uint64_t n
 {
     return guard([&] {
         need(gk && bytes, "null argument");
+        set_device(gk->ctx);
         struct Visit {
             hec_galois_keys *gk;
+            uint64_t max_lists, seen = 0;
             std::string err;
             int rc = HEC_OK;
-        } v{gk, {}};
+        } v{gk, galois_lists_that_fit(gk->ctx->c)};
         // one pass over the object: GaloisKeys::get_index(elt) = (elt - 1) / 2, every non-empty list uploaded as it
         // is parsed
         auto cb = [](void *user, uint64_t index, const uint64_t *words, uint64_t nwords) -> int {
@@ -2034,12 +2165,16 @@ int hec_galois_keys_load_seal(hec_galois_keys *gk, const void *bytes, uint64_t n
                 st->err = "galois_keys is not valid for encryption parameters";
                 return st->rc = HEC_EINVAL;
             }
+            if (++st->seen > st->max_lists) {  // the uncompressed object's form of the inflate budget below
+                st->err = "decompressed SEAL object exceeds the size limit";
+                return st->rc = HEC_EINVAL;
+            }
             const int rc = hec_galois_keys_add(st->gk, (uint32_t)(2 * index + 1), words);
             if (rc != HEC_OK) st->err = hec_last_error();
             return st->rc = rc;
         };
         uint64_t used = 0;
-        const int rc = hec_seal_kswitch_keys_foreach_ex(bytes, nbytes, seal_keys_max_bytes(gk->ctx->c, kMaxGaloisLists),
+        const int rc = hec_seal_kswitch_keys_foreach_ex(bytes, nbytes, seal_keys_max_bytes(gk->ctx->c, v.max_lists),
                                                         cb, &v, nullptr, &used);
         if (v.rc != HEC_OK) {
             if (v.rc == HEC_EINVAL) throw std::invalid_argument(v.err);
@@ -2377,11 +2512,45 @@ int hec_comm_init(hec_context *ctx, int rank, int world, const void *unique_id)
             std::memcpy(&id, unique_id, sizeof(id));
             ncclComm_t comm = nullptr;
             nccl_check(rccl().init_rank(&comm, world, id, rank), "ncclCommInitRank");
-            ctx->comm = comm;
+            ctx->comm = new RcclComm(comm);
         }
         ctx->rank = rank;
         ctx->world = world;
     });
+}
+
+int hec_comm_init_ops(hec_context *ctx, int rank, int world, const hec_comm_ops *ops)
+{
+    return guard([&] {
+        set_device(ctx);
+        need(world >= 1 && rank >= 0 && rank < world, "invalid rank / world");
+        need(world <= 8, "world must be at most 8 (exact u64 partial-sum exchange)");
+        need(ctx->comm == nullptr, "communicator already initialised");
+        need(ops && ops->allreduce_f64 && ops->allreduce_u64_sum, "null argument");
+        ctx->comm = new OpsComm(*ops);
+        ctx->rank = rank;
+        ctx->world = world;
+    });
+}
+
+int hec_shard_agree(const hec_comm_ops *ops, int rank, int status, const char *reason, const double *scales,
+                    uint64_t p, char *msg, uint64_t msg_cap)
+{
+    int agreed = HEC_OK;
+    const int rc = guard([&] {
+        need(ops && ops->allreduce_f64 && ops->allreduce_u64_sum && (p == 0 || scales || status), "null argument");
+        need(status == HEC_OK || status == HEC_EINVAL || status == HEC_ELOGIC, "status must be HEC_OK / EINVAL / ELOGIC");
+        need(rank >= 0 && rank < 255, "invalid rank / world");
+        OpsComm cm(*ops);
+        std::string m = reason ? reason : "";
+        agreed = shard_agree(cm, rank, status, m, scales, p, nullptr);
+        if (msg && msg_cap) {
+            const std::size_t k = std::min<std::size_t>(m.size(), msg_cap - 1);
+            std::memcpy(msg, m.data(), k);
+            msg[k] = 0;
+        }
+    });
+    return rc != HEC_OK ? rc : agreed;
 }
 
 int hec_context_comm(const hec_context *ctx, int *rank, int *world)
@@ -2420,34 +2589,7 @@ int hec_matmul_diag_col_sharded(hec_context *ctx, const hec_ciphertext *const *d
         } catch (const std::logic_error &e) {
             status = HEC_ELOGIC; msg = e.what();
         }
-        const Rccl *nc = ctx->comm ? &rccl() : nullptr;
-        if (nc) {
-            // [0] status << 8 | (rank + 1) of a failing rank (max), [1 .. p] product scales (min), [p+1 .. 2p] (max)
-            const uint64_t words = 1 + p;
-            std::vector<double> hv(words, 0.0), hmin(words), hmax(words);
-            hv[0] = status ? (double)((status << 8) | (ctx->rank + 1)) : 0.0;
-            for (uint64_t i = 0; i < p && i < ps.size(); ++i) hv[1 + i] = ps[i];
-            double *dv = nullptr;
-            HEC_HIP(hipMallocAsync((void **)&dv, 2 * words * sizeof(double), c.stream));
-            HEC_HIP(hipMemcpyAsync(dv, hv.data(), words * sizeof(double), hipMemcpyHostToDevice, c.stream));
-            HEC_HIP(hipMemcpyAsync(dv + words, hv.data(), words * sizeof(double), hipMemcpyHostToDevice, c.stream));
-            nccl_check(nc->all_reduce(dv, dv, words, ncclFloat64, ncclMin, (ncclComm_t)ctx->comm, c.stream), "ncclAllReduce");
-            nccl_check(nc->all_reduce(dv + words, dv + words, words, ncclFloat64, ncclMax, (ncclComm_t)ctx->comm, c.stream),
-                       "ncclAllReduce");
-            HEC_HIP(hipMemcpyAsync(hmin.data(), dv, words * sizeof(double), hipMemcpyDeviceToHost, c.stream));
-            HEC_HIP(hipMemcpyAsync(hmax.data(), dv + words, words * sizeof(double), hipMemcpyDeviceToHost, c.stream));
-            HEC_HIP(hipFreeAsync(dv, c.stream));
-            HEC_HIP(hipStreamSynchronize(c.stream));
-            const int agreed = (int)hmax[0];
-            if (!status && agreed) {
-                status = agreed >> 8;
-                msg = "matmul_diag_col_sharded: the arguments failed SEAL's checks on rank " +
-                      std::to_string((agreed & 0xff) - 1);
-            }
-            if (!status)
-                for (uint64_t i = 0; i < p; ++i)
-                    if (!are_close(hmin[1 + i], hmax[1 + i])) { status = HEC_EINVAL; msg = "scale mismatch"; }
-        }
+        if (ctx->comm) status = shard_agree(*ctx->comm, ctx->rank, status, msg, ps.data(), p, c.stream);
         if (status == HEC_EINVAL) throw std::invalid_argument(msg);
         if (status) throw std::logic_error(msg);
         const std::size_t l = cols[0]->level, S3 = 3 * l * c.N;
@@ -2460,14 +2602,13 @@ int hec_matmul_diag_col_sharded(hec_context *ctx, const hec_ciphertext *const *d
             ~Free() { for (auto &x : a) if (x.d) (void)hipFree(x.d); }
         } free_acc{acc};
         matvec_lanes(ctx, diags, nullptr, n, mine, cols, p, nullptr, gk, false, accp.data());
-        if (nc) {
+        if (ctx->comm) {
             // the one exchange: a plain u64 sum of the world's canonical residues (< world 2^60 < 2^64), then
             // reduce mod q; every rank then holds the full accumulators (he_linalg.cpp:977-997 summed)
             u64 *buf = nullptr;
             HEC_HIP(hipMallocAsync((void **)&buf, p * S3 * sizeof(u64), c.stream));
             for (uint64_t i = 0; i < p; ++i) d2d(c, buf + i * S3, acc[i].d, S3);
-            nccl_check(nc->all_reduce(buf, buf, p * S3, ncclUint64, ncclSum, (ncclComm_t)ctx->comm, c.stream),
-                       "ncclAllReduce");
+            ctx->comm->allreduce_u64_sum(buf, p * S3, c.stream);
             ew_reduce(c, buf, (int)(3 * p), (int)l);
             for (uint64_t i = 0; i < p; ++i) d2d(c, acc[i].d, buf + i * S3, S3);
             HEC_HIP(hipFreeAsync(buf, c.stream));

@@ -97,6 +97,11 @@ struct Ctx {
     int lane_min_batch = 16;       // input vectors per lane at least
     bool fuse_galois = true;       // HEC_FUSE_GALOIS=0: materialise apply_galois before the key switch
     bool fused_modup_mac = true;  // HEC_FUSED_MODUP_MAC=0: separate mod-up pass B and key MAC kernels
+    // HEC_POISON=1 (debug): every workspace carve (Scratch::take) and every freshly allocated output buffer is
+    // filled with 0xFF bytes before use, so a kernel that reads memory this call never wrote sees a value no
+    // residue can have (2^64 - 1; a NaN as FP64 bits) and the parity tests fail deterministically
+    bool poison = false;
+    bool lane_serial = false;      // HEC_LANE_SERIAL=1 (debug): the lanes run one after another, each drained
     // profiling (ProfScope in hec_engine.hip)
     int prof_mode = 0;  // 0 off, 1 synchronous per scope, 2 asynchronous event pairs
     // a scope's algorithmic bytes (compulsory reads + writes of its kernels) and kernel launches, so

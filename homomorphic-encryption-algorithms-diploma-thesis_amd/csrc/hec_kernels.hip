@@ -1143,7 +1143,7 @@ __global__ void __launch_bounds__(NSEG *(1 << LOGP) / 16)
     k_fan2j(const FAN fan, TwTables inv, TwTables fwd, const DevPrime *__restrict__ primes, int logN, int njobs)
 {
     constexpr int P = 1 << LOGP, TPS = P / 16, LD = NSEG + 1, TILE = P * LD;
-    constexpr int S1R = LOGP, D1 = LOGP - 4, G1 = 1 << (4 - D1);
+    constexpr int D1 = LOGP - 4, G1 = 1 << (4 - D1);
     __shared__ u64 lds[(DB ? 2 : 1) * TILE];
     const int seg0 = blockIdx.x * NSEG, lc = logN - LOGP;
     const int ts = threadIdx.x / NSEG, sg = threadIdx.x % NSEG;
@@ -1268,6 +1268,9 @@ __global__ void __launch_bounds__(NSEG *(1 << LOGP) / 16)
 #pragma unroll
             for (int k = 0; k < 16; ++k) tgt.out[gblock(k)] = v[k];
         }
+        // a target slice [t0, t1) without a valid target for this job (gridDim.z > 1) loaded nothing above: the next
+        // job's source still has to replace d (block-uniform, never taken with one target group)
+        if (tl < 0 && jj + 1 < JPB && job + 1 < njobs) load_src(job + 1, d);
     }
 }
 

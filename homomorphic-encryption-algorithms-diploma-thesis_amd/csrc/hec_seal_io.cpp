@@ -370,12 +370,12 @@ const Zlib &zlib()
 // Decompressed member bytes are bounded: a client's bytes arrive over the socket (server.cpp:110-122), so a small
 // compressed payload must not expand without limit.  kMaxCtObject covers a ciphertext object (size <= 16 polys,
 // N <= 2^17, <= 64 limbs of u64: 1 GiB of words).  A KSwitchKeys object is bounded by its caller: the device
-// loaders know N, K and L and pass the exact size of the key lists they accept (hec_engine.hip); the context-free
-// entry points use kMaxKeysObjectDefault (4 GiB: SEAL's default GaloisKeys at N = 2^15, L = 10 take 1.67 GB), and
-// the *_ex forms take an explicit limit.  The output buffer doubles from a small start, so a rejected payload has
+// loaders know N, K and L and pass the size of the key lists they accept (hec_engine.hip); the context-free
+// entry points use kMaxKeysObjectDefault (16 GiB: SEAL's default GaloisKeys take 1.67 GB at N = 2^15, L = 10 and
+// 8.84 GB at the cfg5 size N = 2^16, L = 16, 31 lists), and the *_ex forms take an explicit limit.  The output buffer doubles from a small start, so a rejected payload has
 // cost at most twice the limit.
 constexpr std::size_t kMaxCtObject = (std::size_t)1 << 31;
-constexpr std::size_t kMaxKeysObjectDefault = (std::size_t)1 << 32;
+constexpr std::size_t kMaxKeysObjectDefault = (std::size_t)1 << 34;
 void check_growth(std::size_t want, std::size_t max_out)
 {
     if (want > max_out) throw std::invalid_argument("decompressed SEAL object exceeds the size limit");
@@ -667,6 +667,7 @@ void walk_kswitch_keys(const void *bytes, uint64_t nbytes, uint64_t max_bytes, u
 extern "C" {
 
 const char *hec_seal_last_error(void) { return g_io_err.c_str(); }
+uint64_t hec_seal_kswitch_keys_default_limit(void) { return kMaxKeysObjectDefault; }
 
 int hec_seal_blake2b(const void *in, uint64_t n, uint64_t outlen, void *out)
 {

@@ -58,6 +58,14 @@ int hec_context_create(uint64_t poly_modulus_degree, const uint64_t *coeff_modul
 int hec_context_destroy(hec_context *ctx);
 int hec_context_set_stream(hec_context *ctx, void *hip_stream); /* NULL = context-owned stream */
 int hec_context_synchronize(hec_context *ctx);
+/* Engine knobs at run time (no SEAL counterpart; the HEC_* environment switches of DESIGN.md §4.1 set the
+ * same knobs at context creation): "lanes", "lane_min_batch", "hoist", "hoist_min", "hmac", "hmac_odd3",
+ * "hoist_scan", "fan", "fuse_galois", "fused_modup_mac", "tensor_defer", "tensor_bufs", and two debug switches:
+ * "poison" (every workspace carve and fresh output buffer is filled with 0xFF bytes before use, so a read of
+ * memory the call never wrote becomes a deterministic wrong result) and "lane_serial" (batch lanes run one after
+ * another).  Every schedule is bit-identical.  Applies to the context and its batch lanes; HEC_EINVAL for an
+ * unknown name. */
+int hec_context_set_option(hec_context *ctx, const char *name, int64_t value);
 uint64_t hec_context_poly_degree(const hec_context *ctx);
 uint64_t hec_context_key_moduli(const hec_context *ctx); /* K */
 /* seal::GaloisTool::get_elt_from_step (rotation step -> Galois element); 0 on error */
@@ -194,13 +202,36 @@ int hec_comm_unique_id(void *unique_id);
 /* ncclCommInitRank on the context's device; world == 1 needs no id; 1 <= world <= 8 (the partial-sum exchange
  * adds world canonical 60-bit residues in u64).  The communicator lives until hec_context_destroy. */
 int hec_comm_init(hec_context *ctx, int rank, int world, const void *unique_id);
+/* A host communicator: the caller's own collectives (MPI, a gloo process group, ...) for the sharded
+ * matvec, in place of RCCL.  Both callbacks are all-reduces over the world, in place, on host memory, and return
+ * 0 on success.  allreduce_f64: op HEC_REDUCE_MIN or HEC_REDUCE_MAX.  allreduce_u64_sum: exact (world <= 8
+ * residues < 2^60).  The engine calls them from the thread that called hec_matmul_diag_col_sharded. */
+#define HEC_REDUCE_MIN 0
+#define HEC_REDUCE_MAX 1
+typedef struct hec_comm_ops {
+    void *user;
+    int (*allreduce_f64)(void *user, double *buf, uint64_t count, int op);
+    int (*allreduce_u64_sum)(void *user, uint64_t *buf, uint64_t count);
+} hec_comm_ops;
+/* hec_comm_init with the caller's collectives (*ops is copied); same world bound. */
+int hec_comm_init_ops(hec_context *ctx, int rank, int world, const hec_comm_ops *ops);
+/* The agreement step hec_matmul_diag_col_sharded runs before any data moves (host only, no device needed): each
+ * rank passes its own check result (status HEC_OK / HEC_EINVAL / HEC_ELOGIC and SEAL's message) and its p output
+ * product scales; after two allreduce_f64 calls a failing rank returns its own status and message, every other rank
+ * the status of the failing rank with the larger (status << 8 | rank + 1) and "... failed SEAL's checks on rank r";
+ * when no rank failed, every rank returns HEC_EINVAL "scale mismatch" if the ranks' scales of one output are not
+ * SEAL-close (add_inplace over the whole sum), else HEC_OK.  No rank is left waiting in the exchange.  msg (cap bytes,
+ * may be NULL) receives the message.  HEC_EDEVICE / HEC_ELOGIC when a callback fails. */
+int hec_shard_agree(const hec_comm_ops *ops, int rank, int status, const char *reason, const double *scales,
+                    uint64_t p, char *msg, uint64_t msg_cap);
 /* 1 when the context has a communicator (then *rank, *world are set), 0 when not, HEC_EINVAL on NULL */
 int hec_context_comm(const hec_context *ctx, int *rank, int *world);
 /* BatchedMatrix::matmul diag x col over the world (every rank calls it with the same arguments): rank r
  * computes the partial sums over its planned diagonals (hec_plan_diagonal_shards with the keys of gk): only those
  * diags[j] are read and checked, every other entry is never dereferenced and may be NULL or any handle.  The
  * ranks then agree on the argument checks (a one-int RCCL all-reduce, so an error on one rank is returned on all
- * ranks instead of leaving the others in the exchange), run one RCCL all-reduce of the partials (u64 sum, exact
+ * ranks instead of leaving the others in the exchange; hec_shard_agree), run one all-reduce of the partials (RCCL,
+ * or the host communicator of hec_comm_init_ops; u64 sum, exact
  * for world <= 8 and 60-bit primes) + reduction mod q, and every rank relinearizes and rescales all p outputs:
  * out[i] is bit-identical to hec_matmul_diag_col on one GPU. */
 int hec_matmul_diag_col_sharded(hec_context *ctx, const hec_ciphertext *const *diags, uint64_t n,
@@ -217,7 +248,7 @@ int hec_matmul_diag_col_sharded(hec_context *ctx, const hec_ciphertext *const *d
  * loader hec_ciphertext_load_seal (Ciphertext::expand_seed); hec_seal_ciphertext_load, which has no moduli,
  * rejects them (HEC_EINVAL).  Decompressed objects are bounded, since the bytes come from a client socket
  * (server.cpp:110-122): 2 GiB per ciphertext; a key object (with every compressed member nested in it) by the
- * caller's max_bytes in the *_ex forms, by 4 GiB in the others, and by the size of the key lists the context
+ * caller's max_bytes in the *_ex forms, by 16 GiB in the others, and by the size of the key lists the context
  * accepts in the device loaders.  A payload over its limit is HEC_EINVAL ("decompressed SEAL object exceeds the
  * size limit"); a payload must also hold the words it announces. */
 #define HEC_COMPR_NONE 0
@@ -252,11 +283,14 @@ int hec_seal_parms_load(const void *bytes, uint64_t nbytes, uint64_t *poly_modul
                         uint64_t cap, uint64_t *count, uint64_t *consumed);
 int hec_seal_parms_save(uint64_t poly_modulus_degree, const uint64_t *coeff_modulus, uint64_t count, int compr_mode,
                         void *out, uint64_t cap, uint64_t *written);
+/* the decompressed-size limit of the context-free key loaders below (16 GiB: SEAL's default GaloisKeys at
+ * N = 2^16 with 17 primes take 8.84 GB) */
+uint64_t hec_seal_kswitch_keys_default_limit(void);
 /* KSwitchKeys (RelinKeys, GaloisKeys) load of key list `index` (RelinKeys 0, GaloisKeys (galois_elt - 1) / 2)
  * in the engine's key layout u64[L][2][K][N]; *lists = the object's list count, *words = that list's words */
 int hec_seal_kswitch_keys_load(const void *bytes, uint64_t nbytes, uint64_t index, uint64_t *lists, uint64_t *out,
                                uint64_t cap_words, uint64_t *words, uint64_t *consumed);
-/* ... with at most max_bytes decompressed (0: the 4 GiB default) */
+/* ... with at most max_bytes decompressed (0: the 16 GiB default) */
 int hec_seal_kswitch_keys_load_ex(const void *bytes, uint64_t nbytes, uint64_t index, uint64_t max_bytes,
                                   uint64_t *lists, uint64_t *out, uint64_t cap_words, uint64_t *words,
                                   uint64_t *consumed);
@@ -267,7 +301,7 @@ int hec_seal_kswitch_keys_load_ex(const void *bytes, uint64_t nbytes, uint64_t i
 int hec_seal_kswitch_keys_foreach(const void *bytes, uint64_t nbytes,
                                   int (*visit)(void *user, uint64_t index, const uint64_t *words, uint64_t nwords),
                                   void *user, uint64_t *lists, uint64_t *consumed);
-/* ... with at most max_bytes decompressed (0: the 4 GiB default) */
+/* ... with at most max_bytes decompressed (0: the 16 GiB default) */
 int hec_seal_kswitch_keys_foreach_ex(const void *bytes, uint64_t nbytes, uint64_t max_bytes,
                                      int (*visit)(void *user, uint64_t index, const uint64_t *words, uint64_t nwords),
                                      void *user, uint64_t *lists, uint64_t *consumed);

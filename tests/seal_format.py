@@ -55,7 +55,7 @@ def parms(N, moduli) -> bytes:
     return obj(m)
 
 
-def kswitch_keys(N, moduli, lists) -> bytes:
+def kswitch_keys(N, moduli, lists, compr=0) -> bytes:
     pid = parms_id(N, moduli)
     m = pid.astype(np.uint64).tobytes() + struct.pack("<Q", len(lists))
     for k in lists:
@@ -65,7 +65,7 @@ def kswitch_keys(N, moduli, lists) -> bytes:
         m += struct.pack("<Q", k.shape[0])
         for j in range(k.shape[0]):
             m += obj(ciphertext(k[j], 1.0, moduli, pid=pid))  # PublicKey wrapping its Ciphertext
-    return obj(m)
+    return obj(m, compr)
 
 
 # ---- seeded ciphertexts (Encryptor::encrypt_symmetric(...).save, src/demos/client.cpp:113-114)

@@ -105,12 +105,22 @@ def test_demo_he_math(demo, math_env, tmp_path, iters):
 
 
 def test_demo_he_util(demo, math_env, tmp_path):
+    import subprocess
+    from test_gpu_cpp_facade import read_output, write_input
     N, m, o, sk, rk, x, s, cts = math_env
-    out = run(demo, "util", tmp_path, N, m, cts, rk, {})
+    inp, outp = str(tmp_path / "util.in"), str(tmp_path / "util.out")
+    write_input(inp, N, m, cts, rk, {})
+    txt = subprocess.check_output([demo, "util", inp, outp]).decode()
+    out = read_output(outp, N)
     (d0,) = hm.drop_chain_levels(o, [cts[0]], 2)
     d1, d2 = hm.reach_chain_level(o, [cts[1], cts[2]], d0)
     for g, e in zip(out, [d0, d1, d2]):
         same(g, e)
+    # SEAL's chain walk from the key level: key K-1, first K-2, ..., last 0, and
+    # key_context_data()->next_context_data() is first_context_data()
+    K = len(m)
+    chain = next(line for line in txt.splitlines() if line.startswith("chain"))
+    assert chain == "chain " + " ".join(str(i) for i in range(K - 1, -1, -1)) + " first %d key_next 1" % (K - 2)
 
 
 def test_demo_least_squares(demo, orc, tmp_path):

@@ -131,3 +131,29 @@ def test_server_flow_on_seeded_client_ciphertext(env, hecdna, tmp_path):
     data, scale, _, _ = hecdna.seal_ciphertext_load(outp.read_bytes())
     exp = e.o.rescale(e.o.relinearize(e.o.multiply(op1x, op2), e.rk_h))
     assert np.array_equal(data, exp.data) and scale == exp.scale
+
+
+def test_galois_keys_load_more_than_64_lists_both_modes(orc, hecdna):
+    """the device GaloisKeys loader accepts as many non-empty lists as there are Galois elements and as fit
+    in device memory, the same bound for an uncompressed and a zlib-compressed object (it used to reject more than 64
+    lists only when compressed).  80 keys at N = 2^10, every one loaded and used."""
+    N = 1 << 10
+    m = orc.Oracle.create_coeff_modulus(N, [40, 30, 40])
+    o = orc.Oracle(N, m)
+    sk = o.secret_key(61)
+    elts = [o.elt_from_step(s) for s in range(1, 81)]
+    gk_h = o.galois_keys(sk, elts, 62)
+    lists = [None] * N
+    for elt in elts:
+        lists[(elt - 1) // 2] = gk_h[elt]
+    ctx = hecdna.Context(N, m)
+    rng = np.random.default_rng(63)
+    a = orc.Ct(np.stack([np.stack([rng.integers(0, m[i], N, dtype=np.uint64) for i in range(2)]) for _ in range(2)]),
+               2.0**30)
+    for compr in (0, 1):
+        gk = hecdna.GaloisKeys(ctx)
+        gk.load_seal(sf.kswitch_keys(N, m, lists, compr=compr))
+        assert all(gk.has(elt) for elt in elts)
+        for step in (1, 37, 80):
+            g = ctx.rotate_vector(ctx.ciphertext(a.data, a.scale), step, gk)
+            assert np.array_equal(g.download(), o.rotate(a, step, gk_h).data), (compr, step)

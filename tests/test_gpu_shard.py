@@ -111,3 +111,81 @@ def test_cabi_sharded_null_planned_diagonal_rejected(env, hecdna):
     ref = e.ctx.matmul_diag_col(gA, gX, e.rk, e.gk)[0]           # the context is still usable
     got = e.ctx.matmul_diag_col_sharded(gA, gX, e.rk, e.gk)[0]
     assert np.array_equal(got.download(), ref.download())
+
+
+def _sharded_ops_worker(rank, world, port, q):
+    """One rank of hec_matmul_diag_col_sharded over a host communicator (gloo), its context on cuda:0."""
+    import os
+    import sys
+    import torch
+    import torch.distributed as dist
+    torch.cuda.is_available()
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from _helpers import load_hecdna, load_oracle
+    hec, orc = load_hecdna(), load_oracle()
+    import hecdna.shard as shard
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        e = Env(orc, hec, 1 << 11, [50, 36, 36, 50], seed=31)
+        n, p = 20, 3
+        A = [e.enc(seed=700 + j) for j in range(n)]
+        X = [e.enc(seed=800 + i) for i in range(p)]
+        exp = e.o.matmul_diag_col(A, X, e.rk_h, e.gk_h)
+        plan = shard.plan_diagonal_shards(e.N, n, world)
+        mine = set(plan[rank])
+        gA = [e.up(A[j]) if j in mine else None for j in range(n)]   # other ranks' diagonals: never read
+        gX = [e.up(x) for x in X]
+        e.ctx.comm_init_ops(rank, world, hec.HostComm())
+        res = []
+
+        def call(diags):
+            try:
+                got = e.ctx.matmul_diag_col_sharded(diags, gX, e.rk, e.gk)
+            except hec.InvalidArgument as ex:
+                return "EINVAL: " + str(ex)
+            return all(np.array_equal(g.download(), c.data) and g.scale == c.scale for g, c in zip(got, exp))
+        bad = list(gA)
+        if rank == world - 1:
+            bad[plan[rank][0]] = None                                  # fails its own checks
+        res.append(call(bad))
+        res.append(call(gA))                                           # the next call: bit-exact on every rank
+        other = list(gA)
+        if rank == world - 1:                                          # consistent within the rank, not across
+            other = [e.ctx.ciphertext(A[j].data, A[j].scale * (1 + 1e-6)) if j in mine else None for j in range(n)]
+        res.append(call(other))
+        res.append(call(gA))
+        q.put((rank, "ok", res))
+    except Exception as ex:  # surface the failure to the parent
+        q.put((rank, repr(ex), None))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_cabi_sharded_matvec_multirank_host_comm(world):
+    """hec_matmul_diag_col_sharded at world > 1 (each rank a process with its own context on
+    the one GPU, collectives through hec_comm_init_ops over gloo; RCCL refuses two ranks on one device): a rank that
+    fails its argument checks makes every rank raise invalid_argument without a hang, the next call is bit-exact
+    against the oracle's full matvec on every rank, a cross-rank scale mismatch is an error on every rank."""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_sharded_ops_worker, args=(r, world, port, q)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    res = sorted(q.get(timeout=240) for _ in procs)
+    for pr in procs:
+        pr.join(timeout=60)
+    assert all(r[1] == "ok" for r in res), res
+    last = world - 1
+    for rank, _, (r1, r2, r3, r4) in res:
+        assert r1.startswith("EINVAL") and (rank == last or "on rank %d" % last in r1), (rank, r1)
+        assert r2 is True and r4 is True, (rank, r2, r4)
+        assert r3 == "EINVAL: scale mismatch", (rank, r3)

@@ -250,3 +250,16 @@ def test_foreach_returns_the_visitors_status(hecdna):
         with pytest.raises(hecdna.HecError) as e:
             hecdna.seal_kswitch_keys_lists(b, visit_status=status)
         assert e.value.code == status and "rejected by the caller" in str(e.value)
+
+
+def test_context_free_key_limit_covers_cfg5_galois_keys(hecdna):
+    """the context-free key loaders' default decompression limit admits SEAL's default GaloisKeys at the
+    cfg5 size (N = 2^16, {60, 40 x 15, 60}: 2 log2 N - 1 = 31 lists of 16 PublicKeys of u64[2][17][N], plus at most
+    256 B of metadata per PublicKey and the list-length words), the largest key object BASELINE's configs load."""
+    N, K = 1 << 16, 17
+    L = K - 1
+    lists = 2 * 16 - 1
+    cfg5 = lists * L * (2 * K * N * 8 + 256) + N * 8 + 4096
+    assert cfg5 > 8.8e9
+    limit = hecdna.lib().hec_seal_kswitch_keys_default_limit()
+    assert cfg5 <= limit <= 1 << 36

@@ -148,3 +148,67 @@ def test_cpp_planner_equals_python(hecdna, N, n, world):
     import hecdna.shard as shard
     keys = shard.default_galois_elts(N)
     assert hecdna.plan_diagonal_shards(N, n, world, keys) == shard.plan_diagonal_shards(N, n, world, set(keys))
+
+
+def _agree_worker(rank, world, port, q):
+    import sys
+    import torch.distributed as dist
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__))))
+    from _helpers import load_hecdna
+    hec = load_hecdna()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        comm = hec.HostComm()
+        p, s = 3, 2.0**80
+        out = []
+        # 1. the last rank fails SEAL's checks: every rank returns its status
+        st = hec.HEC_EINVAL if rank == world - 1 else 0
+        out.append(hec.shard_agree(comm, rank, st, "scale out of bounds" if st else "", [s] * p))
+        # 2. all pass with equal scales
+        out.append(hec.shard_agree(comm, rank, 0, "", [s] * p))
+        # 3. all pass locally, but rank 0's product scale of output 1 differs (SEAL's add_inplace over the whole sum)
+        out.append(hec.shard_agree(comm, rank, 0, "", [s, s * (1 + 1e-9) if rank == 0 else s, s]))
+        # 4. two failing ranks (world >= 3: rank 1 invalid_argument, rank 2 logic_error): the larger code names it
+        st = {1: hec.HEC_EINVAL, 2: hec.HEC_ELOGIC}.get(rank, 0) if world >= 3 else 0
+        out.append(hec.shard_agree(comm, rank, st, {1: "bad one", 2: "bad two"}.get(rank, ""), [s] * p))
+        # 5. the protocol holds no state: the next agreement passes
+        out.append(hec.shard_agree(comm, rank, 0, "", [s] * p))
+        q.put((rank, "ok", out))
+    except Exception as e:  # surface the failure to the parent
+        q.put((rank, repr(e), None))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_cabi_shard_agree_gloo(hecdna, world):
+    """hec_matmul_diag_col_sharded's agreement step (hec_shard_agree over a host communicator,
+    the same code the RCCL path runs) at world > 1 on the CPU: a rank failing its argument checks makes every rank
+    return its status without a hang, a cross-rank scale mismatch is an invalid_argument on every rank, and the
+    next call agrees again."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_agree_worker, args=(r, world, port, q)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for pr in procs:
+        pr.join(timeout=60)
+    assert all(r[1] == "ok" for r in res), res
+    EINVAL, ELOGIC = hecdna.HEC_EINVAL, hecdna.HEC_ELOGIC
+    for rank, _, out in res:
+        (s1, m1), (s2, _), (s3, m3), (s4, m4), (s5, _) = out
+        assert s1 == EINVAL
+        assert m1 == ("scale out of bounds" if rank == world - 1 else
+                      "matmul_diag_col_sharded: the arguments failed SEAL's checks on rank %d" % (world - 1))
+        assert s2 == 0 and s5 == 0
+        assert (s3, m3) == (EINVAL, "scale mismatch")
+        if world >= 3:  # a failing rank keeps its own error; the others report the larger code (rank 2's)
+            assert (s4, m4) == {1: (EINVAL, "bad one"), 2: (ELOGIC, "bad two")}.get(
+                rank, (ELOGIC, "matmul_diag_col_sharded: the arguments failed SEAL's checks on rank 2"))
+        else:
+            assert s4 == 0
