@@ -129,13 +129,15 @@ def bench_seeds(rank, sharded):
     return {"relin": 11, "galois": 1000, "diag": 10_000, "col": 90_000 + (0 if sharded else 100 * rank)}
 
 
-def cpu_baseline(N, moduli, n, sample_diags, threads):
+def cpu_baseline(N, moduli, n, sample_diags, threads, data=None):
     """The oracle (the C++ restatement of the reference's SEAL path, kind "port"), built here with
     -march=native, timed on this host:
       all cores: ONE FULL matvec (all n diagonals, SEAL's per-rotation key switches, relinearize + rescale)
                  on `threads` threads (parallel over diagonal ranges, bit-identical partial sums);
       1 core:    the first `sample_diags` diagonals, extrapolated by key-switch count (labelled as such:
-                 a full 1-core cfg3 matvec takes ~15 minutes)."""
+                 a full 1-core cfg3 matvec takes ~15 minutes).
+    data (the GPU run's own inputs, downloaded: {"A": n diagonals, "X": [one input vector], "rk", "gk"}): the full
+    matvec runs on them and its output is returned, so the bench checks the bits it timed against the oracle."""
     import subprocess
     import tempfile
     build = tempfile.mkdtemp(prefix="orc_native_")
@@ -156,16 +158,22 @@ def cpu_baseline(N, moduli, n, sample_diags, threads):
         for i in range(K):
             k[:, :, i] = rng.integers(0, moduli[i], (L, 2, N), dtype=np.uint64)
         return k
-    elts = o.default_galois_elts()
-    gk = {e: rnd_key() for e in elts}
-    rk = rnd_key()
-    A = [rnd_ct() for _ in range(8)]   # n diagonals cycle over 8 distinct ciphertexts (data-oblivious timing)
-    X = [rnd_ct()]
+    if data is not None:
+        A = [orc.Ct(a, 2.0**40) for a in data["A"]]
+        X = [orc.Ct(x, 2.0**40) for x in data["X"]]
+        rk, gk = data["rk"], data["gk"]
+    else:
+        elts = o.default_galois_elts()
+        gk = {e: rnd_key() for e in elts}
+        rk = rnd_key()
+        A = [rnd_ct() for _ in range(8)]   # n diagonals cycle over 8 distinct ciphertexts (data-oblivious timing)
+        X = [rnd_ct()]
     from _helpers import ks_count
     ks_sample = ks_count(N, sample_diags)
-    full = o.bench_matvec(A, n, X, rk, gk, nthreads=threads)
+    full, outs = o.bench_matvec(A, n, X, rk, gk, nthreads=threads, outputs=True)
     one = o.bench_matvec(A, n, X, rk, gk, nthreads=1, j_end=sample_diags, finish=False)
-    return {"full_s": full, "one_core_s": one * ks_total(N, n) / ks_sample, "ks_sample": ks_sample}
+    return {"full_s": full, "one_core_s": one * ks_total(N, n) / ks_sample, "ks_sample": ks_sample,
+            "outputs": [c.data for c in outs]}
 
 
 def run_cfg2(args, hec, world, rank, local, barrier, max_over_ranks):
@@ -202,6 +210,20 @@ def run_cfg2(args, hec, world, rank, local, barrier, max_over_ranks):
     ctx.synchronize()
     barrier()
     dt = max_over_ranks(time.perf_counter() - t0)
+
+    # self-check of the timed outputs, after the timer: three outputs of the last timed step, one
+    # from each concurrent lane, recomputed as ONE single-stream call with just those vectors (another batch split and
+    # schedule) must equal them bit for bit; the one-lane profile step below and, on rank 0 at N = 1, the CPU leg's
+    # oracle matvec of input vector 0 are compared with them too
+    check = None
+    if not sharded:
+        keep = sorted({0, args.batch // 2, args.batch - 1})
+        saved = [(outs[i].download(), outs[i].info()) for i in keep]
+        alone = (ctx.matmul_diagpt_col(diags, [cols[i] for i in keep], gk) if ctpt else
+                 ctx.matmul_diag_col(diags, [cols[i] for i in keep], rk, gk))
+        same = [bool(np.array_equal(a.download(), d) and a.info() == inf) for a, (d, inf) in zip(alone, saved)]
+        del alone
+        check = {"outputs_checked": keep, "single_call_bitexact": all(same)}
     limb_ntts = 2 * nl * npolys * args.steps * world
     kernels, roof = {}, None
     if not args.no_profile:
@@ -473,6 +495,9 @@ def main():
         prof_classes = ctx.profile_classes()
         prof_ex = {c: ctx.profile_read_ex(c) for c in prof_classes}
         ctx.profile(0)
+        if check is not None:  # the profile step ran the whole batch as one lane into the same outputs
+            check["one_lane_step_bitexact"] = all(np.array_equal(outs[i].download(), d) and outs[i].info() == inf
+                                                  for i, (d, inf) in zip(check["outputs_checked"], saved))
 
     # per-kernel table and roofline.  Every kernel launch of the profile step sits in a "k:<kernel>/<role>"
     # scope that carries its algorithmic bytes (compulsory reads + writes of that kernel given the engine's
@@ -511,11 +536,20 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not ctpt:
         model, host_cpus, share, threads, why = cpu_info()
-        res = cpu_baseline(N, moduli, args.n, args.cpu_sample_diags, threads)
+        # the GPU run's own inputs: every diagonal, input vector 0, the relinearization and Galois keys
+        data = {"A": [d.download() for d in diags], "X": [cols[0].download()], "rk": rk.download(),
+                "gk": {e: gk.download(e) for e in elts}}
+        res = cpu_baseline(N, moduli, args.n, args.cpu_sample_diags, threads, data=data)
+        del data
+        if check is not None:
+            d0, (size0, level0, scale0) = saved[0]
+            check["oracle_outputs_checked"] = [0]
+            check["oracle_bitexact"] = bool(np.array_equal(res["outputs"][0], d0))
         cpu = {"value": round(1.0 / res["full_s"], 6), "unit": "matvec/s", "cores": threads, "kind": "port",
                "sample": f"one full n={args.n} N=2^{args.logn} L={L} diag x col matvec ({ks} key switches, SEAL's "
                          f"per-rotation schedule, relinearize + rescale) by the oracle (C++ SEAL-semantics port, "
-                         f"-march=native) on {threads} threads",
+                         f"-march=native) on {threads} threads, on the GPU run's own diagonals, keys and input "
+                         f"vector 0 (its output is compared with the GPU's bit for bit: self_check)",
                "cpu_model": model, "host_cpus": host_cpus, "cpus_available": share, "cores_reason": why,
                "cgroup_cpu_quota": cgroup_cpu_quota(),
                "full_matvec_s": round(res["full_s"], 2),
@@ -523,6 +557,12 @@ def main():
                             "sample": f"diagonals j<{args.cpu_sample_diags} ({res['ks_sample']} key switches) "
                                       f"on 1 thread, scaled to {ks} key switches"}}
 
+    if check is not None:
+        check["bitexact"] = all(v for k, v in check.items() if k.endswith("bitexact"))
+        if dist is not None:  # every rank checked its own outputs
+            t = torch.tensor([0.0 if check["bitexact"] else 1.0], dtype=torch.float64, device=f"cuda:{local}")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            check["all_ranks_bitexact"] = float(t.item()) == 0.0
     algo_mv = algorithmic_bytes_per_matvec(N, L, args.n, args.batch, ks)
     if rank == 0:
         line = {
@@ -544,6 +584,7 @@ def main():
                                               "key sums KW, galois_negw / galois_kw) are built once per key "
                                               "and level before the timed steps, like the keys themselves"},
             "roofline": roof,
+            "self_check": check,
             "sharded": sharded_extra,
             "kernels_one_step": kernels,
             "cpu_baseline": cpu,
@@ -557,6 +598,10 @@ def main():
         print(json.dumps(line))
     if dist is not None:
         dist.destroy_process_group()
+    if check is not None and not (check["bitexact"] and check.get("all_ranks_bitexact", True)):
+        print("bench.py: self-check: the timed outputs are NOT bit-exact (single call / one-lane step / oracle)",
+              file=sys.stderr)
+        sys.exit(1)
     if sharded_extra is not None and "self_check" in sharded_extra and not sharded_extra["self_check"]["bitexact"]:
         # a sharded step whose outputs differ from the 1-rank matvec is no valid measurement: fail the run
         print("bench.py: sharded self-check is NOT bit-exact against the 1-rank matvec", file=sys.stderr)

@@ -78,6 +78,8 @@ def lib():
             "hec_kswitch_key_upload": [vp, u64p, C.POINTER(vp)],
             "hec_kswitch_key_fill_uniform": [vp, C.c_uint64, C.POINTER(vp)],
             "hec_kswitch_key_destroy": [vp],
+            "hec_kswitch_key_download": [vp, u64p],
+            "hec_galois_keys_download": [vp, C.c_uint32, u64p],
             "hec_galois_keys_create": [vp, C.POINTER(vp)],
             "hec_galois_keys_add": [vp, C.c_uint32, u64p],
             "hec_galois_keys_add_uniform": [vp, C.c_uint32, C.c_uint64],
@@ -799,6 +801,13 @@ class KSwitchKey:
             _check(lib().hec_kswitch_key_fill_uniform(ctx.h, int(seed or 0), C.byref(h)))
         self.h = h
 
+    def download(self):
+        """u64[L][2][K][N] (hec_kswitch_key_download)"""
+        c = self.ctx
+        a = np.empty((c.L, 2, c.K, c.N), dtype=np.uint64)
+        _check(lib().hec_kswitch_key_download(self.h, _p(a)))
+        return a
+
     def __del__(self):
         try:
             if self.h:
@@ -824,6 +833,13 @@ class GaloisKeys:
 
     def has(self, elt):
         return bool(lib().hec_galois_keys_has(self.h, int(elt)))
+
+    def download(self, elt):
+        """the key of one Galois element, u64[L][2][K][N] (hec_galois_keys_download)"""
+        c = self.ctx
+        a = np.empty((c.L, 2, c.K, c.N), dtype=np.uint64)
+        _check(lib().hec_galois_keys_download(self.h, int(elt), _p(a)))
+        return a
 
     def load_seal(self, b: bytes):
         """GaloisKeys::load(context, in, size): every key list of a SEAL-serialized GaloisKeys."""

@@ -1489,6 +1489,9 @@ int hec_context_create(uint64_t N, const uint64_t *mod, uint64_t K, int device, 
                 c.ql_inv_q[l].push_back(shoupq(v, q));
                 c.ql_half_mod[l].push_back((ql >> 1) % q);
             }
+        // the tables went up with blocking copies on the null stream, which the non-blocking context stream does
+        // not wait for: finish them before any kernel can read them
+        HEC_HIP(hipDeviceSynchronize());
         *out = ctx;
     });
 }
@@ -1981,8 +1984,21 @@ int hec_kswitch_key_upload(hec_context *ctx, const uint64_t *host, hec_kswitch_k
         auto *k = new hec_kswitch_key();
         k->ctx = ctx;
         k->d = dalloc(key_words(ctx->c));
-        HEC_HIP(hipMemcpy(k->d, host, key_words(ctx->c) * sizeof(u64), hipMemcpyHostToDevice));
+        // on the context stream, drained before the host buffer may go (a pageable hipMemcpy on the null stream is
+        // not ordered with the non-blocking context stream)
+        HEC_HIP(hipMemcpyAsync(k->d, host, key_words(ctx->c) * sizeof(u64), hipMemcpyHostToDevice, ctx->c.stream));
+        HEC_HIP(hipStreamSynchronize(ctx->c.stream));
         *out = k;
+    });
+}
+int hec_kswitch_key_download(const hec_kswitch_key *key, uint64_t *host)
+{
+    return guard([&] {
+        need(key && host, "null argument");
+        set_device(key->ctx);
+        Ctx &c = key->ctx->c;
+        HEC_HIP(hipMemcpyAsync(host, key->d, key_words(c) * sizeof(u64), hipMemcpyDeviceToHost, c.stream));
+        HEC_HIP(hipStreamSynchronize(c.stream));
     });
 }
 int hec_kswitch_key_fill_uniform(hec_context *ctx, uint64_t seed, hec_kswitch_key **out)
@@ -2028,10 +2044,24 @@ int hec_galois_keys_add(hec_galois_keys *gk, uint32_t elt, const uint64_t *host)
         Ctx &c = gk->ctx->c;
         set_device(gk->ctx);
         gk_check_elt(c, elt);
+        HEC_HIP(hipStreamSynchronize(c.stream));  // a replaced key may still be read by enqueued work
         u64 *&d = gk->keys[elt];
         if (!d) d = dalloc(key_words(c));
         gk->drop_kw(elt);
-        HEC_HIP(hipMemcpy(d, host, key_words(c) * sizeof(u64), hipMemcpyHostToDevice));
+        HEC_HIP(hipMemcpyAsync(d, host, key_words(c) * sizeof(u64), hipMemcpyHostToDevice, c.stream));
+        HEC_HIP(hipStreamSynchronize(c.stream));
+    });
+}
+int hec_galois_keys_download(const hec_galois_keys *gk, uint32_t elt, uint64_t *host)
+{
+    return guard([&] {
+        need(gk && host, "null argument");
+        set_device(gk->ctx);
+        Ctx &c = gk->ctx->c;
+        const auto it = gk->keys.find(elt);
+        need(it != gk->keys.end(), "Galois key not present");
+        HEC_HIP(hipMemcpyAsync(host, it->second, key_words(c) * sizeof(u64), hipMemcpyDeviceToHost, c.stream));
+        HEC_HIP(hipStreamSynchronize(c.stream));
     });
 }
 int hec_galois_keys_add_uniform(hec_galois_keys *gk, uint32_t elt, uint64_t seed)
@@ -2041,6 +2071,7 @@ int hec_galois_keys_add_uniform(hec_galois_keys *gk, uint32_t elt, uint64_t seed
         Ctx &c = gk->ctx->c;
         set_device(gk->ctx);
         gk_check_elt(c, elt);
+        HEC_HIP(hipStreamSynchronize(c.stream));
         u64 *&d = gk->keys[elt];
         if (!d) d = dalloc(key_words(c));
         gk->drop_kw(elt);

@@ -119,11 +119,16 @@ int hec_encode_scalar(hec_context *ctx, double value, double scale, uint64_t lev
 /* ---------------------------------------------------------------- keys -------------------- */
 /* RelinKeys (KeyGenerator::create_relin_keys, matrix_operations.cpp:1061-1062): data u64[L][2][K][N] */
 int hec_kswitch_key_upload(hec_context *ctx, const uint64_t *host, hec_kswitch_key **out);
+/* device -> host in the layout of hec_kswitch_key_upload (synchronises) */
+int hec_kswitch_key_download(const hec_kswitch_key *key, uint64_t *host);
 int hec_kswitch_key_fill_uniform(hec_context *ctx, uint64_t seed, hec_kswitch_key **out);
 int hec_kswitch_key_destroy(hec_kswitch_key *key);
 /* GaloisKeys (KeyGenerator::create_galois_keys, matrix_operations.cpp:1063-1064) */
 int hec_galois_keys_create(hec_context *ctx, hec_galois_keys **out);
 int hec_galois_keys_add(hec_galois_keys *gk, uint32_t galois_elt, const uint64_t *host);
+/* one Galois key, device -> host in the layout of hec_galois_keys_add (synchronises); HEC_EINVAL "Galois key not
+ * present" when the set has no key for galois_elt */
+int hec_galois_keys_download(const hec_galois_keys *gk, uint32_t galois_elt, uint64_t *host);
 int hec_galois_keys_add_uniform(hec_galois_keys *gk, uint32_t galois_elt, uint64_t seed);
 int hec_galois_keys_has(const hec_galois_keys *gk, uint32_t galois_elt);
 int hec_galois_keys_destroy(hec_galois_keys *gk);

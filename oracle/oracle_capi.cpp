@@ -359,9 +359,10 @@ int orc_matmul_diagpt_col_set(void *c, const u64 *pts, u64 level, double pscale,
 // rescale) of n diagonals over X, timed with steady_clock around the call as the reference's Timer does
 // (tic_toc.h:20-28).  The n diagonals cycle over the nA distinct ones given (every step is data-oblivious, so
 // the time equals that of n distinct ciphertexts without n copies in memory).  j range [j_begin, j_end).
+// out (may be NULL): the p results, so a benchmark run also checks the bits it timed (bench.py's CPU leg)
 int orc_bench_matvec(void *c, const OrcCt *A, u64 nA, u64 n, const OrcCt *X, u64 p, const u64 *rk, const u32 *elts,
                      const u64 *const *keys, u64 nkeys, int nthreads, u64 j_begin, u64 j_end, int finish,
-                     double *seconds)
+                     double *seconds, OrcCt *out)
 {
     return guard([&] {
         auto &ctx = *static_cast<Context *>(c);
@@ -372,6 +373,8 @@ int orc_bench_matvec(void *c, const OrcCt *A, u64 nA, u64 n, const OrcCt *X, u64
         const auto t0 = std::chrono::steady_clock::now();
         auto r = matmul_diag_col(ctx, diag, ptrs(x), view(rk), gk, nthreads, j_begin, j_end, finish != 0);
         *seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        if (out)
+            for (u64 i = 0; i < p; ++i) out_ct(r[i], out + i);
     });
 }
 int orc_matmul_col_colT(void *c, const OrcCt *A, u64 n, const OrcCt *B, u64 p, const u64 *rk, const u32 *elts,

@@ -374,15 +374,31 @@ class Oracle:
                                                C.c_int(nthreads), C.c_int(int(finish))))
         return self._outs(outs, len(X))
 
-    def bench_matvec(self, A, n, X, rk, gk, nthreads=1, j_begin=0, j_end=None, finish=True):
-        """Seconds for one diag x col matvec of n diagonals (cycling over the distinct A) over X (C++ timer)."""
-        a, ab = self._many(A)
-        x, xb = self._many(X)
+    def _views(self, cts):
+        """OrcCt records pointing at the callers' own C-contiguous u64 arrays (inputs the C side copies in): no
+        padded host copy, which matters for the 21.5 GB of cfg3 diagonals"""
+        arr = (OrcCt * len(cts))()
+        keep = []
+        for i, c in enumerate(cts):
+            d = np.ascontiguousarray(c.data, dtype=np.uint64)
+            keep.append(d)
+            arr[i] = OrcCt(_p(d), c.size, c.level, c.scale)
+        return arr, keep
+
+    def bench_matvec(self, A, n, X, rk, gk, nthreads=1, j_begin=0, j_end=None, finish=True, outputs=False):
+        """Seconds for one diag x col matvec of n diagonals (cycling over the distinct A) over X (C++ timer);
+        outputs=True: (seconds, the results)."""
+        a, ab = self._views(A)
+        x, xb = self._views(X)
         secs = C.c_double()
+        lvl = X[0].level
+        outs, ob = self._many([Ct(np.zeros((3, lvl, self.N), np.uint64), 1.0) for _ in X]) if outputs else (None, None)
         _check(lib().orc_bench_matvec(self.h, a, C.c_uint64(len(A)), C.c_uint64(n), x, C.c_uint64(len(X)), _p(rk),
                                       *self._gk(gk), C.c_int(nthreads), C.c_uint64(j_begin),
                                       C.c_uint64(n if j_end is None else j_end), C.c_int(int(finish)),
-                                      C.byref(secs)))
+                                      C.byref(secs), outs))
+        if outputs:
+            return secs.value, self._outs(outs, len(X))
         return secs.value
 
     def matmul_col_colT(self, A, B, p, rk, gk, nthreads=1):
