@@ -119,7 +119,7 @@ def test_demo_he_util(demo, math_env, tmp_path):
     # SEAL's chain walk from the key level: key K-1, first K-2, ..., last 0, and
     # key_context_data()->next_context_data() is first_context_data()
     K = len(m)
-    chain = next(line for line in txt.splitlines() if line.startswith("chain"))
+    chain = next(line for line in txt.splitlines() if line.startswith("chain "))
     assert chain == "chain " + " ".join(str(i) for i in range(K - 1, -1, -1)) + " first %d key_next 1" % (K - 2)
 
 
