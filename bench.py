@@ -211,19 +211,6 @@ def run_cfg2(args, hec, world, rank, local, barrier, max_over_ranks):
     barrier()
     dt = max_over_ranks(time.perf_counter() - t0)
 
-    # self-check of the timed outputs (VERDICT r04 item 2), after the timer: three outputs of the last timed step, one
-    # from each concurrent lane, recomputed as ONE single-stream call with just those vectors (another batch split and
-    # schedule) must equal them bit for bit; the one-lane profile step below and, on rank 0 at N = 1, the CPU leg's
-    # oracle matvec of input vector 0 are compared with them too
-    check = None
-    if not sharded:
-        keep = sorted({0, args.batch // 2, args.batch - 1})
-        saved = [(outs[i].download(), outs[i].info()) for i in keep]
-        alone = (ctx.matmul_diagpt_col(diags, [cols[i] for i in keep], gk) if ctpt else
-                 ctx.matmul_diag_col(diags, [cols[i] for i in keep], rk, gk))
-        same = [bool(np.array_equal(a.download(), d) and a.info() == inf) for a, (d, inf) in zip(alone, saved)]
-        del alone
-        check = {"outputs_checked": keep, "single_call_bitexact": all(same)}
     limb_ntts = 2 * nl * npolys * args.steps * world
     kernels, roof = {}, None
     if not args.no_profile:
@@ -434,6 +421,20 @@ def main():
     ctx.synchronize()
     barrier()
     dt = max_over_ranks(time.perf_counter() - t0)
+
+    # self-check of the timed outputs (VERDICT r04 item 2), after the timer: three outputs of the last timed step, one
+    # from each concurrent lane, recomputed as ONE single-stream call with just those vectors (another batch split and
+    # schedule) must equal them bit for bit; the one-lane profile step below and, on rank 0 at N = 1, the CPU leg's
+    # oracle matvec of input vector 0 are compared with them too
+    check = None
+    if not sharded:
+        keep = sorted({0, args.batch // 2, args.batch - 1})
+        saved = [(outs[i].download(), outs[i].info()) for i in keep]
+        alone = (ctx.matmul_diagpt_col(diags, [cols[i] for i in keep], gk) if ctpt else
+                 ctx.matmul_diag_col(diags, [cols[i] for i in keep], rk, gk))
+        same = [bool(np.array_equal(a.download(), d) and a.info() == inf) for a, (d, inf) in zip(alone, saved)]
+        del alone
+        check = {"outputs_checked": keep, "single_call_bitexact": all(same)}
 
     ms_per_step = dt / args.steps * 1e3
     total = args.batch * (1 if sharded else world) * args.steps
