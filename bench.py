@@ -291,9 +291,10 @@ def main():
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--batch", type=int, default=192,
-                    help="input vectors per GPU per step (p); the engine runs them as 3 concurrent lanes of 64 "
-                         "(round 4 sweep, profiles/r04i_*, r04j_*: 10.62 matvec/s at 192 vs 10.38 at 96 and 10.64 at "
-                         "288; 384 does not fit the workspaces in 288 GB)")
+                    help="input vectors per GPU per step (p), run as one batch on the context stream (round 4 sweep, "
+                         "profiles/r04i_*, r04j_*: 10.62 matvec/s at 192 vs 10.38 at 96 and 10.64 at 288; 384 does not "
+                         "fit the workspaces in 288 GB; HEC_LANES=3 splits it into 3 concurrent lanes, +1.3 %, "
+                         "profiles/r05b_lanes_ab.json)")
     ap.add_argument("--n", type=int, default=4096, help="matrix dimension (diagonals)")
     ap.add_argument("--logn", type=int, default=15)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -321,7 +322,7 @@ def main():
     if args.config == "cfg5":
         args.logn, args.n = 16, 1024
         if args.batch == ap.get_default("batch"):
-            args.batch = 64  # 2 lanes of 32 (round 4, profiles/r04p_*: 9.93 columns/s vs 9.80 at 32, 9.92 at 48)
+            args.batch = 64  # round 4, profiles/r04p_*: 9.93 columns/s vs 9.80 at 32, 9.92 at 48
     if args.config == "cfg2" and args.batch == ap.get_default("batch"):
         args.batch = 64  # 168 MB per buffer, inside the Infinity Cache: 3.20 M limb-NTT/s vs 2.94 M at 128 (r04p)
 
@@ -422,10 +423,10 @@ def main():
     barrier()
     dt = max_over_ranks(time.perf_counter() - t0)
 
-    # self-check of the timed outputs, after the timer: three outputs of the last timed step, one
-    # from each concurrent lane, recomputed as ONE single-stream call with just those vectors (another batch split and
-    # schedule) must equal them bit for bit; the one-lane profile step below and, on rank 0 at N = 1, the CPU leg's
-    # oracle matvec of input vector 0 are compared with them too
+    # self-check of the timed outputs, after the timer: three outputs of the last timed step (the
+    # first, middle and last vector of the batch), recomputed as ONE call with just those three vectors (another batch
+    # size, so other grids and tilings) must equal them bit for bit; the profile step below (a rerun of the batch) and,
+    # on rank 0 at N = 1, the CPU leg's oracle matvec of input vector 0 on the same inputs are compared with them too
     check = None
     if not sharded:
         keep = sorted({0, args.batch // 2, args.batch - 1})
@@ -496,8 +497,8 @@ def main():
         prof_classes = ctx.profile_classes()
         prof_ex = {c: ctx.profile_read_ex(c) for c in prof_classes}
         ctx.profile(0)
-        if check is not None:  # the profile step ran the whole batch as one lane into the same outputs
-            check["one_lane_step_bitexact"] = all(np.array_equal(outs[i].download(), d) and outs[i].info() == inf
+        if check is not None:  # the profile step reran the whole batch into the same outputs
+            check["profile_step_bitexact"] = all(np.array_equal(outs[i].download(), d) and outs[i].info() == inf
                                                   for i, (d, inf) in zip(check["outputs_checked"], saved))
 
     # per-kernel table and roofline.  Every kernel launch of the profile step sits in a "k:<kernel>/<role>"
@@ -592,15 +593,16 @@ def main():
             "whole_step_algorithmic_GBps": round(algo_mv * total / dt / 1e9, 2),
             "breakdown_ms_one_step": breakdown,
             "profile_schedule": (None if args.no_profile else
-                                 f"one extra untimed step after the timed ones, the batch of {args.batch} as ONE lane "
-                                 f"on the context stream (profiling turns the concurrent lanes off so each launch "
-                                 f"has the GPU to itself); asynchronous HIP event pairs per launch"),
+                                 f"one extra untimed step after the timed ones, the batch of {args.batch} as one lane "
+                                 f"on the context stream (the default schedule; with HEC_LANES > 1 profiling turns the "
+                                 f"concurrent lanes off so each launch has the GPU to itself); asynchronous HIP event "
+                                 f"pairs per launch"),
         }
         print(json.dumps(line))
     if dist is not None:
         dist.destroy_process_group()
     if check is not None and not (check["bitexact"] and check.get("all_ranks_bitexact", True)):
-        print("bench.py: self-check: the timed outputs are NOT bit-exact (single call / one-lane step / oracle)",
+        print("bench.py: self-check: the timed outputs are NOT bit-exact (single call / profile step / oracle)",
               file=sys.stderr)
         sys.exit(1)
     if sharded_extra is not None and "self_check" in sharded_extra and not sharded_extra["self_check"]["bitexact"]:

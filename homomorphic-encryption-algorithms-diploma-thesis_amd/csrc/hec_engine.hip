@@ -989,14 +989,10 @@ hec_context *make_lane(hec_context *parent)
     c.prof_pend.clear();
     c.ev_pool.clear();
     c.ev_used = 0;
-    c.stream = c.side = nullptr;
-    c.ev_fork = c.ev_join = nullptr;
+    c.stream = nullptr;
     c.zflag = nullptr;
     HEC_HIP(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
     c.own_stream = true;
-    HEC_HIP(hipStreamCreateWithFlags(&c.side, hipStreamNonBlocking));
-    HEC_HIP(hipEventCreateWithFlags(&c.ev_fork, hipEventDisableTiming));
-    HEC_HIP(hipEventCreateWithFlags(&c.ev_join, hipEventDisableTiming));
     HEC_HIP(hipMalloc(&c.zflag, sizeof(int)));
     HEC_HIP(hipEventCreateWithFlags(&l->lane_done, hipEventDisableTiming));
     return l;
@@ -1009,9 +1005,6 @@ void free_lane(hec_context *l)
     c.ws.release();
     (void)hipFree(c.zflag);
     (void)hipStreamDestroy(c.stream);
-    (void)hipStreamDestroy(c.side);
-    (void)hipEventDestroy(c.ev_fork);
-    (void)hipEventDestroy(c.ev_join);
     delete l;
 }
 
@@ -1373,9 +1366,6 @@ int hec_context_create(uint64_t N, const uint64_t *mod, uint64_t K, int device, 
         for (u64 q : c.q) c.bits.push_back(64 - __builtin_clzll(q));
         HEC_HIP(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
         c.own_stream = true;
-        HEC_HIP(hipStreamCreateWithFlags(&c.side, hipStreamNonBlocking));
-        HEC_HIP(hipEventCreateWithFlags(&c.ev_fork, hipEventDisableTiming));
-        HEC_HIP(hipEventCreateWithFlags(&c.ev_join, hipEventDisableTiming));
         std::vector<ulonglong2> tw(K * N), itw(K * N);
         std::vector<u64> psipow(K * 2 * N);  // hoisted mod-up: psi_i^e, e in [0, 2N)
         for (uint64_t i = 0; i < K; ++i) {
@@ -1520,9 +1510,6 @@ int hec_context_destroy(hec_context *ctx)
         (void)hipFree(c.enc_map);
         (void)hipFree(c.enc_tw);
         if (c.own_stream) (void)hipStreamDestroy(c.stream);
-        (void)hipStreamDestroy(c.side);
-        (void)hipEventDestroy(c.ev_fork);
-        (void)hipEventDestroy(c.ev_join);
         for (hipEvent_t e : c.ev_pool) (void)hipEventDestroy(e);
         delete ctx;
     });

@@ -51,8 +51,6 @@ struct Ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     bool own_stream = false;
-    hipStream_t side = nullptr;                 // second stream for concurrent kernels inside a call
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     std::size_t N = 0;
     int logN = 0;
     std::size_t K = 0, L = 0;
@@ -93,7 +91,10 @@ struct Ctx {
                                    // (1: INTT pass B, then the fan-out finishes the INTT and lists the zeros)
     int hmac_odd3 = 1;             // HEC_HMAC_ODD3=0: an odd sibling group ends in a pair and a single-child launch
     bool fan_out = true;           // HEC_FAN=0: separate INTT pass A (fan-out fuses it into the forward passes A)
-    int lanes = 3;                 // HEC_LANES: concurrent batch lanes of a matvec (hec_engine.hip matvec_lanes)
+    // HEC_LANES: concurrent batch lanes of a matvec (hec_engine.hip matvec_lanes).  Opt-in since round 5: one lane
+    // (the whole batch on the context's stream) is the default; 3 lanes measured +1.3 % at the bench's B = 192
+    // (profiles/r05b_lanes_ab.json) but share the only unexplained full-size bit mismatch of rounds 2 and 4
+    int lanes = 1;
     int lane_min_batch = 16;       // input vectors per lane at least
     bool fuse_galois = true;       // HEC_FUSE_GALOIS=0: materialise apply_galois before the key switch
     bool fused_modup_mac = true;  // HEC_FUSED_MODUP_MAC=0: separate mod-up pass B and key MAC kernels

@@ -273,10 +273,18 @@ def test_matvec_batched_equals_single_and_oracle(env11):
     e.same(one, exp[1])
 
 
-def test_matvec_batch_lanes_bitexact(env11):
-    """A batch of >= 32 vectors runs as concurrent lanes (one host thread, HIP stream and workspace per
-    lane, hec_engine.hip matvec_lanes): 48 columns -> 3 lanes of 16; every output equals the oracle's."""
-    e = env11
+@pytest.fixture
+def lanes3(env11):
+    """The opt-in concurrent batch lanes (hec_context_set_option "lanes"; the default is one lane since round 5)."""
+    env11.ctx.set_option("lanes", 3)
+    yield env11
+    env11.ctx.set_option("lanes", 1)
+
+
+def test_matvec_batch_lanes_bitexact(lanes3):
+    """With lanes on, a batch of >= 32 vectors runs as concurrent lanes (one host thread, HIP stream and workspace
+    per lane, hec_engine.hip matvec_lanes): 48 columns -> 3 lanes of 16; every output equals the oracle's."""
+    e = lanes3
     n = 10
     A = [e.enc(seed=3000 + j) for j in range(n)]
     X = [e.enc(seed=3100 + i) for i in range(48)]
@@ -305,6 +313,7 @@ def test_lane_workspace_growth_while_lanes_run(orc, hecdna):
     from its own host thread while the other lanes are launching (the round-2 lane hazard); then the small shape
     again (the outgrown bases were reclaimed after the lanes joined).  Every output equals the oracle's."""
     e = Env(orc, hecdna, 1 << 11, [50, 36, 36, 50], seed=5151)
+    e.ctx.set_option("lanes", 3)
     X = [e.enc(seed=5000 + i) for i in range(48)]
     gX = [e.up(x) for x in X]
     for n in (3, 24, 3):
@@ -452,9 +461,9 @@ def test_matvec_ct_x_pt_bitexact(request, which, n):
         e.same(g, c)
 
 
-def test_matvec_ct_x_pt_batch_lanes(env11):
-    """The ct x pt form over 40 vectors (2 concurrent lanes of 20) equals the oracle's SEAL flow."""
-    e = env11
+def test_matvec_ct_x_pt_batch_lanes(lanes3):
+    """The ct x pt form over 40 vectors (with lanes on: 2 concurrent lanes of 20) equals the oracle's SEAL flow."""
+    e = lanes3
     L = len(e.m) - 1
     pscale = 2.0**40
     P = [e.o.encode(e.rng.uniform(-1, 1, e.N // 2), pscale, L) for _ in range(7)]
