@@ -738,8 +738,9 @@ void walk_trie_hoisted(Ctx &c, Scratch &s, const RotTrie &t, int node, PolyArr s
     const Hoist &h = hs[depth];
     hoist_node(c, src, B, l, h);
     const u64 N = c.N;
-    // children in groups of up to `sup` siblings: one sibling-fused k_hmacm launch per hoisted_group() of them,
-    // accumulators h.acc(q), contiguous; then the mod-downs in groups of HOIST_GROUP share their small launches
+    // children in groups of up to `sup` siblings: one sibling-fused k_hmacm launch per hoisted_group() of them (the
+    // default hmac_cfg 2: the whole group, slots of 2; 1: per pair), accumulators h.acc(q), contiguous; then the
+    // mod-downs in groups of HOIST_GROUP share their small launches
     const std::size_t grp = (std::size_t)hoisted_group(c);
     const std::size_t sup = std::max<std::size_t>(grp, HOIST_GROUP / grp * grp);
     // the sibling-fused MAC folds the node's c0 into the children's accumulators (X0 P mod q_I), so their
@@ -763,7 +764,9 @@ void walk_trie_hoisted(Ctx &c, Scratch &s, const RotTrie &t, int node, PolyArr s
             ProfScope ps(c, "ks_hmac");  // digits E (B l^2) + c1 (B l) [+ c0 (B l), folded] + per child
             ProfScope k(c, "k:k_hmacm",
                         (double)B * (l * l + l + (fold ? l : 0)) + nk * (2.0 * l * K + 3.0 * K + 2.0 * B * K));
-            if (nk == 3 && grp == 2)
+            if (c.hmac_cfg == 2)
+                hoisted_mac_group(c, PolyArr{src.p + src.sk, src.sb, 0}, X0, h.E, h.zl, kids + q0, nk, B, l);
+            else if (nk == 3 && grp == 2)
                 hoisted_mac_3(c, PolyArr{src.p + src.sk, src.sb, 0}, X0, h.E, h.zl, kids + q0, B, l);
             else hoisted_mac_multi(c, PolyArr{src.p + src.sk, src.sb, 0}, X0, h.E, h.zl, kids + q0, nk, B, l);
         }

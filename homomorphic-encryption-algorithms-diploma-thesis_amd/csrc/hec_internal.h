@@ -86,7 +86,8 @@ struct Ctx {
     int tensor_defer_bufs = 8;     // HEC_TENSOR_BUFS: rotation buffers per trie depth
     bool hoist = true;             // HEC_HOIST=0: no hoisted mod-up in the rotation trie walk
     int hoist_min_children = 2;    // HEC_HOIST_MIN: children a trie node needs to be hoisted
-    int hmac_cfg = 1;              // HEC_HMAC=0: one hoisted MAC per child (1: sibling pairs fused, k_hmacm)
+    int hmac_cfg = 2;              // HEC_HMAC: 2 a sibling group per k_hmacm launch (slots of 2 children), 1 one
+                                   // launch per sibling pair (round 4), 0 one hoisted MAC per child
     int hoist_scan = 1;            // HEC_HOIST_SCAN=0: hoisted node as INTT pass B, pass A, k_zscan, direct fan-out
                                    // (1: INTT pass B, then the fan-out finishes the INTT and lists the zeros)
     int hmac_odd3 = 1;             // HEC_HMAC_ODD3=0: an odd sibling group ends in a pair and a single-child launch
@@ -169,6 +170,9 @@ void hoisted_mac_multi(Ctx &c, PolyArr X1, PolyArr X0, const u64 *E, const int *
                        int B, int l);
 // three children in one sibling-fused launch (3 x 4 FP64 / 3 x 2 integer batch entries per thread)
 void hoisted_mac_3(Ctx &c, PolyArr X1, PolyArr X0, const u64 *E, const int *zl, const HChildSpec *kids, int B, int l);
+// a whole sibling group (up to HMAC_MAX_CHILDREN) in one launch: slots of 2 children, the digit tile shared through L2
+void hoisted_mac_group(Ctx &c, PolyArr X1, PolyArr X0, const u64 *E, const int *zl, const HChildSpec *kids, int nkids,
+                       int B, int l);
 int hoisted_group(const Ctx &c);  // children per hoisted_mac_multi call for c.hmac_cfg
 void fan_divide_round(Ctx &c, const u64 *Y, u64 ysb, u64 ysk, u64 *Z, int B, int nk, int nl, int last_idx);
 void galois_permute(Ctx &c, PolyArr in, PolyArr out, int B, int nk, int nl, u32 elt);

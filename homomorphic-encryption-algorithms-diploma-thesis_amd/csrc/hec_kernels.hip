@@ -1763,21 +1763,36 @@ void key_wsum(Ctx &c, const u64 *key, u64 *KW, int l)
     HEC_HIP(hipGetLastError());
 }
 
+// Children slots of one k_hmacm launch: NS groups of CG siblings (round 5: a whole sibling group of up to 6 in one
+// launch, 3 slots of 2, instead of one launch per pair)
+template <int CG, int NS>
+struct HSlots {
+    HChildren<CG> s[NS];
+    int ns;
+};
+
 // Two grid segments: the integer-arithmetic targets (Imap[0, nint), 128-bit accumulators) with BTI batch
 // entries per thread, then the FP64 targets with BTF, so neither class carries the other's register
-// budget.  Each segment is XCD-aware: the batch groups of one (coefficient block, I) share an XCD.
-template <int BTF, int BTI, int CG, int MINW>
+// budget.  Each segment is XCD-aware: the batch groups of one (coefficient block, I) share an XCD, and the ns slots
+// of one (coefficient block, I, batch group) — the same digit tile E, the node's c1 / c0 words, different children —
+// are consecutive blocks of that XCD (ids w, w + 8, w + 16): the tile comes from HBM for the first and from the XCD's
+// L2 for the others, so the digits, the kernel's largest stream, cross HBM once per sibling group, not per pair.
+template <int BTF, int BTI, int CG, int MINW, int NS>
 __global__ void __launch_bounds__(256, MINW)  // MINW waves per SIMD: 3 -> <= 168 VGPRs, 2 -> <= 256
-    k_hmacm(PolyArr X1, PolyArr X0, const u64 *__restrict__ E, const int *__restrict__ zl, const HChildren<CG> ch,
+    k_hmacm(PolyArr X1, PolyArr X0, const u64 *__restrict__ E, const int *__restrict__ zl, const HSlots<CG, NS> S,
             int B, int l, int K, int logN, const DevPrime *__restrict__ primes, const int *__restrict__ Imap, int nI,
             int nint, const u64 *__restrict__ cji, const u64 *__restrict__ psipow, int wsplit)
 {
     const u64 N = 1ull << logN;
     const int X = (int)(N / 512);
-    const bool integer = (int)blockIdx.x < wsplit;
+    const int ns = NS == 1 ? 1 : S.ns;
+    const int t8 = (int)blockIdx.x >> 3, slot = NS == 1 ? 0 : t8 % ns;
+    const int wb = (NS == 1 ? t8 : t8 / ns) * 8 + ((int)blockIdx.x & 7);  // the block index without the slot
+    const HChildren<CG> ch = S.s[slot];
+    const bool integer = wb < wsplit;
     const int bt = integer ? BTI : BTF;
     const int nbg = (B + bt - 1) / bt;
-    const int w = integer ? blockIdx.x : blockIdx.x - wsplit;
+    const int w = integer ? wb : wb - wsplit;
     const int g8 = w & 7, rest = w >> 3, bg = rest % nbg, G = (rest / nbg) * 8 + g8;
     if (G >= X * (integer ? nint : nI - nint)) return;
     const int yi = G / X + (integer ? 0 : nint), xb = G % X;
@@ -1792,29 +1807,40 @@ __global__ void __launch_bounds__(256, MINW)  // MINW waves per SIMD: 3 -> <= 16
         hmacm_body<BTI, CG, false>(X1, X0, E, zl, ch, B, l, K, logN, pr, Pq, I, kI, s0, bg * BTI, cji, psipow);
 }
 
-template <int BTF, int BTI, int CG, int MINW = (BTF * CG <= 8 && BTI * CG <= 8) ? 3 : 2>
+// nkids children in slots of CG (the last slot may hold fewer), at most NS slots
+template <int BTF, int BTI, int CG, int NS = 1, int MINW = (BTF * CG <= 8 && BTI * CG <= 8) ? 3 : 2>
 static void launch_hmacm(Ctx &c, PolyArr X1, PolyArr X0, const u64 *E, const int *zl, const HChildSpec *kids,
                          int nkids, int B, int l)
 {
-    HChildren<CG> ch{};
-    ch.n = nkids;
-    for (int q = 0; q < nkids; ++q)
-        ch.c[q] = HChild{kids[q].elt, kids[q].einv, kids[q].key, kids[q].W, kids[q].ACC, kids[q].KW};
+    HSlots<CG, NS> S{};
+    S.ns = (nkids + CG - 1) / CG;
+    if (nkids < 1 || S.ns > NS) throw std::invalid_argument("hoisted MAC: children per launch");
+    for (int q = 0; q < nkids; ++q) {
+        HChildren<CG> &ch = S.s[q / CG];
+        ch.c[q % CG] = HChild{kids[q].elt, kids[q].einv, kids[q].key, kids[q].W, kids[q].ACC, kids[q].KW};
+        ch.n = q % CG + 1;
+    }
     const int nint = c.imap_nint[l], X = (int)(c.N / 512);
     const int gI = (X * nint + 7) / 8 * 8, gF = (X * (l + 1 - nint) + 7) / 8 * 8;
     const int wsplit = gI * ((B + BTI - 1) / BTI), total = wsplit + gF * ((B + BTF - 1) / BTF);
-    k_hmacm<BTF, BTI, CG, MINW><<<dim3((unsigned)total), 256, 0, c.stream>>>(X1, X0, E, zl, ch, B, l, (int)c.K, c.logN,
-                                                                        c.primes, c.imap_at(l), l + 1, nint, c.cji,
-                                                                        c.psipow, wsplit);
+    k_hmacm<BTF, BTI, CG, MINW, NS><<<dim3((unsigned)(total * S.ns)), 256, 0, c.stream>>>(
+        X1, X0, E, zl, S, B, l, (int)c.K, c.logN, c.primes, c.imap_at(l), l + 1, nint, c.cji, c.psipow, wsplit);
     HEC_HIP(hipGetLastError());
 }
 
-int hoisted_group(const Ctx &c) { return c.hmac_cfg ? 2 : 1; }
+int hoisted_group(const Ctx &c) { return c.hmac_cfg == 2 ? HMAC_MAX_CHILDREN : c.hmac_cfg ? 2 : 1; }
+
+void hoisted_mac_group(Ctx &c, PolyArr X1, PolyArr X0, const u64 *E, const int *zl, const HChildSpec *kids, int nkids,
+                       int B, int l)
+{
+    static_assert(HMAC_MAX_CHILDREN <= 2 * 3, "3 slots of 2 children");
+    launch_hmacm<4, 2, 2, 3>(c, X1, X0, E, zl, kids, nkids, B, l);
+}
 
 void hoisted_mac_multi(Ctx &c, PolyArr X1, PolyArr X0, const u64 *E, const int *zl, const HChildSpec *kids, int nkids,
                        int B, int l)
 {
-    if (nkids < 1 || nkids > hoisted_group(c)) throw std::invalid_argument("hoisted_mac_multi: group size");
+    if (nkids < 1 || nkids > 2) throw std::invalid_argument("hoisted_mac_multi: group size");
     // <FP64 batch entries, integer batch entries, children> per thread (the 1x4, 2x2, 3x2, 4x4 ...
     // shapes measured slower)
     if (c.hmac_cfg) launch_hmacm<4, 2, 2>(c, X1, X0, E, zl, kids, nkids, B, l);

@@ -411,7 +411,7 @@ def test_cfg5_params_matvec_bitexact(orc, hecdna):
                                  {"HEC_FAN": "0"}, {"HEC_FAN": "1", "HEC_FUSE_GALOIS": "0"},
                                  {"HEC_HOIST": "0"}, {"HEC_HOIST_MIN": "1"}, {"HEC_HOIST_MIN": "1", "HEC_FAN": "0"},
                                  {"HEC_HMAC": "0"}, {"HEC_HMAC": "0", "HEC_HOIST_MIN": "1"},
-                                 {"HEC_HMAC_ODD3": "0"},
+                                 {"HEC_HMAC": "1"}, {"HEC_HMAC": "1", "HEC_HMAC_ODD3": "0"},
                                  {"HEC_HOIST_SCAN": "0"}])
 def test_keyswitch_variants_bitexact(orc, hecdna, env):
     """The engine's alternative key-switch schedules (separate mod-up pass B + MAC kernels; the fused
@@ -572,11 +572,11 @@ def _env_with(orc, hecdna, env, *args, **kw):
 
 
 @pytest.mark.parametrize("nzeros", [3, 40])  # 40 > HEC_ZCAP: the hoisted walk recomputes without hoisting
-@pytest.mark.parametrize("variant", [{}, {"HEC_HMAC": "0"}, {"HEC_HMAC_ODD3": "0"}])
+@pytest.mark.parametrize("variant", [{}, {"HEC_HMAC": "0"}, {"HEC_HMAC": "1"}, {"HEC_HMAC": "1", "HEC_HMAC_ODD3": "0"}])
 def test_hoisted_modup_zero_coefficients(orc, hecdna, nzeros, variant):
     """The hoisted mod-up corrects for zero digit coefficients that the Galois automorphism negates
     (SEAL maps -0 to 0, not to q_J); a limb with more zeros than the kernels list falls back.  Every hoisted MAC
-    schedule (k_hmacm pairs and triples, one k_hmac per child)."""
+    schedule (k_hmacm over a whole sibling group, pairs and triples, one k_hmac per child)."""
     e = _env_with(orc, hecdna, variant, 1 << 11, [50, 36, 36, 50])
     rng = np.random.default_rng(nzeros)
     X = [_with_coeff_zeros(e, e.enc(seed=1100 + i), {0: rng.choice(e.N, nzeros, replace=False),
