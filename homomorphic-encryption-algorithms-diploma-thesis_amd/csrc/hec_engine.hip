@@ -409,12 +409,6 @@ void moddown_group(Ctx &c, u64 *ACC, u64 *Z, PolyArr IN, int in_nk, const PolyAr
         ProfScope k(c, "k:k_fan2/moddown", 2.0 * B * ng * (l + 1));
         fan_divide_round(c, ACC + l * N, 2 * (l + 1) * N, (l + 1) * N, Z, B * ng, 2, l, (int)c.K - 1);
     }
-    if (in_nk == 0) {  // no IN term (folded into the MAC): the siblings' pass B as one launch, OUT per sibling
-        ProfScope k(c, "k:k_ntt/divround_b", 6.0 * B * l * ng);
-        divide_round(c, ACC + l * N, 2 * (l + 1) * N, (l + 1) * N, PolyArr{ACC, 2 * (l + 1) * N, (l + 1) * N}, IN, 0,
-                     PolyArr{}, B, 2, l, (int)c.K - 1, c.p_inv.data(), c.p_inv_q.data(), Z, 1, 2, OUT, ng);
-        return;
-    }
     for (int q = 0; q < ng; ++q) {
         ProfScope k(c, "k:k_ntt/divround_b", (6.0 + in_nk) * B * l);
         divide_round(c, ACC + q * sacc + l * N, 2 * (l + 1) * N, (l + 1) * N,

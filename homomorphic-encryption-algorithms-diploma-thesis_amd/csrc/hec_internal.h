@@ -140,11 +140,9 @@ void ks_modup_mac(Ctx &c, const u64 *D, u64 *E, PolyArr T, const u64 *key, u64 *
 // X / IN / OUT addressed (b,k,i), nk polys per batch entry, nl output limbs.
 //   OUT = IN + (X - NTT(corr)) * inv   (IN optional; inv = last^-1 mod q_i)
 // in_elt != 1: IN is read through the Galois permutation of in_elt
-// outq != nullptr (no IN): ngroup siblings in one launch; X, Z and Y hold the siblings' B entries back to back (the
-// batch index runs over ngroup B), sibling q's outputs go to outq[q] (same strides for every q)
 void divide_round(Ctx &c, const u64 *Y, u64 ysb, u64 ysk, PolyArr X, PolyArr IN, int in_nk, PolyArr OUT, int B,
                   int nk, int nl, int last_idx, const u64 *inv, const u64 *inv_q, u64 *Z, u32 in_elt = 1,
-                  int stages = 3, const PolyArr *outq = nullptr, int ngroup = 0);
+                  int stages = 3);
 // fan-out kernels (see hec_kernels.hip): finish an INTT whose first pass ran (inverse pass A) and run
 // the forward pass A of every target prime from registers.
 //   mod-up:  D[b][J] -> E[b][I][J] (I != J), the input of k_bmac / ks_modup's pass B

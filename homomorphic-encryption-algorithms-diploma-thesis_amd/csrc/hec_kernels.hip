@@ -207,10 +207,6 @@ struct DivRoundIOB {
     int fpstore;              // FP64 primes: the post-op in FP64 (store_fp)
     const DevPrime *primes;
     u64 inv[HEC_MAXL], inv_q[HEC_MAXL];
-    // bper > 0: the batch index b runs over several siblings' outputs, bper entries each, sibling q writing to
-    // outq[q] (OUT.p unused; strides OUT.sb / OUT.sk), so a sibling group's pass B is one launch (divide_round_group)
-    int bper;
-    u64 *outq[HMAC_MAX_CHILDREN];
     struct Bound {
         static constexpr bool kFpStore = true;
         static constexpr bool kLatePre = !HAS_IN;  // the one operand is loaded at the store (4 waves/SIMD)
@@ -250,9 +246,8 @@ struct DivRoundIOB {
     {
         const int i = job % nl, t = job / nl, k = t % nk, b = t / nk;
         const u64 li = (u64)i << logN;
-        u64 *const out = bper ? outq[b / bper] + (b % bper) * OUT.sb + k * OUT.sk + li : OUT.p + b * OUT.sb + k * OUT.sk + li;
         return Bound{Z + ((u64)job << logN), X.p + b * X.sb + k * X.sk + li,
-                     (IN.p && k < in_nk) ? IN.p + b * IN.sb + k * IN.sk + li : nullptr, out,
+                     (IN.p && k < in_nk) ? IN.p + b * IN.sb + k * IN.sk + li : nullptr, OUT.p + b * OUT.sb + k * OUT.sk + li,
                      primes[i].q, inv[i], inv_q[i], i, elt, logN, fpstore != 0};
     }
 };
@@ -804,12 +799,9 @@ void ks_modup(Ctx &c, const u64 *D, u64 *E, int B, int l, int stages)
 }
 
 void divide_round(Ctx &c, const u64 *Y, u64 ysb, u64 ysk, PolyArr X, PolyArr IN, int in_nk, PolyArr OUT, int B,
-                  int nk, int nl, int last_idx, const u64 *inv, const u64 *inv_q, u64 *Z, u32 in_elt, int stages,
-                  const PolyArr *outq, int ngroup)
+                  int nk, int nl, int last_idx, const u64 *inv, const u64 *inv_q, u64 *Z, u32 in_elt, int stages)
 {
     if (nl > HEC_MAXL) throw std::invalid_argument("too many limbs");
-    if (outq && (ngroup < 1 || ngroup > HMAC_MAX_CHILDREN || (IN.p && in_nk > 0)))
-        throw std::invalid_argument("divide_round: sibling group");
     DivRoundIO_A a{};
     a.Y = Y; a.ysb = ysb; a.ysk = ysk; a.Z = Z; a.nk = nk; a.nl = nl; a.logN = c.logN;
     a.last = c.q[last_idx]; a.half = a.last >> 1; a.primes = c.primes;
@@ -819,15 +811,7 @@ void divide_round(Ctx &c, const u64 *Y, u64 ysb, u64 ysk, PolyArr X, PolyArr IN,
         b.elt = in_elt; b.primes = c.primes;
         b.fpstore = 1;
         for (int i = 0; i < nl; ++i) { b.inv[i] = inv[i]; b.inv_q[i] = inv_q[i]; }
-        b.bper = 0;
-        int njobs = B * nk * nl;
-        if (outq) {  // ngroup siblings: X and Z run on contiguously (the caller's layout), OUT per sibling
-            b.bper = B;
-            b.OUT = PolyArr{nullptr, outq[0].sb, outq[0].sk};
-            for (int q = 0; q < ngroup; ++q) b.outq[q] = outq[q].p;
-            njobs *= ngroup;
-        }
-        ntt_dispatch<false>(c, njobs, a, b, stages);
+        ntt_dispatch<false>(c, B * nk * nl, a, b, stages);
     };
     if (IN.p != nullptr && in_nk > 0) run(DivRoundIOB<true>{});
     else run(DivRoundIOB<false>{});
