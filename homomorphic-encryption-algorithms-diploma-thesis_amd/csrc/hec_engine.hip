@@ -1359,6 +1359,7 @@ int hec_context_create(uint64_t N, const uint64_t *mod, uint64_t K, int device, 
         if (const char *f = std::getenv("HEC_HOIST_MIN")) c.hoist_min_children = std::max(1, std::atoi(f));
         if (const char *f = std::getenv("HEC_TENSOR_DEFER")) c.tensor_defer_max = std::max(1, std::atoi(f));
         if (const char *f = std::getenv("HEC_TENSOR_BUFS")) c.tensor_defer_bufs = std::max(1, std::atoi(f));
+        if (const char *f = std::getenv("HEC_TENSOR_XCD")) c.tensor_xcd = std::max(0, std::atoi(f));
         if (const char *f = std::getenv("HEC_POISON")) c.poison = f[0] != '0';
         if (const char *f = std::getenv("HEC_LANE_SERIAL")) c.lane_serial = f[0] != '0';
         c.N = N;
@@ -1556,6 +1557,7 @@ int hec_context_set_option(hec_context *ctx, const char *name, int64_t value)
             else if (n == "fused_modup_mac") c.fused_modup_mac = value != 0;
             else if (n == "tensor_defer") c.tensor_defer_max = (int)std::max<int64_t>(1, value);
             else if (n == "tensor_bufs") c.tensor_defer_bufs = (int)std::max<int64_t>(1, value);
+            else if (n == "tensor_xcd") c.tensor_xcd = (int)std::max<int64_t>(0, value);
             else throw std::invalid_argument("unknown option");
         };
         HEC_HIP(hipStreamSynchronize(ctx->c.stream));

@@ -84,6 +84,7 @@ struct Ctx {
     std::vector<std::vector<u64>> ql_inv, ql_inv_q, ql_half_mod;  // rescale at level l (drop prime l-1)
     int tensor_defer_max = 12;     // HEC_TENSOR_DEFER: terminals per deferred tensor batch (1 = immediate)
     int tensor_defer_bufs = 8;     // HEC_TENSOR_BUFS: rotation buffers per trie depth
+    int tensor_xcd = 0;            // HEC_TENSOR_XCD: k_tensor_multi2 grid in XCD clusters of this many batch groups
     bool hoist = true;             // HEC_HOIST=0: no hoisted mod-up in the rotation trie walk
     int hoist_min_children = 2;    // HEC_HOIST_MIN: children a trie node needs to be hoisted
     int hmac_cfg = 2;              // HEC_HMAC: 2 a sibling group per k_hmacm launch (slots of 2 children), 1 one

@@ -2408,14 +2408,24 @@ void tensor_acc(Ctx &c, PolyArr R, const u64 *A, u64 a_sk, PolyArr ACC, int B, i
 // (FP64: |sum| < 12 x 0.53 q; 60-bit primes: 128-bit sums of < 2^120 products) and canonicalised once.
 // (Blocks of 4 waves on 4 batch groups sharing the diagonal words through L1 measured slower: 556 vs 522 ms per
 // step, round 4.)
+// xs > 0: a 1-D grid in clusters of xs batch groups per coefficient block, each cluster's blocks consecutive on one
+// XCD (ids w, w + 8, ...), so a coefficient block's diagonal words come from HBM once per cluster and from that XCD's
+// L2 for the rest, while every batch group still streams its rotated inputs over consecutive coefficient blocks
 template <bool PT, int BG>
 __global__ void __launch_bounds__(256)
     k_tensor_multi2(TensorBatch tb, u64 r_sb, u64 r_sk, u64 a_sk, PolyArr ACC, int B, int logN, u64 total, int assign,
-                    const DevPrime *__restrict__ primes)
+                    const DevPrime *__restrict__ primes, int xs, int ncb)
 {
-    const u64 idx = (u64)blockIdx.x * 256 + threadIdx.x;
+    int cb = blockIdx.x, bgi = blockIdx.y;
+    if (xs > 0) {
+        const int t = (int)blockIdx.x >> 3, s = t % xs, c = (t / xs) * 8 + ((int)blockIdx.x & 7);
+        cb = c % ncb;
+        bgi = (c / ncb) * xs + s;
+        if (bgi * BG >= B) return;
+    }
+    const u64 idx = (u64)cb * 256 + threadIdx.x;
     if (idx >= total) return;
-    const int b0 = blockIdx.y * BG;
+    const int b0 = bgi * BG;
     const int nb = min(BG, B - b0);
     const DevPrime pr = primes[idx >> logN];
     u64 d0[BG], d1[BG], d2[BG];
@@ -2489,13 +2499,19 @@ void tensor_multi(Ctx &c, const TensorBatch &tb, u64 r_sb, u64 r_sk, u64 a_sk, P
 {
     const u64 total = (u64)l * c.N;
     constexpr int BG = 2;  // batch entries per thread (round 3, r03t: 533 vs 578 ms per step for 4, 577 for 8)
-    const dim3 g2((unsigned)((total + 255) / 256), (unsigned)((B + BG - 1) / BG));
+    const int ncb = (int)((total + 255) / 256), nbg = (B + BG - 1) / BG;
+    const int xs = std::min(std::max(0, c.tensor_xcd), nbg);
+    dim3 g2((unsigned)ncb, (unsigned)nbg);
+    if (xs > 0) {  // clusters of xs batch groups: ncb * ceil(nbg / xs) clusters, padded to whole XCD rounds
+        const long clusters = (long)ncb * ((nbg + xs - 1) / xs);
+        g2 = dim3((unsigned)((clusters + 7) / 8 * 8 * xs), 1);
+    }
     if (plain)
         k_tensor_multi2<true, BG><<<g2, 256, 0, c.stream>>>(tb, r_sb, r_sk, a_sk, ACC, B, c.logN, total, assign ? 1 : 0,
-                                                           c.primes);
+                                                           c.primes, xs, ncb);
     else
         k_tensor_multi2<false, BG><<<g2, 256, 0, c.stream>>>(tb, r_sb, r_sk, a_sk, ACC, B, c.logN, total,
-                                                            assign ? 1 : 0, c.primes);
+                                                            assign ? 1 : 0, c.primes, xs, ncb);
     HEC_HIP(hipGetLastError());
 }
 

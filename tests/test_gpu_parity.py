@@ -408,6 +408,7 @@ def test_cfg5_params_matvec_bitexact(orc, hecdna):
 @pytest.mark.parametrize("env", [{"HEC_FUSED_MODUP_MAC": "0"},
                                  {"HEC_FUSE_GALOIS": "0"}, {"HEC_FUSE_GALOIS": "0", "HEC_FUSED_MODUP_MAC": "0"},
                                  {"HEC_TENSOR_DEFER": "1"}, {"HEC_TENSOR_BUFS": "1"}, {"HEC_TENSOR_DEFER": "3"},
+                                 {"HEC_TENSOR_XCD": "1"}, {"HEC_TENSOR_XCD": "3"},
                                  {"HEC_FAN": "0"}, {"HEC_FAN": "1", "HEC_FUSE_GALOIS": "0"},
                                  {"HEC_HOIST": "0"}, {"HEC_HOIST_MIN": "1"}, {"HEC_HOIST_MIN": "1", "HEC_FAN": "0"},
                                  {"HEC_HMAC": "0"}, {"HEC_HMAC": "0", "HEC_HOIST_MIN": "1"},
