@@ -26,6 +26,9 @@ for S in 0 8 32; do
       > $GRAFT_REPO_ROOT/$OUT/pmc_x$S.log 2>&1 || { tail -5 $GRAFT_REPO_ROOT/$OUT/pmc_x$S.log; exit 1; }
   python3 -c "
 import csv
-v=[float(r['Counter_Value']) for r in csv.DictReader(open('$GRAFT_REPO_ROOT/$OUT/pmc_x$S/run_counter_collection.csv')) if 'k_tensor_multi2' in r['Kernel_Name']]
-print('xcd=$S FETCH_SIZE kB per dispatch', sum(v)/len(v), 'dispatches', len(v))"
+d={}
+for r in csv.DictReader(open('$GRAFT_REPO_ROOT/$OUT/pmc_x$S/run_counter_collection.csv')):
+    if 'k_tensor_multi2' in r['Kernel_Name'] and r['Counter_Name']=='FETCH_SIZE':
+        d[r['Dispatch_Id']]=d.get(r['Dispatch_Id'],0.0)+float(r['Counter_Value'])
+print('xcd=$S FETCH_SIZE kB per dispatch', sum(d.values())/len(d), 'dispatches', len(d))"
 done
