@@ -168,7 +168,16 @@ int main(int argc, char **argv)
     std::vector<Ciphertext> keep;
     if (mode == "batched_diag_sharded")  // the same demo with the context on a (one-rank) RCCL communicator
         ctx.comm_init(0, 1, hecdna::Context::comm_unique_id());
-    if (mode == "batched_diag" || mode == "batched_col" || mode == "batched_diag_sharded") {
+    if (mode == "batched_diag_sharded_host") {  // ... on a host communicator (hec_comm_init_ops) of a one-rank world:
+        // the all-reduces over one rank are the identity, so the partials still take the host exchange path
+        // (download, allreduce_u64_sum, upload) and the agreement step
+        hec_comm_ops ops{};
+        ops.allreduce_f64 = [](void *, double *, uint64_t, int) { return 0; };
+        ops.allreduce_u64_sum = [](void *, uint64_t *, uint64_t) { return 0; };
+        ctx.comm_init(0, 1, ops);
+    }
+    if (mode == "batched_diag" || mode == "batched_col" || mode == "batched_diag_sharded" ||
+        mode == "batched_diag_sharded_host") {
         // matrix_operations.cpp:1112-1141 — the same code the reference runs over seal:: types
         const std::size_t dim = cts.size();
         std::vector<BatchedVector> mat1_cols_bvec;

@@ -211,6 +211,11 @@ public:
     {
         check(hec_comm_init(h_.get(), rank, world, unique_id.empty() ? nullptr : unique_id.data()));
     }
+    // the same sharding over the caller's own collectives (MPI, gloo, ...): hec_comm_init_ops, INTEGRATION.md §5.2
+    void comm_init(int rank, int world, const hec_comm_ops &ops) const
+    {
+        check(hec_comm_init_ops(h_.get(), rank, world, &ops));
+    }
     bool has_comm() const { return hec_context_comm(h_.get(), nullptr, nullptr) == 1; }
     void synchronize() const { check(hec_context_synchronize(h_.get())); }
 

@@ -81,14 +81,17 @@ def test_demo_batched_col_matches_golden(demo, orc, tmp_path):
     assert [sha(d, sc) for d, sc in out] == fx["output_sha256"]
 
 
-def test_demo_batched_diag_sharded_rccl(demo, orc, tmp_path):
-    """The he_linalg.h drop-in with its context on an RCCL communicator (one rank): BatchedMatrix::matmul takes
-    the sharded C-ABI path (hec_matmul_diag_col_sharded) and still reproduces the cfg1 golden hashes."""
+@pytest.mark.parametrize("mode", ["batched_diag_sharded", "batched_diag_sharded_host"])
+def test_demo_batched_diag_sharded_rccl(demo, orc, tmp_path, mode):
+    """The he_linalg.h drop-in with its context on a communicator of one rank — RCCL (hec_comm_init) or the caller's
+    host collectives (hec_comm_init_ops): BatchedMatrix::matmul takes the sharded C-ABI path
+    (hec_matmul_diag_col_sharded: agreement step, partials, exchange, finish) and still reproduces the cfg1 golden
+    hashes."""
     sys.path.insert(0, GOLD)
     from make_golden import cfg1_inputs, sha
     fx = json.load(open(os.path.join(GOLD, "cfg1_matvec.json")))
     o, m, sk, rk, gk, cts = cfg1_inputs(orc)
-    out = run(demo, "batched_diag_sharded", tmp_path, fx["N"], m, cts, rk, gk)
+    out = run(demo, mode, tmp_path, fx["N"], m, cts, rk, gk)
     assert [sha(d, sc) for d, sc in out] == fx["output_sha256"]
 
 
