@@ -174,10 +174,49 @@ def reduce_rows_mod_q(rows: np.ndarray, moduli, level: int, N: int) -> np.ndarra
     return (r % q).reshape(rows.shape[0], -1)
 
 
+def _are_close(a: float, b: float) -> bool:  # SEAL util::are_close
+    return abs(a - b) < np.finfo(np.float64).eps * max(abs(a), abs(b), 1.0)
+
+
+def agree(err, scales, rank: int, world: int, group=None, device=None):
+    """The agreement step before the exchange (the protocol of hec_shard_agree, include/hecdna.h): every rank passes
+    its own argument-check result (err: None or the hecdna.HecError it raised) and the product scales of its p
+    partial outputs; two all-reduces later a failing rank re-raises its own error, every other rank raises the error
+    of the failing rank with the larger (code << 8 | rank + 1), and when no rank failed every rank raises
+    invalid_argument "scale mismatch" if the ranks' scales of one output are not SEAL-close (add_inplace over the
+    whole sum).  So no rank is left waiting in the exchange.  Returns None when the ranks agree."""
+    import torch
+    import torch.distributed as dist
+    import hecdna
+    p = len(scales)
+    code = 0
+    if err is not None:
+        code = ((err.code if isinstance(err, hecdna.HecError) and err.code in (1, 2) else 2) << 8) | (rank + 1)
+    inf = float("inf")
+    mn = torch.tensor([float(code)] + [inf if code else float(s) for s in scales], dtype=torch.float64, device=device)
+    mx = torch.tensor([float(code)] + [-inf if code else float(s) for s in scales], dtype=torch.float64, device=device)
+    if world > 1:
+        dist.all_reduce(mn, op=dist.ReduceOp.MIN, group=group)
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX, group=group)
+    mn, mx = mn.cpu().numpy(), mx.cpu().numpy()
+    if err is not None:
+        return err
+    agreed = int(mx[0])
+    if agreed:
+        cls = hecdna.InvalidArgument if agreed >> 8 == 1 else hecdna.LogicError
+        return cls(agreed >> 8, "matmul_diag_col_sharded: the arguments failed SEAL's checks on rank %d"
+                   % ((agreed & 0xFF) - 1))
+    for i in range(p):
+        if not _are_close(float(mn[1 + i]), float(mx[1 + i])):
+            return hecdna.InvalidArgument(1, "scale mismatch")
+    return None
+
+
 def sharded_matvec(ctx, diags, cols, rk, gk, rank: int, world: int, plan=None, group=None):
     """Row-sharded diag x col matvec on this rank's GPU (torch.distributed already initialised).
 
-    Returns (owned output indices, their finished Ciphertexts)."""
+    Returns (owned output indices, their finished Ciphertexts).  The ranks agree on the argument checks before the
+    exchange (`agree`), so an error on one rank is raised on every rank instead of leaving the others waiting."""
     import torch
     import hecdna
     if not torch.cuda.is_available():
@@ -185,10 +224,20 @@ def sharded_matvec(ctx, diags, cols, rk, gk, rank: int, world: int, plan=None, g
                            "HIP runtime (see INTEGRATION.md)")
     N, n, p = ctx.N, len(diags), len(cols)
     plan = plan or plan_diagonal_shards(N, n, world)
-    accs = ctx.matmul_diag_col_partial_set(diags, plan[rank], cols, gk)
+    dev = torch.device("cuda", ctx.device)
+    accs, err = None, None
+    try:
+        accs = ctx.matmul_diag_col_partial_set(diags, plan[rank], cols, gk)
+    except hecdna.HecError as e:
+        err = e
+    import torch.distributed as dist
+    on_dev = world > 1 and dist.get_backend(group) == "nccl"
+    err = agree(err, [a.info()[2] for a in accs] if accs else [0.0] * p, rank, world, group,
+                dev if on_dev else None)
+    if err is not None:
+        raise err
     size, level, scale = accs[0].info()
     words = size * level * N
-    dev = torch.device("cuda", ctx.device)
     buf = torch.empty((p, words), dtype=torch.int64, device=dev)
     for i, a in enumerate(accs):
         a.export_device(buf[i].data_ptr())

@@ -212,3 +212,58 @@ def test_cabi_shard_agree_gloo(hecdna, world):
                 rank, (ELOGIC, "matmul_diag_col_sharded: the arguments failed SEAL's checks on rank 2"))
         else:
             assert s4 == 0
+
+
+def _py_agree_worker(rank, world, port, q):
+    import sys
+    import torch.distributed as dist
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__))))
+    from _helpers import load_hecdna
+    hec = load_hecdna()
+    import hecdna.shard as shard
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        s, p = 2.0**80, 3
+        out = []
+
+        def run(err, scales):
+            r = shard.agree(err, scales, rank, world)
+            out.append(None if r is None else (type(r).__name__, str(r)))
+        run(hec.InvalidArgument(1, "scale out of bounds") if rank == world - 1 else None, [s] * p)
+        run(None, [s] * p)
+        run(None, [s, s * (1 + 1e-9) if rank == 0 else s, s])
+        run(hec.LogicError(2, "bad two") if rank == 1 else None, [s] * p)
+        run(None, [s] * p)
+        q.put((rank, "ok", out))
+    except Exception as e:  # surface the failure to the parent
+        q.put((rank, repr(e), None))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_python_shard_agree_gloo(hecdna, world):
+    """shard.sharded_matvec's agreement step (the hec_shard_agree protocol over torch.distributed) at world > 1 on
+    the CPU: an argument error on one rank is raised on every rank, a cross-rank scale mismatch too, and the next
+    agreement passes."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_py_agree_worker, args=(r, world, port, q)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for pr in procs:
+        pr.join(timeout=60)
+    assert all(r[1] == "ok" for r in res), res
+    last = world - 1
+    for rank, _, (a1, a2, a3, a4, a5) in res:
+        assert a1 == ("InvalidArgument", "scale out of bounds" if rank == last else
+                      "matmul_diag_col_sharded: the arguments failed SEAL's checks on rank %d" % last)
+        assert a2 is None and a5 is None
+        assert a3 == ("InvalidArgument", "scale mismatch")
+        assert a4 == ("LogicError", "bad two" if rank == 1 else
+                      "matmul_diag_col_sharded: the arguments failed SEAL's checks on rank 1")
