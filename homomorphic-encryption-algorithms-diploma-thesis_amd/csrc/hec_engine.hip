@@ -1356,7 +1356,6 @@ int hec_context_create(uint64_t N, const uint64_t *mod, uint64_t K, int device, 
         if (const char *f = std::getenv("HEC_HOIST")) c.hoist = f[0] != '0';
         if (const char *f = std::getenv("HEC_HMAC")) c.hmac_cfg = std::atoi(f);
         if (const char *f = std::getenv("HEC_HMAC_ODD3")) c.hmac_odd3 = std::atoi(f);
-        if (const char *f = std::getenv("HEC_HMAC_SHAPE")) c.hmac_shape = std::atoi(f);
         if (const char *f = std::getenv("HEC_HOIST_MIN")) c.hoist_min_children = std::max(1, std::atoi(f));
         if (const char *f = std::getenv("HEC_TENSOR_DEFER")) c.tensor_defer_max = std::max(1, std::atoi(f));
         if (const char *f = std::getenv("HEC_TENSOR_BUFS")) c.tensor_defer_bufs = std::max(1, std::atoi(f));
@@ -1552,7 +1551,6 @@ int hec_context_set_option(hec_context *ctx, const char *name, int64_t value)
             else if (n == "hoist_min") c.hoist_min_children = (int)std::max<int64_t>(1, value);
             else if (n == "hmac") c.hmac_cfg = (int)value;
             else if (n == "hmac_odd3") c.hmac_odd3 = (int)value;
-            else if (n == "hmac_shape") c.hmac_shape = (int)value;
             else if (n == "hoist_scan") c.hoist_scan = (int)value;
             else if (n == "fan") c.fan_out = value != 0;
             else if (n == "fuse_galois") c.fuse_galois = value != 0;

@@ -91,7 +91,6 @@ struct Ctx {
                                    // launch per sibling pair (round 4), 0 one hoisted MAC per child
     int hoist_scan = 1;            // HEC_HOIST_SCAN=0: hoisted node as INTT pass B, pass A, k_zscan, direct fan-out
                                    // (1: INTT pass B, then the fan-out finishes the INTT and lists the zeros)
-    int hmac_shape = 0;            // HEC_HMAC_SHAPE: batch entries / children per thread of the group launch
     int hmac_odd3 = 1;             // HEC_HMAC_ODD3=0: an odd sibling group ends in a pair and a single-child launch
     bool fan_out = true;           // HEC_FAN=0: separate INTT pass A (fan-out fuses it into the forward passes A)
     // HEC_LANES: concurrent batch lanes of a matvec (hec_engine.hip matvec_lanes).  Opt-in since round 5: one lane

@@ -1834,13 +1834,7 @@ void hoisted_mac_group(Ctx &c, PolyArr X1, PolyArr X0, const u64 *E, const int *
                        int B, int l)
 {
     static_assert(HMAC_MAX_CHILDREN <= 2 * 3, "3 slots of 2 children");
-    switch (c.hmac_shape) {  // HEC_HMAC_SHAPE: <FP64 / integer batch entries per thread, children per slot>
-    case 1: launch_hmacm<2, 2, 2, 3>(c, X1, X0, E, zl, kids, nkids, B, l); break;
-    case 2: launch_hmacm<4, 2, 3, 2>(c, X1, X0, E, zl, kids, nkids, B, l); break;
-    case 3: launch_hmacm<2, 1, 2, 3>(c, X1, X0, E, zl, kids, nkids, B, l); break;
-    case 4: launch_hmacm<2, 1, 3, 2>(c, X1, X0, E, zl, kids, nkids, B, l); break;
-    default: launch_hmacm<4, 2, 2, 3>(c, X1, X0, E, zl, kids, nkids, B, l); break;
-    }
+    launch_hmacm<4, 2, 2, 3>(c, X1, X0, E, zl, kids, nkids, B, l);
 }
 
 void hoisted_mac_multi(Ctx &c, PolyArr X1, PolyArr X0, const u64 *E, const int *zl, const HChildSpec *kids, int nkids,
