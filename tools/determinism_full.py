@@ -54,6 +54,7 @@ del raw
 rawx = e.o.encrypt_many(e.sk, xs[:, r], 2.0**40, L, 90000, nthreads=T)
 gX = [e.ctx.ciphertext(rawx[i], 2.0**40) for i in range(p)]
 ref = xs @ M.T
+e.ctx.set_option("lanes", 3)  # the opt-in lanes (one lane is the default since round 5)
 print("setup %.1f s" % (time.time() - t0), flush=True)
 idx = [0, 16, 32, 47]
 
