@@ -737,6 +737,7 @@ void walk_trie_hoisted(Ctx &c, Scratch &s, const RotTrie &t, int node, PolyArr s
     }
     const Hoist &h = hs[depth];
     hoist_node(c, src, B, l, h);
+    if (c.debug_lanes) debug_count_zl(c, h.zl, c.zflag + 1);
     const u64 N = c.N;
     // children in groups of up to `sup` siblings: one sibling-fused k_hmacm launch per hoisted_group() of them (the
     // default hmac_cfg 2: the whole group, slots of 2; 1: per pair), accumulators h.acc(q), contiguous; then the
@@ -926,7 +927,7 @@ void matvec_core(hec_context *ctx, const hec_ciphertext *const *diags, const hec
         }
         std::vector<Hoist> hs(D);
         for (int d = 0; d < D; ++d) hs[d] = hoist_alloc(c, s, (int)p, (int)l);
-        HEC_HIP(hipMemsetAsync(c.zflag, 0, sizeof(int), c.stream));
+        HEC_HIP(hipMemsetAsync(c.zflag, 0, 2 * sizeof(int), c.stream));
         walk_trie_hoisted(c, s, trie, 0, Xa, 0, (int)p, (int)l, ctx, gkm, bufs, hs, S2, c.hoist_min_children, visit,
                           before_write);
     } else {
@@ -934,9 +935,13 @@ void matvec_core(hec_context *ctx, const hec_ciphertext *const *diags, const hec
     }
     flush();
     if (hoist) {  // a digit limb with more zero coefficients than the hoisted MAC corrects: recompute
-        int zf = 0;
-        HEC_HIP(hipMemcpyAsync(&zf, c.zflag, sizeof(int), hipMemcpyDeviceToHost, c.stream));
+        int zfl[2] = {0, 0};
+        HEC_HIP(hipMemcpyAsync(zfl, c.zflag, 2 * sizeof(int), hipMemcpyDeviceToHost, c.stream));
         HEC_HIP(hipStreamSynchronize(c.stream));
+        const int zf = zfl[0];
+        if (c.debug_lanes)
+            std::fprintf(stderr, "hec-debug: %s p=%zu zero-list nodes %d overflow %d\n", exec ? "lane" : "ctx", p, zfl[1],
+                         zfl[0]);
         if (zf) {
             if (std::getenv("HEC_DEBUG")) std::fprintf(stderr, "hec: zero-list overflow, matvec recomputed without hoisting (p=%zu)\n", p);
             c.hoist = false;
@@ -996,7 +1001,8 @@ hec_context *make_lane(hec_context *parent)
     c.zflag = nullptr;
     HEC_HIP(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
     c.own_stream = true;
-    HEC_HIP(hipMalloc(&c.zflag, sizeof(int)));
+    HEC_HIP(hipMalloc(&c.zflag, 2 * sizeof(int)));
+    HEC_HIP(hipMemset(c.zflag, 0, 2 * sizeof(int)));
     HEC_HIP(hipEventCreateWithFlags(&l->lane_done, hipEventDisableTiming));
     return l;
 }
@@ -1009,6 +1015,38 @@ void free_lane(hec_context *l)
     (void)hipFree(c.zflag);
     (void)hipStreamDestroy(c.stream);
     delete l;
+}
+
+// HEC_DEBUG_LANES: a checksum of every key's sign-mask NTTs W and key sums KW at this level, compared with the first one
+// seen (they are built once and must never change)
+void debug_key_tables(hec_context *ctx, const hec_galois_keys &gk, int l)
+{
+    static std::mutex mu;
+    static std::map<std::pair<const void *, int>, u64> first;
+    std::lock_guard<std::mutex> lock(mu);
+    Ctx &c = ctx->c;
+    HEC_HIP(hipDeviceSynchronize());
+    auto sum = [&](const u64 *d, std::size_t words) {
+        std::vector<u64> h(words);
+        HEC_HIP(hipMemcpy(h.data(), d, words * sizeof(u64), hipMemcpyDeviceToHost));
+        u64 s = 1469598103934665603ull;
+        for (u64 w : h) s = (s ^ w) * 1099511628211ull;
+        return s;
+    };
+    int changed = 0, n = 0;
+    for (const auto &kv : gk.negw) {
+        const u64 sw = sum(kv.second, c.K * c.N);
+        auto it = gk.kw.find({kv.first, l});
+        const u64 sk = it == gk.kw.end() ? 0 : sum(it->second, (std::size_t)2 * (l + 1) * c.N);
+        for (auto [key, v] : {std::pair{std::pair{(const void *)kv.second, 0}, sw},
+                              std::pair{std::pair{(const void *)(it == gk.kw.end() ? nullptr : it->second), l}, sk}}) {
+            auto f = first.find(key);
+            if (f == first.end()) first[key] = v;
+            else if (f->second != v) ++changed;
+            ++n;
+        }
+    }
+    std::fprintf(stderr, "hec-debug: key tables %d checked, %d changed\n", n, changed);
 }
 
 void matvec_lanes(hec_context *ctx, const hec_ciphertext *const *diags, const hec_plaintext *const *pdiags,
@@ -1076,6 +1114,7 @@ void matvec_lanes(hec_context *ctx, const hec_ciphertext *const *diags, const he
         if (done[i]) HEC_HIP(hipStreamWaitEvent(c.stream, ctx->lanes[i]->lane_done, 0));
     for (int i = 0; i < nl; ++i)  // outgrown lane workspaces, now that no lane thread runs (waits only after a growth)
         ctx->lanes[i]->c.ws.reclaim(ctx->lanes[i]->c.stream);
+    if (c.debug_lanes && c.hoist) debug_key_tables(ctx, *gk, (int)cols[0]->level);
     for (auto &e : err)
         if (e) std::rethrow_exception(e);
 }
@@ -1362,6 +1401,7 @@ int hec_context_create(uint64_t N, const uint64_t *mod, uint64_t K, int device, 
         if (const char *f = std::getenv("HEC_TENSOR_XCD")) c.tensor_xcd = std::max(0, std::atoi(f));
         if (const char *f = std::getenv("HEC_POISON")) c.poison = f[0] != '0';
         if (const char *f = std::getenv("HEC_LANE_SERIAL")) c.lane_serial = f[0] != '0';
+        if (const char *f = std::getenv("HEC_DEBUG_LANES")) c.debug_lanes = f[0] != '0';
         c.N = N;
         c.logN = __builtin_ctzll(N);
         c.K = K;
@@ -1440,8 +1480,8 @@ int hec_context_create(uint64_t N, const uint64_t *mod, uint64_t K, int device, 
                 for (std::size_t I = 0; I < K; ++I) cji[J * K + I] = c.q[J] % c.q[I];
             HEC_HIP(hipMalloc(&c.cji, cji.size() * sizeof(u64)));
             HEC_HIP(hipMemcpy(c.cji, cji.data(), cji.size() * sizeof(u64), hipMemcpyHostToDevice));
-            HEC_HIP(hipMalloc(&c.zflag, sizeof(int)));
-            HEC_HIP(hipMemset(c.zflag, 0, sizeof(int)));
+            HEC_HIP(hipMalloc(&c.zflag, 2 * sizeof(int)));
+            HEC_HIP(hipMemset(c.zflag, 0, 2 * sizeof(int)));
         }
         {   // target-prime order tables per level (integer primes first)
             std::vector<int> tab((c.L + 1) * (HEC_MAXL + 2), 0);
@@ -1547,6 +1587,7 @@ int hec_context_set_option(hec_context *ctx, const char *name, int64_t value)
             else if (n == "lane_min_batch") c.lane_min_batch = (int)std::max<int64_t>(1, value);
             else if (n == "poison") c.poison = value != 0;
             else if (n == "lane_serial") c.lane_serial = value != 0;
+            else if (n == "debug_lanes") c.debug_lanes = value != 0;
             else if (n == "hoist") c.hoist = value != 0;
             else if (n == "hoist_min") c.hoist_min_children = (int)std::max<int64_t>(1, value);
             else if (n == "hmac") c.hmac_cfg = (int)value;

@@ -72,7 +72,7 @@ struct Ctx {
     // and a device flag raised when a digit limb holds more zero coefficients than the kernels correct
     u64 *psipow = nullptr;
     u64 *cji = nullptr;
-    int *zflag = nullptr;
+    int *zflag = nullptr;           // [0] zero-list overflow, [1] debug count (HEC_DEBUG_LANES)
     int logR = 0;                   // pass split N = R x C, R = 2^ceil(logN/2)
     // CKKS encoder tables (hec_encode.hip), built on first encode: SEAL's matrix_reps_index_map_ (u32[N]) and
     // inv_root_powers_ (complex[N], entry 0 unused)
@@ -105,6 +105,8 @@ struct Ctx {
     // residue can have (2^64 - 1; a NaN as FP64 bits) and the parity tests fail deterministically
     bool poison = false;
     bool lane_serial = false;      // HEC_LANE_SERIAL=1 (debug): the lanes run one after another, each drained
+    bool debug_lanes = false;      // HEC_DEBUG_LANES=1 (debug): per call, report nodes with zero lists, the overflow
+                                   // flag and changes of the per-key tables (stderr)
     // profiling (ProfScope in hec_engine.hip)
     int prof_mode = 0;  // 0 off, 1 synchronous per scope, 2 asynchronous event pairs
     // a scope's algorithmic bytes (compulsory reads + writes of its kernels) and kernel launches, so
@@ -155,6 +157,7 @@ void fan_modup(Ctx &c, const u64 *D, u64 *E, int B, int l, bool direct = false, 
 // from the node's NTT-form digits E, the child's sign-mask NTTs W (K limbs) and X1 = the node's c1.
 #define HEC_ZCAP 8
 void zero_scan(Ctx &c, const u64 *D, int nlimbs, int *zl);
+void debug_count_zl(Ctx &c, const int *zl, int *cnt);  // HEC_DEBUG_LANES: ++*cnt when zl[0] != 0
 void hoisted_mac(Ctx &c, PolyArr X1, const u64 *E, const u64 *W, const int *zl, const u64 *key, u64 *ACC, int B,
                  int l, u32 elt);
 // the same for up to 4 sibling rotations at once (the node's digits read once for all of them)

@@ -1319,6 +1319,18 @@ void fan_modup(Ctx &c, const u64 *D, u64 *E, int B, int l, bool direct, int *zl)
     fan_dispatch(c, B * l, f, g);
 }
 
+// debug (HEC_DEBUG_LANES): count the hoisted nodes whose zero list is not empty (uniform residues almost never have a
+// zero coefficient, so a count is a sign the list was read before it was written)
+__global__ void __launch_bounds__(64) k_dbg_zl(const int *__restrict__ zl, int *cnt)
+{
+    if (threadIdx.x == 0 && zl[0] != 0) atomicAdd(cnt, 1);
+}
+void debug_count_zl(Ctx &c, const int *zl, int *cnt)
+{
+    k_dbg_zl<<<1, 64, 0, c.stream>>>(zl, cnt);
+    HEC_HIP(hipGetLastError());
+}
+
 // ================================================================================ hoisted mod-up ==
 // A trie node's rotations all key-switch digits of the same polynomial, permuted.  With D = INTT(c1)
 // of the node (canonical, coefficient form) the child for Galois element elt has digit J
