@@ -638,7 +638,9 @@ void set_device(hec_context *ctx)
 
 void d2d(Ctx &c, void *dst, const void *src, std::size_t words)
 {
-    if (words) HEC_HIP(hipMemcpyAsync(dst, src, words * sizeof(u64), hipMemcpyDeviceToDevice, c.stream));
+    if (!words) return;
+    if (c.kernel_memops) dev_copy64(c, (u64 *)dst, (const u64 *)src, words);
+    else HEC_HIP(hipMemcpyAsync(dst, src, words * sizeof(u64), hipMemcpyDeviceToDevice, c.stream));
 }
 
 // ------------------------------------------------------------------ he::linalg driver -----
@@ -927,7 +929,7 @@ void matvec_core(hec_context *ctx, const hec_ciphertext *const *diags, const hec
         }
         std::vector<Hoist> hs(D);
         for (int d = 0; d < D; ++d) hs[d] = hoist_alloc(c, s, (int)p, (int)l);
-        HEC_HIP(hipMemsetAsync(c.zflag, 0, 2 * sizeof(int), c.stream));
+        dev_zero(c, c.zflag, 2 * sizeof(int));
         walk_trie_hoisted(c, s, trie, 0, Xa, 0, (int)p, (int)l, ctx, gkm, bufs, hs, S2, c.hoist_min_children, visit,
                           before_write);
     } else {
@@ -1402,6 +1404,7 @@ int hec_context_create(uint64_t N, const uint64_t *mod, uint64_t K, int device, 
         if (const char *f = std::getenv("HEC_POISON")) c.poison = f[0] != '0';
         if (const char *f = std::getenv("HEC_LANE_SERIAL")) c.lane_serial = f[0] != '0';
         if (const char *f = std::getenv("HEC_DEBUG_LANES")) c.debug_lanes = f[0] != '0';
+        if (const char *f = std::getenv("HEC_KERNEL_MEMOPS")) c.kernel_memops = f[0] != '0';
         c.N = N;
         c.logN = __builtin_ctzll(N);
         c.K = K;
@@ -1588,6 +1591,7 @@ int hec_context_set_option(hec_context *ctx, const char *name, int64_t value)
             else if (n == "poison") c.poison = value != 0;
             else if (n == "lane_serial") c.lane_serial = value != 0;
             else if (n == "debug_lanes") c.debug_lanes = value != 0;
+            else if (n == "kernel_memops") c.kernel_memops = value != 0;
             else if (n == "hoist") c.hoist = value != 0;
             else if (n == "hoist_min") c.hoist_min_children = (int)std::max<int64_t>(1, value);
             else if (n == "hmac") c.hmac_cfg = (int)value;

@@ -1312,11 +1312,40 @@ void fan_modup(Ctx &c, const u64 *D, u64 *E, int B, int l, bool direct, int *zl)
     }
     FanModUp f{D, E, l, c.logN, (int)c.K - 1, c.primes};
     if (zl) {
-        HEC_HIP(hipMemsetAsync(zl, 0, (1 + (std::size_t)B * l * (HEC_ZCAP + 1)) * sizeof(int), c.stream));
+        dev_zero(c, zl, (1 + (std::size_t)B * l * (HEC_ZCAP + 1)) * sizeof(int));
         f.zl = zl;
         f.zflag = c.zflag;
     }
     fan_dispatch(c, B * l, f, g);
+}
+
+// Device fills and copies as engine kernels on the context stream (HEC_KERNEL_MEMOPS=1), in place of the runtime's
+// hipMemsetAsync / device-to-device hipMemcpyAsync
+__global__ void __launch_bounds__(256) k_fill32(u32 *__restrict__ p, u32 v, u64 n)
+{
+    for (u64 i = (u64)blockIdx.x * 256 + threadIdx.x; i < n; i += (u64)gridDim.x * 256) p[i] = v;
+}
+__global__ void __launch_bounds__(256) k_copy64(u64 *__restrict__ dst, const u64 *__restrict__ src, u64 n)
+{
+    for (u64 i = (u64)blockIdx.x * 256 + threadIdx.x; i < n; i += (u64)gridDim.x * 256) dst[i] = src[i];
+}
+void dev_fill32(Ctx &c, void *p, u32 v, std::size_t bytes)
+{
+    const u64 n = bytes / 4;
+    if (!n) return;
+    k_fill32<<<(unsigned)std::min<u64>((n + 255) / 256, 8192), 256, 0, c.stream>>>((u32 *)p, v, n);
+    HEC_HIP(hipGetLastError());
+}
+void dev_copy64(Ctx &c, u64 *dst, const u64 *src, std::size_t words)
+{
+    if (!words) return;
+    k_copy64<<<(unsigned)std::min<u64>((words + 255) / 256, 8192), 256, 0, c.stream>>>(dst, src, words);
+    HEC_HIP(hipGetLastError());
+}
+void dev_zero(Ctx &c, void *p, std::size_t bytes)
+{
+    if (c.kernel_memops) dev_fill32(c, p, 0, bytes);
+    else HEC_HIP(hipMemsetAsync(p, 0, bytes, c.stream));
 }
 
 // debug (HEC_DEBUG_LANES): count the hoisted nodes whose zero list is not empty (uniform residues almost never have a
@@ -1355,7 +1384,7 @@ __global__ void __launch_bounds__(256) k_zscan(const u64 *__restrict__ D, int *_
 
 void zero_scan(Ctx &c, const u64 *D, int nlimbs, int *zl)
 {
-    HEC_HIP(hipMemsetAsync(zl, 0, (1 + (std::size_t)nlimbs * (HEC_ZCAP + 1)) * sizeof(int), c.stream));
+    dev_zero(c, zl, (1 + (std::size_t)nlimbs * (HEC_ZCAP + 1)) * sizeof(int));
     k_zscan<<<dim3((unsigned)(c.N / 256), nlimbs), 256, 0, c.stream>>>(D, zl, c.zflag, c.logN);
     HEC_HIP(hipGetLastError());
 }
