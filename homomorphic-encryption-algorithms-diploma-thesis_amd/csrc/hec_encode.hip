@@ -164,8 +164,8 @@ void encode_batch(Ctx &c, const double *re, const double *im, u64 nv, int count,
     const int logc = logN - 1 < 11 ? logN - 1 : 11, ts = logN - logc;
     const double2 *roots = reinterpret_cast<const double2 *>(c.enc_tw);
     double2 *a = reinterpret_cast<double2 *>(work);
-    HEC_HIP(hipMemsetAsync(maxabs, 0, count * sizeof(u64), c.stream));
-    HEC_HIP(hipMemsetAsync(work, 0, (u64)count * N * sizeof(double2), c.stream));
+    dev_zero(c, maxabs, count * sizeof(u64));
+    dev_zero(c, work, (u64)count * N * sizeof(double2));
     if (nv) {
         k_enc_scatter<<<dim3((unsigned)((nv + 255) / 256), count), 256, 0, c.stream>>>(re, im, nv, c.enc_map, a, logN);
         HEC_HIP(hipGetLastError());

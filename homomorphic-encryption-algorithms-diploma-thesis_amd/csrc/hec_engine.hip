@@ -254,8 +254,7 @@ void ensure(hec_ciphertext *ct, std::size_t words)
     if (ct->d) HEC_HIP(hipFree(ct->d));
     ct->d = dalloc(words);
     ct->cap = words;
-    if (ct->ctx && ct->ctx->c.poison)
-        HEC_HIP(hipMemsetAsync(ct->d, 0xFF, words * sizeof(u64), ct->ctx->c.stream));
+    if (ct->ctx && ct->ctx->c.poison) dev_fill(ct->ctx->c, ct->d, 0xFFFFFFFFu, words * sizeof(u64));
 }
 
 // stack-style carving of the context workspace; kernels are stream ordered, so a region released
@@ -285,7 +284,7 @@ struct Scratch {
         if (top + w > c.ws.words) throw std::logic_error("workspace overflow");
         u64 *p = c.ws.base + top;
         top += w;
-        if (c.poison) HEC_HIP(hipMemsetAsync(p, 0xFF, w * sizeof(u64), c.stream));
+        if (c.poison) dev_fill(c, p, 0xFFFFFFFFu, w * sizeof(u64));
         return p;
     }
 };

@@ -105,7 +105,11 @@ struct Ctx {
     // residue can have (2^64 - 1; a NaN as FP64 bits) and the parity tests fail deterministically
     bool poison = false;
     bool lane_serial = false;      // HEC_LANE_SERIAL=1 (debug): the lanes run one after another, each drained
-    bool kernel_memops = false;    // HEC_KERNEL_MEMOPS=1: engine fill / copy kernels for workspace zeroing and D2D copies
+    // stream-ordered workspace fills and device-to-device copies as the engine's own kernels (k_fill32 / k_copy64) in
+    // place of hipMemsetAsync / hipMemcpyAsync D2D.  Default since round 5: with the runtime calls, concurrent batch
+    // lanes read a zero list whose fill had not landed (the round-2/4 bit mismatch);
+    // HEC_KERNEL_MEMOPS=0 restores the runtime calls (A/B only)
+    bool kernel_memops = true;
     bool debug_lanes = false;      // HEC_DEBUG_LANES=1 (debug): per call, report nodes with zero lists, the overflow
                                    // flag and changes of the per-key tables (stderr)
     // profiling (ProfScope in hec_engine.hip)
@@ -159,9 +163,11 @@ void fan_modup(Ctx &c, const u64 *D, u64 *E, int B, int l, bool direct = false, 
 #define HEC_ZCAP 8
 void zero_scan(Ctx &c, const u64 *D, int nlimbs, int *zl);
 void debug_count_zl(Ctx &c, const int *zl, int *cnt);  // HEC_DEBUG_LANES: ++*cnt when zl[0] != 0
-// stream-ordered device fill / copy as engine kernels; dev_zero uses them when c.kernel_memops, else hipMemsetAsync
+// stream-ordered device fill / copy as engine kernels; dev_fill / dev_zero use them when c.kernel_memops, else the
+// runtime's hipMemsetAsync
 void dev_fill32(Ctx &c, void *p, u32 v, std::size_t bytes);
 void dev_copy64(Ctx &c, u64 *dst, const u64 *src, std::size_t words);
+void dev_fill(Ctx &c, void *p, u32 v, std::size_t bytes);
 void dev_zero(Ctx &c, void *p, std::size_t bytes);
 void hoisted_mac(Ctx &c, PolyArr X1, const u64 *E, const u64 *W, const int *zl, const u64 *key, u64 *ACC, int B,
                  int l, u32 elt);

@@ -1319,8 +1319,8 @@ void fan_modup(Ctx &c, const u64 *D, u64 *E, int B, int l, bool direct, int *zl)
     fan_dispatch(c, B * l, f, g);
 }
 
-// Device fills and copies as engine kernels on the context stream (HEC_KERNEL_MEMOPS=1), in place of the runtime's
-// hipMemsetAsync / device-to-device hipMemcpyAsync
+// Device fills and copies as engine kernels on the context stream (c.kernel_memops, the default), in place of the
+// runtime's hipMemsetAsync / device-to-device hipMemcpyAsync (see hec_internal.h)
 __global__ void __launch_bounds__(256) k_fill32(u32 *__restrict__ p, u32 v, u64 n)
 {
     for (u64 i = (u64)blockIdx.x * 256 + threadIdx.x; i < n; i += (u64)gridDim.x * 256) p[i] = v;
@@ -1342,11 +1342,13 @@ void dev_copy64(Ctx &c, u64 *dst, const u64 *src, std::size_t words)
     k_copy64<<<(unsigned)std::min<u64>((words + 255) / 256, 8192), 256, 0, c.stream>>>(dst, src, words);
     HEC_HIP(hipGetLastError());
 }
-void dev_zero(Ctx &c, void *p, std::size_t bytes)
+void dev_fill(Ctx &c, void *p, u32 v, std::size_t bytes)  // bytes: a multiple of 4
 {
-    if (c.kernel_memops) dev_fill32(c, p, 0, bytes);
-    else HEC_HIP(hipMemsetAsync(p, 0, bytes, c.stream));
+    if (c.kernel_memops) dev_fill32(c, p, v, bytes);
+    else if (v == 0 || v == 0xFFFFFFFFu) HEC_HIP(hipMemsetAsync(p, (int)(v & 0xFF), bytes, c.stream));
+    else HEC_HIP(hipMemsetD32Async((hipDeviceptr_t)p, (int)v, bytes / 4, c.stream));
 }
+void dev_zero(Ctx &c, void *p, std::size_t bytes) { dev_fill(c, p, 0, bytes); }
 
 // debug (HEC_DEBUG_LANES): count the hoisted nodes whose zero list is not empty (uniform residues almost never have a
 // zero coefficient, so a count is a sign the list was read before it was written)
