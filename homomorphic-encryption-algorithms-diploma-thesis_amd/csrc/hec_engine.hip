@@ -1404,6 +1404,7 @@ int hec_context_create(uint64_t N, const uint64_t *mod, uint64_t K, int device, 
         if (const char *f = std::getenv("HEC_LANE_SERIAL")) c.lane_serial = f[0] != '0';
         if (const char *f = std::getenv("HEC_DEBUG_LANES")) c.debug_lanes = f[0] != '0';
         if (const char *f = std::getenv("HEC_KERNEL_MEMOPS")) c.kernel_memops = f[0] != '0';
+        if (const char *f = std::getenv("HEC_SPLIT_BFLY")) c.split_bfly = std::atoi(f);
         c.N = N;
         c.logN = __builtin_ctzll(N);
         c.K = K;
@@ -1508,6 +1509,21 @@ int hec_context_create(uint64_t N, const uint64_t *mod, uint64_t K, int device, 
         HEC_HIP(hipMalloc(&c.itw, K * N * sizeof(ulonglong2)));
         HEC_HIP(hipMemcpy(c.tw, tw.data(), K * N * sizeof(ulonglong2), hipMemcpyHostToDevice));
         HEC_HIP(hipMemcpy(c.itw, itw.data(), K * N * sizeof(ulonglong2), hipMemcpyHostToDevice));
+        {   // split-input Shoup words a = w 2^31 mod q of tw / itw (integer primes; hec_device.h shoup_split_lazy)
+            std::vector<u64> ta(K * N, 0), ita(K * N, 0);
+            for (uint64_t i = 0; i < K; ++i) {
+                if (c.hprimes[i].fp) continue;
+                const u64 q = c.q[i];
+                for (uint64_t k = 0; k < N; ++k) {
+                    ta[i * N + k] = (u64)(((u128)tw[i * N + k].x << 31) % q);
+                    ita[i * N + k] = (u64)(((u128)itw[i * N + k].x << 31) % q);
+                }
+            }
+            HEC_HIP(hipMalloc(&c.tws, K * N * sizeof(u64)));
+            HEC_HIP(hipMalloc(&c.itws, K * N * sizeof(u64)));
+            HEC_HIP(hipMemcpy(c.tws, ta.data(), K * N * sizeof(u64), hipMemcpyHostToDevice));
+            HEC_HIP(hipMemcpy(c.itws, ita.data(), K * N * sizeof(u64), hipMemcpyHostToDevice));
+        }
         const u64 P = c.q[K - 1];
         for (uint64_t i = 0; i < c.L; ++i) {
             const u64 q = c.q[i], pi = invm(P % q, q);
@@ -1552,6 +1568,8 @@ int hec_context_destroy(hec_context *ctx)
         (void)hipFree(c.itw);
         (void)hipFree(c.twb);
         (void)hipFree(c.itwb);
+        (void)hipFree(c.tws);
+        (void)hipFree(c.itws);
         for (double *p : {c.twf, c.itwf, c.twbf, c.itwbf}) (void)hipFree(p);
         (void)hipFree(c.enc_map);
         (void)hipFree(c.enc_tw);
@@ -1591,6 +1609,7 @@ int hec_context_set_option(hec_context *ctx, const char *name, int64_t value)
             else if (n == "lane_serial") c.lane_serial = value != 0;
             else if (n == "debug_lanes") c.debug_lanes = value != 0;
             else if (n == "kernel_memops") c.kernel_memops = value != 0;
+            else if (n == "split_bfly") c.split_bfly = (int)value;
             else if (n == "hoist") c.hoist = value != 0;
             else if (n == "hoist_min") c.hoist_min_children = (int)std::max<int64_t>(1, value);
             else if (n == "hmac") c.hmac_cfg = (int)value;

@@ -259,6 +259,7 @@ using DivRoundIO_B = DivRoundIOB<true>;
 struct TwTables {
     const ulonglong2 *a, *b;  // integer: pass A (SEAL order), pass B ([s][i][chunk])
     const double *fa, *fb;    // FP64 twins
+    const u64 *sa = nullptr;  // w 2^31 mod q for a (the split-input Shoup butterflies, hec_device.h)
 };
 
 // One round: stages [S0, S1) of a P = 2^LOGP point sub-transform.  Thread `ts` of its segment owns
@@ -292,6 +293,28 @@ struct ConstTw {
         return ulonglong2{a, b};
     }
 };
+// The same SEAL-ordered tables with the split-input Shoup word a = w 2^31 mod q of each integer twiddle (kSplit):
+// the integer butterflies then run shoup_split_lazy (8 instead of 10 32-bit multiplies, hec_device.h)
+template <class IdxF>
+struct GlobalTwS : GlobalTw<IdxF> {
+    static constexpr bool kSplit = true;
+    const u64 *ta;
+    __device__ u64 a(int s, int i) const { return ta[this->idx(s, i)]; }
+};
+struct ConstTwS : ConstTw {
+    static constexpr bool kSplit = true;
+    const u64 *ta;
+    __device__ u64 a(int s, int i) const
+    {
+        typedef __attribute__((address_space(4))) const u64 cword;
+        return ((cword *)ta)[(1u << s) + (unsigned)i];
+    }
+};
+template <class T, class = void>
+struct HasSplitTw : std::false_type {};
+template <class T>
+struct HasSplitTw<T, std::void_t<decltype(T::kSplit)>> : std::bool_constant<T::kSplit> {};
+
 struct LdsTw {  // entry k = 2^s - 1 + i of this segment; FP: one word (double bits), integer: {w, w_shoup}
     const u64 *row;
     __device__ double f(int s, int i) const { return __longlong_as_double((long long)row[(1 << s) - 1 + i]); }
@@ -306,11 +329,12 @@ struct LdsTw {  // entry k = 2^s - 1 + i of this segment; FP: one word (double b
 // the round's stages.  Round-stage st uses twiddle twidx(S0+st, hi 2^st + m), m = a >> (D - st) the top st bits
 // of the element slot a.  The group's 2^D - 1 twiddles do not depend on data: GroupTw loads them first, so their
 // latency overlaps the data loads.
-template <int S0, int D, bool FP>
+template <int S0, int D, bool FP, bool SPL = false>
 struct GroupTw {
     static constexpr int NQ = 1 << D;
     double wf[FP ? NQ - 1 : 1];
     ulonglong2 wi[FP ? 1 : NQ - 1];
+    u64 wa[(FP || !SPL) ? 1 : NQ - 1];  // SPL: the split-input words (a TwG with kSplit)
     template <class TwG>
     __device__ __forceinline__ void load(int hi, const TwG &twg)
     {
@@ -320,6 +344,7 @@ struct GroupTw {
             for (int m = 0; m < (1 << st); ++m) {
                 if constexpr (FP) wf[(1 << st) - 1 + m] = twg.f(S0 + st, (hi << st) | m);
                 else wi[(1 << st) - 1 + m] = twg.w(S0 + st, (hi << st) | m);
+                if constexpr (!FP && SPL) wa[(1 << st) - 1 + m] = twg.a(S0 + st, (hi << st) | m);
             }
     }
     template <bool INV>
@@ -340,6 +365,9 @@ struct GroupTw {
                     else gs_bfly_fp(X, Y, wf[wk], pr.qd, pr.qinv);
                     v[a] = (u64)__double_as_longlong(X);
                     v[a | bit] = (u64)__double_as_longlong(Y);
+                } else if constexpr (SPL) {
+                    if constexpr (!INV) ct_bfly_s(v[a], v[a | bit], wi[wk].x, wi[wk].y, wa[wk], q, two_q);
+                    else gs_bfly_s(v[a], v[a | bit], wi[wk].x, wi[wk].y, wa[wk], q, two_q);
                 } else {
                     if constexpr (!INV) ct_bfly(v[a], v[a | bit], wi[wk].x, wi[wk].y, q, two_q);
                     else gs_bfly(v[a], v[a | bit], wi[wk].x, wi[wk].y, q, two_q);
@@ -1027,6 +1055,11 @@ __device__ __forceinline__ void ntt_round_r(u64 *v, int ts, const TwG &twg, cons
                     else gs_bfly_fp(x, y, w, pr.qd, pr.qinv);
                     X = (u64)__double_as_longlong(x);
                     Y = (u64)__double_as_longlong(y);
+                } else if constexpr (HasSplitTw<TwG>::value) {
+                    const ulonglong2 w = twg.w(S0 + st, (hi << st) | m);
+                    const u64 wa = twg.a(S0 + st, (hi << st) | m);
+                    if constexpr (!INV) ct_bfly_s(X, Y, w.x, w.y, wa, q, two_q);
+                    else gs_bfly_s(X, Y, w.x, w.y, wa, q, two_q);
                 } else {
                     const ulonglong2 w = twg.w(S0 + st, (hi << st) | m);
                     if constexpr (!INV) ct_bfly(X, Y, w.x, w.y, q, two_q);
@@ -1044,7 +1077,9 @@ __device__ __forceinline__ void ntt_round_r(u64 *v, int ts, const TwG &twg, cons
 // DB: two alternating LDS tiles and one barrier per exchange (2 blocks per CU at N = 2^15); DB = false: one
 // tile and a second barrier per target.  (One tile with 3 waves per SIMD forced, 168 VGPRs and 20-30 spilled,
 // measured slower: k_fan 3,565 vs 2,601 ms per step.)
-template <int LOGP, int NSEG, class FAN, bool DB = true>
+// SPL: the integer primes' butterflies as split-input Shoup (inv.sa / fwd.sa, hec_device.h shoup_split_lazy), bit 0 in
+// the round on scalar (block-uniform) twiddles, bit 1 in the round on per-thread twiddles
+template <int LOGP, int NSEG, class FAN, int SPL, bool DB = true>
 __global__ void __launch_bounds__(NSEG *(1 << LOGP) / 16)
     k_fan2(const FAN fan, TwTables inv, TwTables fwd, const DevPrime *__restrict__ primes, int logN)
 {
@@ -1071,7 +1106,10 @@ __global__ void __launch_bounds__(NSEG *(1 << LOGP) / 16)
         for (int k = 0; k < 16; ++k) v[k] = src.in[gblock(k)];
         const GlobalTw<decltype(twidx)> tg{twidx, inv.a + ((u64)src.prime << logN), inv.fa + ((u64)src.prime << logN)};
         const ConstTw ctg{inv.a + ((u64)src.prime << logN), inv.fa + ((u64)src.prime << logN)};
+        const GlobalTwS<decltype(twidx)> tgs{tg, SPL ? inv.sa + ((u64)src.prime << logN) : nullptr};
+        const ConstTwS ctgs{ctg, SPL ? inv.sa + ((u64)src.prime << logN) : nullptr};
         if (ps.fp) ntt_round_r<LOGP, 4, LOGP, true, true>(v, ts, tg, ps);
+        else if constexpr ((SPL & 2) != 0) ntt_round_r<LOGP, 4, LOGP, true, false>(v, ts, tgs, ps);
         else ntt_round_r<LOGP, 4, LOGP, true, false>(v, ts, tg, ps);
 #pragma unroll
         for (int k = 0; k < 16; ++k) lds[lblock(k)] = v[k];
@@ -1089,7 +1127,8 @@ __global__ void __launch_bounds__(NSEG *(1 << LOGP) / 16)
                 if constexpr (FAN::kSrcDouble) d[k] = (u64)__double_as_longlong(u2d(d[k]));
             }
         } else {
-            ntt_round_r<LOGP, 0, 4, true, false, ConstTw, true>(v, ts, ctg, ps);
+            if constexpr ((SPL & 1) != 0) ntt_round_r<LOGP, 0, 4, true, false, ConstTwS, true>(v, ts, ctgs, ps);
+            else ntt_round_r<LOGP, 0, 4, true, false, ConstTw, true>(v, ts, ctg, ps);
 #pragma unroll
             for (int k = 0; k < 16; ++k) d[k] = shoup(v[k], ps.ninv, ps.ninv_q, ps.q);
         }
@@ -1111,6 +1150,8 @@ __global__ void __launch_bounds__(NSEG *(1 << LOGP) / 16)
         const DevPrime pt = cprime(primes, tgt.prime);
         const GlobalTw<decltype(twidx)> tw{twidx, fwd.a + ((u64)tgt.prime << logN), fwd.fa + ((u64)tgt.prime << logN)};
         const ConstTw ctw{fwd.a + ((u64)tgt.prime << logN), fwd.fa + ((u64)tgt.prime << logN)};
+        const GlobalTwS<decltype(twidx)> tws{tw, SPL ? fwd.sa + ((u64)tgt.prime << logN) : nullptr};
+        const ConstTwS ctws{ctw, SPL ? fwd.sa + ((u64)tgt.prime << logN) : nullptr};
         u64 *tile = lds + (DB ? buf * TILE : 0);
         buf ^= 1;
         if (!DB) __syncthreads();  // the previous exchange's reads are done
@@ -1120,7 +1161,8 @@ __global__ void __launch_bounds__(NSEG *(1 << LOGP) / 16)
             ntt_round_r<LOGP, 0, 4, false, true, ConstTw, true>(v, ts, ctw, pt);
         } else {
             fan.xf16(tgt, false, d, lo, v, FAN::kSrcDouble && ps.fp);
-            ntt_round_r<LOGP, 0, 4, false, false, ConstTw, true>(v, ts, ctw, pt);
+            if constexpr ((SPL & 1) != 0) ntt_round_r<LOGP, 0, 4, false, false, ConstTwS, true>(v, ts, ctws, pt);
+            else ntt_round_r<LOGP, 0, 4, false, false, ConstTw, true>(v, ts, ctw, pt);
         }
 #pragma unroll
         for (int k = 0; k < 16; ++k) tile[lstride(k)] = v[k];
@@ -1128,6 +1170,7 @@ __global__ void __launch_bounds__(NSEG *(1 << LOGP) / 16)
 #pragma unroll
         for (int k = 0; k < 16; ++k) v[k] = tile[lblock(k)];
         if (pt.fp) ntt_round_r<LOGP, 4, LOGP, false, true>(v, ts, tw, pt);
+        else if constexpr ((SPL & 2) != 0) ntt_round_r<LOGP, 4, LOGP, false, false>(v, ts, tws, pt);
         else ntt_round_r<LOGP, 4, LOGP, false, false>(v, ts, tw, pt);
         // (16-B stores and loads through lane-pair trades measured slower: 2,613 vs 2,580 ms per step, round 4)
 #pragma unroll
@@ -1138,8 +1181,8 @@ __global__ void __launch_bounds__(NSEG *(1 << LOGP) / 16)
 // k_fan2 over JPB source jobs per block (FanModUpT): the next job's source words are loaded during the current
 // job's last target.  A separate kernel: folded into k_fan2, the restructured body costs the divide-and-round
 // fan-out (one job per block) 12 VGPRs and a wave.
-template <int LOGP, int NSEG, class FAN, int JPB, bool DB = true>
-__global__ void __launch_bounds__(NSEG *(1 << LOGP) / 16)
+template <int LOGP, int NSEG, class FAN, int JPB, int SPL, bool DB = true>
+__global__ void __launch_bounds__(NSEG *(1 << LOGP) / 16, 2)  // 2 waves per SIMD (<= 256 VGPRs) with the split words too
     k_fan2j(const FAN fan, TwTables inv, TwTables fwd, const DevPrime *__restrict__ primes, int logN, int njobs)
 {
     constexpr int P = 1 << LOGP, TPS = P / 16, LD = NSEG + 1, TILE = P * LD;
@@ -1177,7 +1220,10 @@ __global__ void __launch_bounds__(NSEG *(1 << LOGP) / 16)
             for (int k = 0; k < 16; ++k) v[k] = d[k];
             const GlobalTw<decltype(twidx)> tg{twidx, inv.a + ((u64)src.prime << logN), inv.fa + ((u64)src.prime << logN)};
             const ConstTw ctg{inv.a + ((u64)src.prime << logN), inv.fa + ((u64)src.prime << logN)};
+            const GlobalTwS<decltype(twidx)> tgs{tg, SPL ? inv.sa + ((u64)src.prime << logN) : nullptr};
+            const ConstTwS ctgs{ctg, SPL ? inv.sa + ((u64)src.prime << logN) : nullptr};
             if (ps.fp) ntt_round_r<LOGP, 4, LOGP, true, true>(v, ts, tg, ps);
+            else if constexpr ((SPL & 2) != 0) ntt_round_r<LOGP, 4, LOGP, true, false>(v, ts, tgs, ps);
             else ntt_round_r<LOGP, 4, LOGP, true, false>(v, ts, tg, ps);
             u64 *tile = lds + (DB ? buf * TILE : 0);
             if (!DB || jj > 0) __syncthreads();  // the previous job's last exchange reads are done
@@ -1197,7 +1243,8 @@ __global__ void __launch_bounds__(NSEG *(1 << LOGP) / 16)
                     if constexpr (FAN::kSrcDouble) d[k] = (u64)__double_as_longlong(u2d(d[k]));
                 }
             } else {
-                ntt_round_r<LOGP, 0, 4, true, false, ConstTw, true>(v, ts, ctg, ps);
+                if constexpr ((SPL & 1) != 0) ntt_round_r<LOGP, 0, 4, true, false, ConstTwS, true>(v, ts, ctgs, ps);
+                else ntt_round_r<LOGP, 0, 4, true, false, ConstTw, true>(v, ts, ctg, ps);
 #pragma unroll
                 for (int k = 0; k < 16; ++k) d[k] = shoup(v[k], ps.ninv, ps.ninv_q, ps.q);
             }
@@ -1225,6 +1272,8 @@ __global__ void __launch_bounds__(NSEG *(1 << LOGP) / 16)
             const DevPrime pt = cprime(primes, tgt.prime);
             const GlobalTw<decltype(twidx)> tw{twidx, fwd.a + ((u64)tgt.prime << logN), fwd.fa + ((u64)tgt.prime << logN)};
             const ConstTw ctw{fwd.a + ((u64)tgt.prime << logN), fwd.fa + ((u64)tgt.prime << logN)};
+            const GlobalTwS<decltype(twidx)> tws{tw, SPL ? fwd.sa + ((u64)tgt.prime << logN) : nullptr};
+            const ConstTwS ctws{ctw, SPL ? fwd.sa + ((u64)tgt.prime << logN) : nullptr};
             u64 *tile = lds + (DB ? buf * TILE : 0);
             buf ^= 1;
             if (!DB) __syncthreads();  // the previous exchange's reads are done
@@ -1234,7 +1283,8 @@ __global__ void __launch_bounds__(NSEG *(1 << LOGP) / 16)
                 ntt_round_r<LOGP, 0, 4, false, true, ConstTw, true>(v, ts, ctw, pt);
             } else {
                 fan.xf16(tgt, false, d, lo, v, FAN::kSrcDouble && ps.fp);
-                ntt_round_r<LOGP, 0, 4, false, false, ConstTw, true>(v, ts, ctw, pt);
+                if constexpr ((SPL & 1) != 0) ntt_round_r<LOGP, 0, 4, false, false, ConstTwS, true>(v, ts, ctws, pt);
+                else ntt_round_r<LOGP, 0, 4, false, false, ConstTw, true>(v, ts, ctw, pt);
             }
 #pragma unroll
             for (int k = 0; k < 16; ++k) tile[lstride(k)] = v[k];
@@ -1251,9 +1301,12 @@ __global__ void __launch_bounds__(NSEG *(1 << LOGP) / 16)
 #pragma unroll
                     for (int gi = 0; gi < G1; ++gi) g1[gi].template run<false>(v + gi * (1 << D1), pt);
                 } else {
-                    GroupTw<4, D1, false> g1[G1];
+                    GroupTw<4, D1, false, (SPL & 2) != 0> g1[G1];
 #pragma unroll
-                    for (int gi = 0; gi < G1; ++gi) g1[gi].load(ts * G1 + gi, tw);
+                    for (int gi = 0; gi < G1; ++gi) {
+                        if constexpr ((SPL & 2) != 0) g1[gi].load(ts * G1 + gi, tws);
+                        else g1[gi].load(ts * G1 + gi, tw);
+                    }
                     asm volatile("" ::: "memory");
                     load_src(job + 1, d);
 #pragma unroll
@@ -1261,6 +1314,8 @@ __global__ void __launch_bounds__(NSEG *(1 << LOGP) / 16)
                 }
             } else if (pt.fp) {
                 ntt_round_r<LOGP, 4, LOGP, false, true>(v, ts, tw, pt);
+            } else if constexpr ((SPL & 2) != 0) {
+                ntt_round_r<LOGP, 4, LOGP, false, false>(v, ts, tws, pt);
             } else {
                 ntt_round_r<LOGP, 4, LOGP, false, false>(v, ts, tw, pt);
             }
@@ -1278,13 +1333,24 @@ template <int LOGR, int LOGC, int NA, class FAN>
 static void run_fan(Ctx &c, int njobs, const FAN &fan, int groups)
 {
     constexpr int R = 1 << LOGR, C = 1 << LOGC;
-    const TwTables fwd{c.tw, c.twb, c.twf, c.twbf}, inv{c.itw, c.itwb, c.itwf, c.itwbf};
+    const TwTables fwd{c.tw, c.twb, c.twf, c.twbf, c.tws}, inv{c.itw, c.itwb, c.itwf, c.itwbf, c.itws};
     constexpr int JPB = FAN::kJobs;
-    if constexpr (JPB > 1)
-        k_fan2j<LOGR, NA, FAN, JPB><<<dim3(C / NA, (njobs + JPB - 1) / JPB, groups), NA * R / 16, 0, c.stream>>>(
-            fan, inv, fwd, c.primes, c.logN, njobs);
-    else
-        k_fan2<LOGR, NA><<<dim3(C / NA, njobs, groups), NA * R / 16, 0, c.stream>>>(fan, inv, fwd, c.primes, c.logN);
+    const dim3 grid(C / NA, (njobs + JPB - 1) / JPB, groups);
+    // c.split_bfly (HEC_SPLIT_BFLY): 0 plain Shoup everywhere; 1 split-input Shoup in k_fan2 (the mod-down fan-out);
+    // 2 also in k_fan2j's per-thread-twiddle rounds; 3 in all of k_fan2j's rounds
+    const int sp = c.split_bfly;
+    if constexpr (JPB > 1) {
+        if (sp >= 3)
+            k_fan2j<LOGR, NA, FAN, JPB, 3><<<grid, NA * R / 16, 0, c.stream>>>(fan, inv, fwd, c.primes, c.logN, njobs);
+        else if (sp == 2)
+            k_fan2j<LOGR, NA, FAN, JPB, 2><<<grid, NA * R / 16, 0, c.stream>>>(fan, inv, fwd, c.primes, c.logN, njobs);
+        else
+            k_fan2j<LOGR, NA, FAN, JPB, 0><<<grid, NA * R / 16, 0, c.stream>>>(fan, inv, fwd, c.primes, c.logN, njobs);
+    } else if (sp >= 1) {
+        k_fan2<LOGR, NA, FAN, 3><<<grid, NA * R / 16, 0, c.stream>>>(fan, inv, fwd, c.primes, c.logN);
+    } else {
+        k_fan2<LOGR, NA, FAN, 0><<<grid, NA * R / 16, 0, c.stream>>>(fan, inv, fwd, c.primes, c.logN);
+    }
     HEC_HIP(hipGetLastError());
 }
 template <class FAN>

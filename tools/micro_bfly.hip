@@ -68,13 +68,47 @@ __device__ __forceinline__ u64 csub_sign(u64 x, u64 m)  // x < 2m... : x - m if 
     return d + (m & s);
 }
 
+// V6 / V7 (round 5): split-input Shoup.  Y = y1 2^31 + y0 (Y < 4q < 2^62, y0, y1 < 2^31), so
+//   Y w = y1 a + y0 b (mod q),  a = w 2^31 mod q, b = w,
+// and the quotient comes from two 32-bit Shoup factors a' = floor(a 2^32 / q), b' = floor(b 2^32 / q):
+//   qh = (y1 a' + y0 b') >> 32  (the sum < 2^63 + 2^63, exact in one v_mad_u64_u32 chain),
+// T / q - qh < (y1 + y0) / 2^32 + 1 < 2, so qh is Q or Q - 1 and t = T - qh q is in [0, 2q) (no extra subtraction).
+// Multiplies: 2 (quotient) + 4 (T mod 2^64) + 1 (qh q with q = 2^60 - c, V6) or 2 (any q, V7), against Shoup's 10.
+struct TwS { u64 a, b; u32 ap, bp; };
+__device__ __forceinline__ u64 shoup_split(u64 Y, const TwS &w, u64 q, u32 c, bool special)
+{
+    const u32 y0 = (u32)Y & 0x7fffffffu, y1 = (u32)(Y >> 31);
+    const u64 qs = (u64)y1 * w.ap + (u64)y0 * w.bp;
+    const u32 qh = (u32)(qs >> 32);
+    const u64 T = (u64)y1 * (u32)w.a + (u64)y0 * (u32)w.b +
+                  ((u64)(y1 * (u32)(w.a >> 32) + y0 * (u32)(w.b >> 32)) << 32);
+    if (special) return T + (u64)qh * c - ((u64)qh << 60);
+    return T - ((u64)qh * (u32)q + ((u64)(qh * (u32)(q >> 32)) << 32));
+}
+
+// V8: V7 with the quotient product folded into the same multiply-add chain through nq = 2^64 - q: t = (y0 b + y1 a +
+// qh nq) mod 2^64, the low words in one v_mad_u64_u32 chain, the high words as three 32-bit products
+__device__ __forceinline__ u64 shoup_split_nq(u64 Y, const TwS &w, u64 nq)
+{
+    const u32 y0 = (u32)Y & 0x7fffffffu, y1 = (u32)(Y >> 31);
+    const u32 qh = (u32)(((u64)y1 * w.ap + (u64)y0 * w.bp) >> 32);
+    const u64 lo = (u64)y0 * (u32)w.b + (u64)y1 * (u32)w.a + (u64)qh * (u32)nq;
+    const u32 hi = y0 * (u32)(w.b >> 32) + y1 * (u32)(w.a >> 32) + qh * (u32)(nq >> 32);
+    return lo + ((u64)hi << 32);
+}
+
 template <int V>
 __global__ void __launch_bounds__(256) k_bfly(u64 *io, const u64 *tw_in, const double *twd, u64 q, int iters)
 {
     const int g = blockIdx.x * 256 + threadIdx.x;
     u64 X[CHAINS], Y[CHAINS], W[CHAINS], WQ[CHAINS];
     double FH[CHAINS], FL[CHAINS];
+    TwS WS[CHAINS];
     for (int c = 0; c < CHAINS; ++c) {
+        WS[c].a = tw_in[2 * CHAINS + 3 * c];
+        WS[c].b = tw_in[2 * CHAINS + 3 * c + 1];
+        WS[c].ap = (u32)tw_in[2 * CHAINS + 3 * c + 2];
+        WS[c].bp = (u32)(tw_in[2 * CHAINS + 3 * c + 2] >> 32);
         X[c] = io[(size_t)g * 2 * CHAINS + 2 * c];
         Y[c] = io[(size_t)g * 2 * CHAINS + 2 * c + 1];
         W[c] = tw_in[2 * c];
@@ -107,6 +141,16 @@ __global__ void __launch_bounds__(256) k_bfly(u64 *io, const u64 *tw_in, const d
             } else if constexpr (V == 5) {
                 const u64 x = csub_sign(X[c], two_q);
                 const u64 tt = shoup_lazy(Y[c], W[c], WQ[c], q);
+                X[c] = x + tt;
+                Y[c] = x - tt + two_q;
+            } else if constexpr (V == 6 || V == 7) {
+                const u64 x = X[c] >= two_q ? X[c] - two_q : X[c];
+                const u64 tt = shoup_split(Y[c], WS[c], q, (u32)((1ull << 60) - q), V == 6);
+                X[c] = x + tt;
+                Y[c] = x - tt + two_q;
+            } else if constexpr (V == 8) {
+                const u64 x = X[c] >= two_q ? X[c] - two_q : X[c];
+                const u64 tt = shoup_split_nq(Y[c], WS[c], 0 - q);
                 X[c] = x + tt;
                 Y[c] = x - tt + two_q;
             } else if constexpr (V == 2) {
@@ -165,13 +209,17 @@ int main()
     std::vector<u64> init(n);
     u64 s = 88172645463325252ull;
     for (auto &v : init) { s ^= s << 13; s ^= s >> 7; s ^= s << 17; v = s % (4 * q); }
-    std::vector<u64> tw(2 * CHAINS);
+    std::vector<u64> tw(5 * CHAINS);
     std::vector<double> twd(2 * CHAINS);
     for (int c = 0; c < CHAINS; ++c) {
         s ^= s << 13; s ^= s >> 7; s ^= s << 17;
         const u64 w = s % q;
         tw[2 * c] = w;
         tw[2 * c + 1] = (u64)(((unsigned __int128)w << 64) / q);
+        const u64 a = (u64)(((unsigned __int128)w << 31) % q);
+        tw[2 * CHAINS + 3 * c] = a;
+        tw[2 * CHAINS + 3 * c + 1] = w;
+        tw[2 * CHAINS + 3 * c + 2] = (u64)(((unsigned __int128)a << 32) / q) | ((u64)(((unsigned __int128)w << 32) / q) << 32);
         const long double f = (long double)w / (long double)q * 2147483648.0L;
         twd[2 * c] = (double)f;
         twd[2 * c + 1] = (double)(f - (long double)twd[2 * c]);
@@ -191,5 +239,8 @@ int main()
     run<3>("shoup, q = 2^60 - c", q, init, d_io, d_tw, d_twd, ref);
     run<4>("shoup, q = 2^60 - c, sign csub", q, init, d_io, d_tw, d_twd, ref);
     run<5>("shoup, sign csub", q, init, d_io, d_tw, d_twd, ref);
+    run<6>("split-input shoup, 2^60 - c", q, init, d_io, d_tw, d_twd, ref);
+    run<7>("split-input shoup, any q", q, init, d_io, d_tw, d_twd, ref);
+    run<8>("split-input shoup, nq chain", q, init, d_io, d_tw, d_twd, ref);
     return 0;
 }
