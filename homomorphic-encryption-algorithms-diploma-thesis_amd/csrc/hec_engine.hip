@@ -488,18 +488,6 @@ Hoist hoist_alloc(const Ctx &c, Scratch &s, int B, int l)
     h.acc0 = s.take((u64)HOIST_GROUP * h.sacc);
     return h;
 }
-// pass B of the hoisted digits: canonical NTT form for k_hmacm; with HEC_HMAC=3 the integer target rows only (k_hmacb
-// runs the FP64 rows' pass B itself)
-void modup_h_b(Ctx &c, const Hoist &h, int B, int l)
-{
-    if (c.hmac_cfg == 3) {
-        ProfScope k(c, "k:k_ntt/modup_h_b", 2.0 * B * c.imap_nint[l] * l);
-        ks_modup_int(c, h.E, B, l);
-        return;
-    }
-    ProfScope k(c, "k:k_ntt/modup_h_b", 2.0 * B * l * l);
-    ks_modup(c, h.D, h.E, B, l, 2);
-}
 void hoist_node(Ctx &c, PolyArr X, int B, int l, const Hoist &h)
 {
     const u64 N = c.N;
@@ -516,7 +504,8 @@ void hoist_node(Ctx &c, PolyArr X, int B, int l, const Hoist &h)
             ProfScope k(c, "k:k_fan2j/hoist", (double)B * l * (l + 1));
             fan_modup(c, h.D, h.E, B, l, false, h.zl);
         }
-        modup_h_b(c, h, B, l);
+        ProfScope k(c, "k:k_ntt/modup_h_b", 2.0 * B * l * l);
+        ks_modup(c, h.D, h.E, B, l, 2);  // pass B, canonical NTT-form digits
         return;
     }
     {
@@ -537,7 +526,8 @@ void hoist_node(Ctx &c, PolyArr X, int B, int l, const Hoist &h)
         ProfScope k(c, "k:k_fan2j/hoist", (double)B * l * (l + 1));
         fan_modup(c, h.D, h.E, B, l, true);  // pass A of every NTT_I(D_J mod q_I), from the canonical D
     }
-    modup_h_b(c, h, B, l);
+    ProfScope k(c, "k:k_ntt/modup_h_b", 2.0 * B * l * l);
+    ks_modup(c, h.D, h.E, B, l, 2);      // pass B, canonical NTT-form digits
 }
 // one child of a hoisted node: OUT = key switch of apply_galois(X, elt) (X: the node's ciphertexts)
 void hoisted_child(Ctx &c, Scratch &s, PolyArr X, const Hoist &h, const u64 *W, const u64 *key, PolyArr OUT, int B,
@@ -774,16 +764,6 @@ void walk_trie_hoisted(Ctx &c, Scratch &s, const RotTrie &t, int node, PolyArr s
             // an odd group's last three children as one 3-child launch (the digits read once, not twice)
             if (c.hmac_odd3 && grp == 2 && ng - q0 == 3) nk = 3;
             ProfScope ps(c, "ks_hmac");  // digits E (B l^2) + c1 (B l) [+ c0 (B l), folded] + per child
-            if (c.hmac_cfg == 3) {  // integer targets (k_hmacm, NTT-form rows), FP64 targets (k_hmacb, pass-A rows)
-                const double ki = c.imap_nint[l], kf = K - ki;
-                {
-                    ProfScope k(c, "k:k_hmacm", (double)B * ki * (l + 1) + nk * (2.0 * l * ki + 3.0 * ki + 2.0 * B * ki));
-                    hoisted_mac_group(c, PolyArr{src.p + src.sk, src.sb, 0}, X0, h.E, h.zl, kids + q0, nk, B, l);
-                }
-                ProfScope k(c, "k:k_hmacb", (double)B * kf * (l + 1) + nk * (2.0 * l * kf + 3.0 * kf + 2.0 * B * kf));
-                hoisted_mac_fp_passb(c, PolyArr{src.p + src.sk, src.sb, 0}, X0, h.E, h.zl, kids + q0, nk, B, l);
-                continue;
-            }
             ProfScope k(c, "k:k_hmacm",
                         (double)B * (l * l + l + (fold ? l : 0)) + nk * (2.0 * l * K + 3.0 * K + 2.0 * B * K));
             if (c.hmac_cfg == 2)

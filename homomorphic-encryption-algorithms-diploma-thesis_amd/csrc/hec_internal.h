@@ -92,8 +92,7 @@ struct Ctx {
     int tensor_xcd = 0;            // HEC_TENSOR_XCD: k_tensor_multi2 grid in XCD clusters of this many batch groups
     bool hoist = true;             // HEC_HOIST=0: no hoisted mod-up in the rotation trie walk
     int hoist_min_children = 2;    // HEC_HOIST_MIN: children a trie node needs to be hoisted
-    int hmac_cfg = 2;              // HEC_HMAC: 3 as 2 with the FP64 targets' digit pass B inside the MAC (k_hmacb),
-                                   // 2 a sibling group per k_hmacm launch (slots of 2 children), 1 one
+    int hmac_cfg = 2;              // HEC_HMAC: 2 a sibling group per k_hmacm launch (slots of 2 children), 1 one
                                    // launch per sibling pair (round 4), 0 one hoisted MAC per child
     int hoist_scan = 1;            // HEC_HOIST_SCAN=0: hoisted node as INTT pass B, pass A, k_zscan, direct fan-out
                                    // (1: INTT pass B, then the fan-out finishes the INTT and lists the zeros)
@@ -195,11 +194,6 @@ void hoisted_mac_3(Ctx &c, PolyArr X1, PolyArr X0, const u64 *E, const int *zl, 
 void hoisted_mac_group(Ctx &c, PolyArr X1, PolyArr X0, const u64 *E, const int *zl, const HChildSpec *kids, int nkids,
                        int B, int l);
 int hoisted_group(const Ctx &c);  // children per hoisted_mac_multi call for c.hmac_cfg
-// HEC_HMAC=3: the sibling group's FP64 targets from the pass-A digits with their pass B in the MAC (k_hmacb); the
-// integer target rows of E go through ks_modup_int (pass B) and hoisted_mac_group (k_hmacm, integer targets only)
-void hoisted_mac_fp_passb(Ctx &c, PolyArr X1, PolyArr X0, const u64 *E, const int *zl, const HChildSpec *kids,
-                          int nkids, int B, int l);
-void ks_modup_int(Ctx &c, u64 *E, int B, int l);
 void fan_divide_round(Ctx &c, const u64 *Y, u64 ysb, u64 ysk, u64 *Z, int B, int nk, int nl, int last_idx);
 void galois_permute(Ctx &c, PolyArr in, PolyArr out, int B, int nk, int nl, u32 elt);
 void tensor_acc(Ctx &c, PolyArr R, const u64 *A, u64 a_sk, PolyArr ACC, int B, int l, bool assign);

@@ -1917,10 +1917,9 @@ __global__ void __launch_bounds__(256, MINW)  // MINW waves per SIMD: 3 -> <= 16
 }
 
 // nkids children in slots of CG (the last slot may hold fewer), at most NS slots
-// int_only: the integer-arithmetic targets only (HEC_HMAC=3: k_hmacb takes the FP64 targets)
 template <int BTF, int BTI, int CG, int NS = 1, int MINW = (BTF * CG <= 8 && BTI * CG <= 8) ? 3 : 2>
 static void launch_hmacm(Ctx &c, PolyArr X1, PolyArr X0, const u64 *E, const int *zl, const HChildSpec *kids,
-                         int nkids, int B, int l, bool int_only = false)
+                         int nkids, int B, int l)
 {
     HSlots<CG, NS> S{};
     S.ns = (nkids + CG - 1) / CG;
@@ -1932,20 +1931,19 @@ static void launch_hmacm(Ctx &c, PolyArr X1, PolyArr X0, const u64 *E, const int
     }
     const int nint = c.imap_nint[l], X = (int)(c.N / 512);
     const int gI = (X * nint + 7) / 8 * 8, gF = (X * (l + 1 - nint) + 7) / 8 * 8;
-    const int wsplit = gI * ((B + BTI - 1) / BTI), total = wsplit + (int_only ? 0 : gF * ((B + BTF - 1) / BTF));
-    if (total == 0) return;
+    const int wsplit = gI * ((B + BTI - 1) / BTI), total = wsplit + gF * ((B + BTF - 1) / BTF);
     k_hmacm<BTF, BTI, CG, MINW, NS><<<dim3((unsigned)(total * S.ns)), 256, 0, c.stream>>>(
         X1, X0, E, zl, S, B, l, (int)c.K, c.logN, c.primes, c.imap_at(l), l + 1, nint, c.cji, c.psipow, wsplit);
     HEC_HIP(hipGetLastError());
 }
 
-int hoisted_group(const Ctx &c) { return c.hmac_cfg >= 2 ? HMAC_MAX_CHILDREN : c.hmac_cfg ? 2 : 1; }
+int hoisted_group(const Ctx &c) { return c.hmac_cfg == 2 ? HMAC_MAX_CHILDREN : c.hmac_cfg ? 2 : 1; }
 
 void hoisted_mac_group(Ctx &c, PolyArr X1, PolyArr X0, const u64 *E, const int *zl, const HChildSpec *kids, int nkids,
                        int B, int l)
 {
     static_assert(HMAC_MAX_CHILDREN <= 2 * 3, "3 slots of 2 children");
-    launch_hmacm<4, 2, 2, 3>(c, X1, X0, E, zl, kids, nkids, B, l, c.hmac_cfg == 3);
+    launch_hmacm<4, 2, 2, 3>(c, X1, X0, E, zl, kids, nkids, B, l);
 }
 
 void hoisted_mac_multi(Ctx &c, PolyArr X1, PolyArr X0, const u64 *E, const int *zl, const HChildSpec *kids, int nkids,
@@ -2322,293 +2320,6 @@ void ks_modup_mac(Ctx &c, const u64 *D, u64 *E, PolyArr T, const u64 *key, u64 *
     case 16: run_modup_fused<8, 8, 16, 4>(c, D, E, T, key, ACC, B, l, part, elt); break;
     default: throw std::invalid_argument("poly_modulus_degree must be 2^10 .. 2^16");
     }
-}
-
-// ============================================================ hoisted MAC with the digits' pass B (k_hmacb)
-// HEC_HMAC=3: the FP64 targets of a hoisted node's sibling group read the node's digits E[b][I][J] in the pass-A
-// domain, as the fan-out wrote them, and run the forward pass B inside the MAC kernel (as k_bmac does for one
-// rotation), so the NTT-form copy of those rows is never written and read back (hoist_node's pass B keeps the integer
-// rows only, which k_hmacm still serves).  The Galois permutation of NTT slots maps each pass-B chunk (C consecutive
-// slots) onto one chunk: for a slot k = chunk C + u, the low logR + 1 bits of elt (2 bitrev(k) + 1) depend on the
-// chunk alone, and they are the top bits of gal(k).  So a block that owns whole source chunks scatters every child's
-// products into that child's output chunk, exactly as k_hmacm's threads scatter their source pairs.
-// A thread owns EPT = 4 consecutive source slots (two pairs) of one chunk for one batch entry and CG children.  Grid:
-// the NS slots of one (chunk block, I, b) are consecutive blocks of one XCD (the pass-A tile from HBM once, then from
-// that XCD's L2) and the B batch entries of one (chunk block, I) follow them there (each child's key chunk from L2).
-// Every term is the one k_hmacm adds (same W KW start, folded c0, digit products, zero corrections), exact mod q_I
-// and canonicalised once, so the outputs are bit-identical.
-template <int LOGP, int NSEG, int EPT, int CG>
-__device__ __forceinline__ void hmacb_body(u64 *lds, u64 *ltw, PolyArr X1, PolyArr X0, const u64 *__restrict__ E,
-                                           const int *__restrict__ zl, const HChildren<CG> &ch, const TwTables &tt,
-                                           const DevPrime &pr, u64 Pq, int I, int kI, int b, int xb, int logN, int l,
-                                           int K, const u64 *__restrict__ cji, const u64 *__restrict__ psipow)
-{
-    constexpr int P = 1 << LOGP, THREADS = NSEG * P / EPT, LD = bmac_ld(LOGP), TWS = 2 * P + 2;
-    constexpr bool SWZ = BSwz<LOGP>::on;
-    static_assert(EPT == 4, "rounds of 2 stages; two source pairs per thread");
-    static_assert(SWZ || LOGP <= 6, "P = 128 / 256 chunk rows are swizzled");
-    const u64 N = 1ull << logN;
-    const int seg0 = xb * NSEG;
-    const u64 base = (u64)seg0 << LOGP;
-    const double *twf = tt.fb + ((u64)kI << logN);
-    const int ts = (int)threadIdx.x % (P / EPT), sg = (int)threadIdx.x / (P / EPT);
-    auto addr = [sg](int x) { return sg * LD + x + (x >> 4); };
-    const u64 R = 1ull << (logN - LOGP);
-    for (int t = threadIdx.x; t < NSEG * (P - 1); t += THREADS) {  // the chunks' pass-B twiddles, as k_bmac
-        const int sl = t % NSEG, k = t / NSEG;
-        const int st = 31 - __clz(k + 1), i = k + 1 - (1 << st);
-        ltw[sl * TWS + k] = (u64)__double_as_longlong(twf[R * ((1ull << st) - 1) + (u64)i * R + (u64)(seg0 + sl)]);
-    }
-    const LdsTw twg{ltw + sg * TWS};
-    const u64 g0 = ((u64)(seg0 + sg) << LOGP) + (u64)ts * EPT;  // this thread's first source slot
-    // per child and source pair p (slots g0 + 2p, + 1): the output pair kc (even slot) and whether it is swapped
-    u64 kc[CG][2];
-    bool sw[CG][2];
-    double f[CG][EPT][2];  // [child][source slot][poly]
-#pragma unroll
-    for (int q = 0; q < CG; ++q)
-#pragma unroll
-        for (int p = 0; p < 2; ++p) {
-            kc[q][p] = 0;
-            sw[q][p] = false;
-            f[q][2 * p][0] = f[q][2 * p][1] = f[q][2 * p + 1][0] = f[q][2 * p + 1][1] = 0.0;
-            if (q >= ch.n) continue;
-            const u32 t = galois_src((u32)(g0 + 2 * p), ch.c[q].einv, logN);
-            kc[q][p] = t & ~1u;
-            sw[q][p] = t & 1;
-            const ulonglong2 w = *(const ulonglong2 *)(ch.c[q].W + ((u64)kI << logN) + kc[q][p]);
-            const ulonglong2 m0 = *(const ulonglong2 *)(ch.c[q].KW + ((u64)I << logN) + kc[q][p]);
-            const ulonglong2 m1 = *(const ulonglong2 *)(ch.c[q].KW + ((u64)(l + 1 + I) << logN) + kc[q][p]);
-            const double wx = u2d(w.x), wy = u2d(w.y);
-            const double a0 = fp_mulmod(wx, u2d(m0.x), pr.qd, pr.qinv), a1 = fp_mulmod(wy, u2d(m0.y), pr.qd, pr.qinv);
-            const double c0 = fp_mulmod(wx, u2d(m1.x), pr.qd, pr.qinv), c1 = fp_mulmod(wy, u2d(m1.y), pr.qd, pr.qinv);
-            const bool s = sw[q][p];  // output slot kc + (j ^ s) holds source slot g0 + 2p + j
-            f[q][2 * p][0] = s ? a1 : a0;
-            f[q][2 * p + 1][0] = s ? a0 : a1;
-            f[q][2 * p][1] = s ? c1 : c0;
-            f[q][2 * p + 1][1] = s ? c0 : c1;
-        }
-    if (X0.p != nullptr && I < l) {  // the node's c0 folded into every child's c0 accumulator: X0 (P mod q_I)
-        const double pmd = u2d(barrett64(Pq, pr.q, pr.r1));
-        const u64 *xp = X0.p + b * X0.sb + ((u64)I << logN) + g0;
-        const ulonglong2 x01 = *(const ulonglong2 *)xp, x23 = *(const ulonglong2 *)(xp + 2);
-        const double t4[4] = {fp_mulmod(u2d(x01.x), pmd, pr.qd, pr.qinv), fp_mulmod(u2d(x01.y), pmd, pr.qd, pr.qinv),
-                              fp_mulmod(u2d(x23.x), pmd, pr.qd, pr.qinv), fp_mulmod(u2d(x23.y), pmd, pr.qd, pr.qinv)};
-#pragma unroll
-        for (int q = 0; q < CG; ++q)
-#pragma unroll
-            for (int e = 0; e < EPT; ++e) f[q][e][0] += t4[e];
-    }
-    // the pass-A words of digit J's chunks, as 16-B pairs: pair w = threadIdx.x + e THREADS holds block elements 2w, 2w+1
-    u64 nx[EPT];
-    auto load_tile = [&](int J) {
-        const ulonglong2 *sp = (const ulonglong2 *)(E + (((u64)((b * (l + 1) + I) * l + J)) << logN) + base);
-#pragma unroll
-        for (int e = 0; e < EPT / 2; ++e) {
-            const ulonglong2 w = sp[threadIdx.x + e * THREADS];
-            nx[2 * e] = w.x;
-            nx[2 * e + 1] = w.y;
-        }
-    };
-    auto next_digit = [&](int J) { return J + 1 == I ? J + 2 : J + 1; };
-    u64 *const row = lds + sg * LD;
-    int jn = I == 0 ? 1 : 0;
-    if (jn < l) load_tile(jn);
-    for (int J = 0; J < l; ++J) {
-        // the children's key words of digit J at their output pairs, in source order (swapped with the pair)
-        ulonglong2 kw[CG][2][2];
-#pragma unroll
-        for (int q = 0; q < CG; ++q)
-#pragma unroll
-            for (int p = 0; p < 2; ++p)
-#pragma unroll
-                for (int k = 0; k < 2; ++k) {
-                    kw[q][p][k] = ulonglong2{0, 0};
-                    if (q < ch.n) {
-                        const ulonglong2 v = *(const ulonglong2 *)(ch.c[q].key + (((u64)(J * 2 + k) * K + kI) << logN) +
-                                                                  kc[q][p]);
-                        kw[q][p][k] = sw[q][p] ? ulonglong2{v.y, v.x} : v;
-                    }
-                }
-        u64 v[EPT];
-        if (J == I) {  // the node's own c1 at q_I (NTT form, canonical) at the thread's slots
-            const u64 *xp = X1.p + b * X1.sb + ((u64)I << logN) + g0;
-            const ulonglong2 x01 = *(const ulonglong2 *)xp, x23 = *(const ulonglong2 *)(xp + 2);
-            v[0] = (u64)__double_as_longlong(u2d(x01.x));
-            v[1] = (u64)__double_as_longlong(u2d(x01.y));
-            v[2] = (u64)__double_as_longlong(u2d(x23.x));
-            v[3] = (u64)__double_as_longlong(u2d(x23.y));
-        } else {
-#pragma unroll
-            for (int e = 0; e < EPT; e += 2) {
-                const int li = 2 * (threadIdx.x + (e / 2) * THREADS);
-                if constexpr (SWZ) {
-                    *(ulonglong2 *)(lds + (li / P) * LD + bswz<LOGP>(li % P)) = ulonglong2{nx[e], nx[e + 1]};
-                } else {
-                    lds[(li / P) * LD + (li % P) + ((li % P) >> 4)] = nx[e];
-                    lds[(li / P) * LD + (li % P) + 1 + (((li % P) + 1) >> 4)] = nx[e + 1];
-                }
-            }
-            jn = next_digit(J);
-            if (jn < l) load_tile(jn);
-            __syncthreads();
-            if constexpr (SWZ) {
-                ntt_round_x<LOGP, 0, 2, EPT, false, true, false>(row, ts, twg, pr, nullptr);
-                __syncthreads();
-                ntt_round_x<LOGP, 2, 4, EPT, false, true, false>(row, ts, twg, pr, nullptr);
-                __syncthreads();
-                ntt_round_x<LOGP, 4, 6, EPT, false, true, false>(row, ts, twg, pr, nullptr);
-                __syncthreads();
-                ntt_round_x<LOGP, 6, LOGP, EPT, false, true, true>(row, ts, twg, pr, v);
-            } else {
-                ntt_round_g<LOGP, 0, 2, EPT, false, true, false>(lds, addr, ts, twg, pr, nullptr);
-                __syncthreads();
-                ntt_round_g<LOGP, 2, 4, EPT, false, true, false>(lds, addr, ts, twg, pr, nullptr);
-                __syncthreads();
-                ntt_round_g<LOGP, 4, LOGP, EPT, false, true, true>(lds, addr, ts, twg, pr, v);
-            }
-        }
-#pragma unroll
-        for (int q = 0; q < CG; ++q) {
-            if (q >= ch.n) break;
-#pragma unroll
-            for (int e = 0; e < EPT; ++e) {
-                const double dv = __longlong_as_double((long long)v[e]);  // |dv| < 10 q_I (pass B) or canonical
-                const ulonglong2 k0 = kw[q][e >> 1][0], k1 = kw[q][e >> 1][1];
-                f[q][e][0] += fp_mulmod(dv, u2d((e & 1) ? k0.y : k0.x), pr.qd, pr.qinv);
-                f[q][e][1] += fp_mulmod(dv, u2d((e & 1) ? k1.y : k1.x), pr.qd, pr.qinv);
-            }
-        }
-        if (J != I) __syncthreads();  // the rounds' LDS reads are done before the next digit's tile is written
-    }
-    if (zl[0] != 0) {  // the rare zero corrections (k_hmacm's, per source pair)
-        const u64 *pp = psipow + ((u64)kI << (logN + 1));
-        for (int J = 0; J < l; ++J) {
-            if (J == I) continue;
-            const int *z = zl + 1 + (b * l + J) * (HEC_ZCAP + 1);
-            const int nz = min(z[0], HEC_ZCAP);
-            if (nz == 0) continue;
-            const u64 cj = cji[J * K + kI];
-#pragma unroll
-            for (int q = 0; q < CG; ++q) {
-                if (q >= ch.n) break;
-#pragma unroll
-                for (int p = 0; p < 2; ++p) {
-                    const u64 ko0 = kc[q][p] | (u64)sw[q][p], ko1 = kc[q][p] | (u64)!sw[q][p];
-                    u64 c0 = 0, c1 = 0;
-                    for (int zi = 0; zi < nz; ++zi) {
-                        u64 tt2 = ((u64)z[1 + zi] * ch.c[q].elt) & (2 * N - 1);
-                        if (tt2 < N) continue;
-                        tt2 -= N;
-                        const u64 ex0 = ((2 * (u64)bitrev((u32)ko0, logN) + 1) * tt2) & (2 * N - 1);
-                        const u64 ex1 = ((2 * (u64)bitrev((u32)ko1, logN) + 1) * tt2) & (2 * N - 1);
-                        c0 = addmod(c0, mulmod(cj, pp[ex0], pr), pr.q);
-                        c1 = addmod(c1, mulmod(cj, pp[ex1], pr), pr.q);
-                    }
-                    if (c0 == 0 && c1 == 0) continue;
-                    const u64 n0 = c0 ? pr.q - c0 : 0, n1 = c1 ? pr.q - c1 : 0;
-                    const u64 *kp = ch.c[q].key + (((u64)(J * 2) * K + kI) << logN) + kc[q][p];
-                    ulonglong2 k0 = *(const ulonglong2 *)kp, k1 = *(const ulonglong2 *)(kp + ((u64)K << logN));
-                    if (sw[q][p]) {
-                        k0 = ulonglong2{k0.y, k0.x};
-                        k1 = ulonglong2{k1.y, k1.x};
-                    }
-                    f[q][2 * p][0] += fp_mulmod(u2d(n0), u2d(k0.x), pr.qd, pr.qinv);
-                    f[q][2 * p + 1][0] += fp_mulmod(u2d(n1), u2d(k0.y), pr.qd, pr.qinv);
-                    f[q][2 * p][1] += fp_mulmod(u2d(n0), u2d(k1.x), pr.qd, pr.qinv);
-                    f[q][2 * p + 1][1] += fp_mulmod(u2d(n1), u2d(k1.y), pr.qd, pr.qinv);
-                }
-            }
-        }
-    }
-#pragma unroll
-    for (int q = 0; q < CG; ++q) {
-        if (q >= ch.n) break;
-#pragma unroll
-        for (int p = 0; p < 2; ++p) {
-            u64 r[4];
-#pragma unroll
-            for (int k = 0; k < 2; ++k) {
-                r[2 * k] = fp_canon(f[q][2 * p][k], pr.qd, pr.qinv);
-                r[2 * k + 1] = fp_canon(f[q][2 * p + 1][k], pr.qd, pr.qinv);
-            }
-            u64 *o0 = ch.c[q].ACC + (((u64)((b * 2 + 0) * (l + 1) + I)) << logN) + kc[q][p];
-            u64 *o1 = ch.c[q].ACC + (((u64)((b * 2 + 1) * (l + 1) + I)) << logN) + kc[q][p];
-            *(ulonglong2 *)o0 = sw[q][p] ? ulonglong2{r[1], r[0]} : ulonglong2{r[0], r[1]};
-            *(ulonglong2 *)o1 = sw[q][p] ? ulonglong2{r[3], r[2]} : ulonglong2{r[2], r[3]};
-        }
-    }
-}
-
-// FP64 targets Imap[nI0, nI) only (the integer ones stay on k_hmacm)
-template <int LOGP, int NSEG, int EPT, int CG, int NS>
-__global__ void __launch_bounds__(NSEG *(1 << LOGP) / EPT)
-    k_hmacb(PolyArr X1, PolyArr X0, const u64 *__restrict__ E, const int *__restrict__ zl, const HSlots<CG, NS> S,
-            TwTables tt, const DevPrime *__restrict__ primes, const int *__restrict__ Imap, int nI0, int nI, int B,
-            int l, int K, int logN, const u64 *__restrict__ cji, const u64 *__restrict__ psipow)
-{
-    __shared__ __attribute__((aligned(16))) u64 lds[NSEG * bmac_ld(LOGP)];
-    __shared__ __attribute__((aligned(16))) u64 ltw[NSEG * (2 * (1 << LOGP) + 2)];
-    const int w = blockIdx.x, ns = S.ns;
-    const int g8 = w & 7, t8 = w >> 3, slot = t8 % ns, rest = t8 / ns, b = rest % B, G = (rest / B) * 8 + g8;
-    const int X = (1 << (logN - LOGP)) / NSEG;
-    if (G >= X * (nI - nI0)) return;  // block-uniform
-    const int yi = nI0 + G / X, xb = G % X;
-    const int I = Imap[yi];
-    const int kI = I == l ? K - 1 : I;
-    const DevPrime pr = primes[kI];
-    const u64 Pq = cprime(primes, K - 1).q;
-    hmacb_body<LOGP, NSEG, EPT, CG>(lds, ltw, X1, X0, E, zl, S.s[slot], tt, pr, Pq, I, kI, b, xb, logN, l, K, cji,
-                                    psipow);
-}
-
-template <int LOGC, int NB2, int CG, int NS>
-static void launch_hmacb_t(Ctx &c, PolyArr X1, PolyArr X0, const u64 *E, const int *zl, const HChildSpec *kids,
-                           int nkids, int B, int l)
-{
-    HSlots<CG, NS> S{};
-    S.ns = (nkids + CG - 1) / CG;
-    if (nkids < 1 || S.ns > NS) throw std::invalid_argument("hoisted MAC: children per launch");
-    for (int q = 0; q < nkids; ++q) {
-        HChildren<CG> &ch = S.s[q / CG];
-        ch.c[q % CG] = HChild{kids[q].elt, kids[q].einv, kids[q].key, kids[q].W, kids[q].ACC, kids[q].KW};
-        ch.n = q % CG + 1;
-    }
-    const int nint = c.imap_nint[l], nI = l + 1;
-    const int X = (1 << (c.logN - LOGC)) / NB2, gpad = (X * (nI - nint) + 7) / 8 * 8;
-    if (gpad == 0) return;
-    const TwTables fwd{c.tw, c.twb, c.twf, c.twbf};
-    k_hmacb<LOGC, NB2, 4, CG, NS><<<dim3((unsigned)(gpad * B * S.ns)), NB2 * (1 << LOGC) / 4, 0, c.stream>>>(
-        X1, X0, E, zl, S, fwd, c.primes, c.imap_at(l), nint, nI, B, l, (int)c.K, c.logN, c.cji, c.psipow);
-    HEC_HIP(hipGetLastError());
-}
-
-void hoisted_mac_fp_passb(Ctx &c, PolyArr X1, PolyArr X0, const u64 *E, const int *zl, const HChildSpec *kids,
-                          int nkids, int B, int l)
-{
-    static_assert(HMAC_MAX_CHILDREN <= 2 * 3, "3 slots of 2 children");
-    // <pass-B chunk size, chunks per block> as k_bmac (ks_modup_mac)
-    switch (c.logN) {
-    case 10: launch_hmacb_t<5, 16, 2, 3>(c, X1, X0, E, zl, kids, nkids, B, l); break;
-    case 11: launch_hmacb_t<5, 16, 2, 3>(c, X1, X0, E, zl, kids, nkids, B, l); break;
-    case 12: launch_hmacb_t<6, 8, 2, 3>(c, X1, X0, E, zl, kids, nkids, B, l); break;
-    case 13: launch_hmacb_t<6, 8, 2, 3>(c, X1, X0, E, zl, kids, nkids, B, l); break;
-    case 14: launch_hmacb_t<7, 4, 2, 3>(c, X1, X0, E, zl, kids, nkids, B, l); break;
-    case 15: launch_hmacb_t<7, 4, 2, 3>(c, X1, X0, E, zl, kids, nkids, B, l); break;
-    case 16: launch_hmacb_t<8, 4, 2, 3>(c, X1, X0, E, zl, kids, nkids, B, l); break;
-    default: throw std::invalid_argument("poly_modulus_degree must be 2^10 .. 2^16");
-    }
-}
-
-// pass B of the hoisted digits for the integer-arithmetic target rows only (HEC_HMAC=3)
-void ks_modup_int(Ctx &c, u64 *E, int B, int l)
-{
-    const int nint = c.imap_nint[l];
-    if (nint == 0) return;
-    ModUpMap m{l, c.logN, (int)c.K - 1, c.imap_at(l), nint};
-    ModUpIO_A a{m, nullptr, E, c.primes};
-    ModUpIO_B bio{m, E};
-    ntt_dispatch<false>(c, B * nint * l, a, bio, 2);
 }
 
 // =============================================================================== key MAC ===

@@ -413,9 +413,7 @@ def test_cfg5_params_matvec_bitexact(orc, hecdna):
                                  {"HEC_HOIST": "0"}, {"HEC_HOIST_MIN": "1"}, {"HEC_HOIST_MIN": "1", "HEC_FAN": "0"},
                                  {"HEC_HMAC": "0"}, {"HEC_HMAC": "0", "HEC_HOIST_MIN": "1"},
                                  {"HEC_HMAC": "1"}, {"HEC_HMAC": "1", "HEC_HMAC_ODD3": "0"},
-                                 {"HEC_HOIST_SCAN": "0"}, {"HEC_KERNEL_MEMOPS": "0"},
-                                 {"HEC_HMAC": "3"}, {"HEC_HMAC": "3", "HEC_HOIST_SCAN": "0"}, {"HEC_SPLIT_BFLY": "0"},
-                                 {"HEC_SPLIT_BFLY": "3"}])
+                                 {"HEC_HOIST_SCAN": "0"}, {"HEC_KERNEL_MEMOPS": "0"}])
 def test_keyswitch_variants_bitexact(orc, hecdna, env):
     """The engine's alternative key-switch schedules (separate mod-up pass B + MAC kernels; the fused
     kernel's key-load placements) give the same bits as the oracle."""
@@ -575,8 +573,7 @@ def _env_with(orc, hecdna, env, *args, **kw):
 
 
 @pytest.mark.parametrize("nzeros", [3, 40])  # 40 > HEC_ZCAP: the hoisted walk recomputes without hoisting
-@pytest.mark.parametrize("variant", [{}, {"HEC_HMAC": "0"}, {"HEC_HMAC": "1"}, {"HEC_HMAC": "1", "HEC_HMAC_ODD3": "0"},
-                                     {"HEC_HMAC": "3"}])
+@pytest.mark.parametrize("variant", [{}, {"HEC_HMAC": "0"}, {"HEC_HMAC": "1"}, {"HEC_HMAC": "1", "HEC_HMAC_ODD3": "0"}])
 def test_hoisted_modup_zero_coefficients(orc, hecdna, nzeros, variant):
     """The hoisted mod-up corrects for zero digit coefficients that the Galois automorphism negates
     (SEAL maps -0 to 0, not to q_J); a limb with more zeros than the kernels list falls back.  Every hoisted MAC
