@@ -901,51 +901,15 @@ void matvec_core(hec_context *ctx, const hec_ciphertext *const *diags, const hec
     // deferred and applied in one k_tensor_multi pass (the accumulator read/written once per batch); a
     // batch is flushed when full or before one of its rotation buffers is overwritten
     TensorBatch tb{};
-    // side stream (c.tensor_side): the batches' rotation buffers still read by an enqueued batch
-    const bool side = c.tensor_side && c.prof_mode == 0;
-    if (side && !c.side) {
-        HEC_HIP(hipStreamCreateWithFlags(&c.side, hipStreamNonBlocking));
-        HEC_HIP(hipEventCreateWithFlags(&c.side_ready, hipEventDisableTiming));
-        HEC_HIP(hipEventCreateWithFlags(&c.side_done, hipEventDisableTiming));
-    }
-    std::vector<const u64 *> side_reads;
-    struct SideGuard {  // an exception leaves no batch running into the workspace the next call reuses
-        Ctx &c;
-        bool on;
-        ~SideGuard()
-        {
-            if (on && std::uncaught_exceptions() > 0) (void)hipStreamSynchronize(c.side);
-        }
-    } side_guard{c, side};
     auto flush = [&] {
         if (tb.T == 0) return;
         ProfScope pr(c, "tensor");
         // T rotated inputs (2 B l each) + T diagonals (2 l, or l plaintext) + ACC read (unless first) + write
         const double accl = (pt ? 2.0 : 3.0) * p * l;
         ProfScope k(c, "k:k_tensor_multi2", tb.T * (2.0 * p * l + (pt ? 1.0 : 2.0) * l) + (first ? 1 : 2) * accl);
-        if (side) {  // after the main stream's rotations, in order with the earlier batches (the accumulator)
-            HEC_HIP(hipEventRecord(c.side_ready, c.stream));
-            HEC_HIP(hipStreamWaitEvent(c.side, c.side_ready, 0));
-            std::swap(c.stream, c.side);
-            try {
-                tensor_multi(c, tb, S2, l * N, l * N, Aa, (int)p, (int)l, first, pt);
-            } catch (...) {
-                std::swap(c.stream, c.side);
-                throw;
-            }
-            std::swap(c.stream, c.side);
-            HEC_HIP(hipEventRecord(c.side_done, c.side));
-            for (int t = 0; t < tb.T; ++t) side_reads.push_back(tb.r[t]);
-        } else {
-            tensor_multi(c, tb, S2, l * N, l * N, Aa, (int)p, (int)l, first, pt);
-        }
+        tensor_multi(c, tb, S2, l * N, l * N, Aa, (int)p, (int)l, first, pt);
         first = false;
         tb.T = 0;
-    };
-    auto side_join = [&] {  // the main stream waits for every enqueued batch
-        if (!side || side_reads.empty()) return;
-        HEC_HIP(hipStreamWaitEvent(c.stream, c.side_done, 0));
-        side_reads.clear();
     };
     auto visit = [&](std::size_t j, PolyArr src) {
         tb.r[tb.T] = src.p;
@@ -954,12 +918,7 @@ void matvec_core(hec_context *ctx, const hec_ciphertext *const *diags, const hec
     };
     auto before_write = [&](const u64 *buf) {
         for (int t = 0; t < tb.T; ++t)
-            if (tb.r[t] == buf) {
-                flush();
-                break;
-            }
-        for (const u64 *r : side_reads)
-            if (r == buf) return side_join();
+            if (tb.r[t] == buf) return flush();
     };
     if (hoist) {
         hec_galois_keys &gkm = const_cast<hec_galois_keys &>(*gk);  // negw is a per-key cache
@@ -976,7 +935,6 @@ void matvec_core(hec_context *ctx, const hec_ciphertext *const *diags, const hec
         walk_trie(c, s, trie, 0, Xa, 0, (int)p, (int)l, *gk, bufs, S2, visit, before_write);
     }
     flush();
-    side_join();
     if (hoist) {  // a digit limb with more zero coefficients than the hoisted MAC corrects: recompute
         int zfl[2] = {0, 0};
         HEC_HIP(hipMemcpyAsync(zfl, c.zflag, 2 * sizeof(int), hipMemcpyDeviceToHost, c.stream));
@@ -1042,8 +1000,6 @@ hec_context *make_lane(hec_context *parent)
     c.ev_used = 0;
     c.stream = nullptr;
     c.zflag = nullptr;
-    c.side = nullptr;  // created on first use, per lane
-    c.side_ready = c.side_done = nullptr;
     HEC_HIP(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
     c.own_stream = true;
     HEC_HIP(hipMalloc(&c.zflag, 2 * sizeof(int)));
@@ -1051,22 +1007,10 @@ hec_context *make_lane(hec_context *parent)
     HEC_HIP(hipEventCreateWithFlags(&l->lane_done, hipEventDisableTiming));
     return l;
 }
-void free_side(Ctx &c)
-{
-    if (c.side) {
-        (void)hipStreamSynchronize(c.side);
-        (void)hipStreamDestroy(c.side);
-    }
-    if (c.side_ready) (void)hipEventDestroy(c.side_ready);
-    if (c.side_done) (void)hipEventDestroy(c.side_done);
-    c.side = nullptr;
-    c.side_ready = c.side_done = nullptr;
-}
 void free_lane(hec_context *l)
 {
     Ctx &c = l->c;
     (void)hipStreamSynchronize(c.stream);
-    free_side(c);
     if (l->lane_done) (void)hipEventDestroy(l->lane_done);
     c.ws.release();
     (void)hipFree(c.zflag);
@@ -1461,7 +1405,6 @@ int hec_context_create(uint64_t N, const uint64_t *mod, uint64_t K, int device, 
         if (const char *f = std::getenv("HEC_DEBUG_LANES")) c.debug_lanes = f[0] != '0';
         if (const char *f = std::getenv("HEC_KERNEL_MEMOPS")) c.kernel_memops = f[0] != '0';
         if (const char *f = std::getenv("HEC_SPLIT_BFLY")) c.split_bfly = std::atoi(f);
-        if (const char *f = std::getenv("HEC_TENSOR_SIDE")) c.tensor_side = std::atoi(f);
         c.N = N;
         c.logN = __builtin_ctzll(N);
         c.K = K;
@@ -1614,7 +1557,6 @@ int hec_context_destroy(hec_context *ctx)
         (void)hipStreamSynchronize(c.stream);
         for (hec_context *l : ctx->lanes) free_lane(l);
         if (ctx->lanes_start) (void)hipEventDestroy(ctx->lanes_start);
-        free_side(c);
         delete ctx->comm;
         c.ws.release();
         (void)hipFree(c.primes);
@@ -1668,7 +1610,6 @@ int hec_context_set_option(hec_context *ctx, const char *name, int64_t value)
             else if (n == "debug_lanes") c.debug_lanes = value != 0;
             else if (n == "kernel_memops") c.kernel_memops = value != 0;
             else if (n == "split_bfly") c.split_bfly = (int)value;
-            else if (n == "tensor_side") c.tensor_side = (int)value;
             else if (n == "hoist") c.hoist = value != 0;
             else if (n == "hoist_min") c.hoist_min_children = (int)std::max<int64_t>(1, value);
             else if (n == "hmac") c.hmac_cfg = (int)value;

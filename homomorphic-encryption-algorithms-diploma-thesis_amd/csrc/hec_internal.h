@@ -90,12 +90,6 @@ struct Ctx {
     int tensor_defer_max = 12;     // HEC_TENSOR_DEFER: terminals per deferred tensor batch (1 = immediate)
     int tensor_defer_bufs = 8;     // HEC_TENSOR_BUFS: rotation buffers per trie depth
     int tensor_xcd = 0;            // HEC_TENSOR_XCD: k_tensor_multi2 grid in XCD clusters of this many batch groups
-    // HEC_TENSOR_SIDE: the deferred tensor batches (memory-bound) run on a second stream of the context, overlapping
-    // the VALU-bound key switches; the main stream waits for them (side_done) only before it overwrites a rotation
-    // buffer a batch still reads, and at the end of the trie walk.  Off while profiling (one stream, per-phase events)
-    int tensor_side = 1;
-    hipStream_t side = nullptr;
-    hipEvent_t side_ready = nullptr, side_done = nullptr;
     bool hoist = true;             // HEC_HOIST=0: no hoisted mod-up in the rotation trie walk
     int hoist_min_children = 2;    // HEC_HOIST_MIN: children a trie node needs to be hoisted
     int hmac_cfg = 2;              // HEC_HMAC: 2 a sibling group per k_hmacm launch (slots of 2 children), 1 one
