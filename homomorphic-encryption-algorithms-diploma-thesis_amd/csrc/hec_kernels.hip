@@ -1337,10 +1337,12 @@ static void run_fan(Ctx &c, int njobs, const FAN &fan, int groups)
     constexpr int JPB = FAN::kJobs;
     const dim3 grid(C / NA, (njobs + JPB - 1) / JPB, groups);
     // c.split_bfly (HEC_SPLIT_BFLY): 0 plain Shoup everywhere; 1 split-input Shoup in k_fan2 (the mod-down fan-out);
-    // 2 also in k_fan2j's per-thread-twiddle rounds; 3 in all of k_fan2j's rounds
+    // 2 also in k_fan2j's per-thread-twiddle rounds; 3 in all of k_fan2j's rounds; 4 k_fan2j's scalar-twiddle round only
     const int sp = c.split_bfly;
     if constexpr (JPB > 1) {
-        if (sp >= 3)
+        if (sp == 4)
+            k_fan2j<LOGR, NA, FAN, JPB, 1><<<grid, NA * R / 16, 0, c.stream>>>(fan, inv, fwd, c.primes, c.logN, njobs);
+        else if (sp == 3)
             k_fan2j<LOGR, NA, FAN, JPB, 3><<<grid, NA * R / 16, 0, c.stream>>>(fan, inv, fwd, c.primes, c.logN, njobs);
         else if (sp == 2)
             k_fan2j<LOGR, NA, FAN, JPB, 2><<<grid, NA * R / 16, 0, c.stream>>>(fan, inv, fwd, c.primes, c.logN, njobs);
