@@ -66,8 +66,9 @@ struct Ctx {
     // device [K][N] w 2^31 mod q for the SEAL-ordered tw / itw (integer primes; the split-input Shoup butterflies of
     // the fan-out kernels, hec_device.h shoup_split_lazy), 0 at FP64 primes
     u64 *tws = nullptr, *itws = nullptr;
-    int split_bfly = 1;            // HEC_SPLIT_BFLY: 0 plain Shoup in the fan-out kernels, 1 split-input Shoup in
-                                   // k_fan2, 2 also k_fan2j's per-thread-twiddle rounds, 3 all of k_fan2j (hec_kernels.hip)
+    int split_bfly = 4;            // HEC_SPLIT_BFLY: 0 plain Shoup in the fan-out kernels, 1 split-input Shoup in
+                                   // k_fan2, 2 also k_fan2j's per-thread-twiddle rounds, 3 all of k_fan2j, 4 k_fan2 and
+                                   // k_fan2j's scalar-twiddle round (hec_kernels.hip run_fan; profiles/r05s_*)
     // key-switch target primes I in [0, l] (I == l is P) per level l, integer-arithmetic primes first:
     // device table imap + l * (HEC_MAXL + 2), built once at context creation; imap_nint[l] of them integer
     int *imap = nullptr;
