@@ -1,7 +1,7 @@
 """rocprofv3 kernel-trace average of the roofline kernel over bench.py's profile step only (development
-tool).  bench.py times its steps with the batch split into concurrent lanes, then runs one extra step as a
-single lane with HIP event pairs (the roofline's avg_ms); that step's dispatches are the roofline kernel's
-last `launches_per_step` dispatches in the trace.
+tool).  bench.py times its steps (one lane by default since round 5; concurrent lanes with HEC_LANES=3), then runs
+one extra step as a single lane with HIP event pairs (the roofline's avg_ms), its last GPU work; that step's
+dispatches are the roofline kernel's last `launches_per_step` dispatches in the trace.
 usage: python tools/profile_step.py <run_kernel_trace.csv> <bench.json> <out.json>"""
 import csv
 import json
@@ -24,8 +24,8 @@ res = {"kernel": kern, "profile_step_dispatches": len(last),
        "profile_step_avg_us": round(sum(last) / len(last) / 1e3, 2),
        "event_timed_avg_us": round(roof["avg_ms"] * 1e3, 2),
        "all_dispatches": len(durs), "all_dispatch_avg_us": round(sum(d for _, d in durs) / len(durs) / 1e3, 2),
-       "note": "timed steps run the batch as concurrent lanes (smaller, overlapping launches); the profile "
-               "step runs one lane, as the event-timed roofline does"}
+       "note": "the profile step runs the batch as one lane, as the event-timed roofline does (the timed steps "
+               "too unless HEC_LANES > 1)"}
 # every kernel of the bench's per-kernel table over the same profile step (its last `launches` dispatches):
 # rocprof's own time shares for the single-lane step, to set beside the whole-run stats CSV, whose shares
 # are inflated for kernels that overlap each other in the concurrent lanes
