@@ -1405,6 +1405,7 @@ int hec_context_create(uint64_t N, const uint64_t *mod, uint64_t K, int device, 
         if (const char *f = std::getenv("HEC_DEBUG_LANES")) c.debug_lanes = f[0] != '0';
         if (const char *f = std::getenv("HEC_KERNEL_MEMOPS")) c.kernel_memops = f[0] != '0';
         if (const char *f = std::getenv("HEC_SPLIT_BFLY")) c.split_bfly = std::atoi(f);
+        if (const char *f = std::getenv("HEC_BMAC_SPLIT")) c.bmac_split = f[0] != '0';
         c.N = N;
         c.logN = __builtin_ctzll(N);
         c.K = K;
@@ -1475,6 +1476,14 @@ int hec_context_create(uint64_t N, const uint64_t *mod, uint64_t K, int device, 
         HEC_HIP(hipMalloc(&c.itwb, K * N * sizeof(ulonglong2)));
         HEC_HIP(hipMemcpy(c.twb, twb.data(), K * N * sizeof(ulonglong2), hipMemcpyHostToDevice));
         HEC_HIP(hipMemcpy(c.itwb, itwb.data(), K * N * sizeof(ulonglong2), hipMemcpyHostToDevice));
+        {   // pass-B layout of the split-input Shoup words (k_bmac's integer targets): a = w 2^31 mod q of twb
+            std::vector<u64> tba(K * N, 0);
+            for (uint64_t i = 0; i < K; ++i)
+                if (!c.hprimes[i].fp)
+                    for (uint64_t k = 0; k < N; ++k) tba[i * N + k] = (u64)(((u128)twb[i * N + k].x << 31) % c.q[i]);
+            HEC_HIP(hipMalloc(&c.twbs, K * N * sizeof(u64)));
+            HEC_HIP(hipMemcpy(c.twbs, tba.data(), K * N * sizeof(u64), hipMemcpyHostToDevice));
+        }
         {   // hoisted mod-up constants: psi powers per key prime, q_J mod q_I
             HEC_HIP(hipMalloc(&c.psipow, psipow.size() * sizeof(u64)));
             HEC_HIP(hipMemcpy(c.psipow, psipow.data(), psipow.size() * sizeof(u64), hipMemcpyHostToDevice));
@@ -1570,6 +1579,7 @@ int hec_context_destroy(hec_context *ctx)
         (void)hipFree(c.itwb);
         (void)hipFree(c.tws);
         (void)hipFree(c.itws);
+        (void)hipFree(c.twbs);
         for (double *p : {c.twf, c.itwf, c.twbf, c.itwbf}) (void)hipFree(p);
         (void)hipFree(c.enc_map);
         (void)hipFree(c.enc_tw);
@@ -1610,6 +1620,7 @@ int hec_context_set_option(hec_context *ctx, const char *name, int64_t value)
             else if (n == "debug_lanes") c.debug_lanes = value != 0;
             else if (n == "kernel_memops") c.kernel_memops = value != 0;
             else if (n == "split_bfly") c.split_bfly = (int)value;
+            else if (n == "bmac_split") c.bmac_split = value != 0;
             else if (n == "hoist") c.hoist = value != 0;
             else if (n == "hoist_min") c.hoist_min_children = (int)std::max<int64_t>(1, value);
             else if (n == "hmac") c.hmac_cfg = (int)value;

@@ -66,6 +66,8 @@ struct Ctx {
     // device [K][N] w 2^31 mod q for the SEAL-ordered tw / itw (integer primes; the split-input Shoup butterflies of
     // the fan-out kernels, hec_device.h shoup_split_lazy), 0 at FP64 primes
     u64 *tws = nullptr, *itws = nullptr;
+    u64 *twbs = nullptr;           // the same words for twb (pass-B layout; k_bmac's integer targets)
+    bool bmac_split = true;        // HEC_BMAC_SPLIT=0: k_bmac's integer-target pass B on plain Shoup butterflies
     int split_bfly = 4;            // HEC_SPLIT_BFLY: 0 plain Shoup in the fan-out kernels, 1 split-input Shoup in
                                    // k_fan2, 2 also k_fan2j's per-thread-twiddle rounds, 3 all of k_fan2j, 4 k_fan2 and
                                    // k_fan2j's scalar-twiddle round (hec_kernels.hip run_fan; profiles/r05s_*)

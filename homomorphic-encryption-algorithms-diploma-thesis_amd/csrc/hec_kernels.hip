@@ -260,6 +260,7 @@ struct TwTables {
     const ulonglong2 *a, *b;  // integer: pass A (SEAL order), pass B ([s][i][chunk])
     const double *fa, *fb;    // FP64 twins
     const u64 *sa = nullptr;  // w 2^31 mod q for a (the split-input Shoup butterflies, hec_device.h)
+    const u64 *sb = nullptr;  // the same for b
 };
 
 // One round: stages [S0, S1) of a P = 2^LOGP point sub-transform.  Thread `ts` of its segment owns
@@ -310,6 +311,7 @@ struct ConstTwS : ConstTw {
         return ((cword *)ta)[(1u << s) + (unsigned)i];
     }
 };
+struct LdsTwS;
 template <class T, class = void>
 struct HasSplitTw : std::false_type {};
 template <class T>
@@ -323,6 +325,11 @@ struct LdsTw {  // entry k = 2^s - 1 + i of this segment; FP: one word (double b
         const u64 *p = row + 2 * ((1 << s) - 1 + i);
         return ulonglong2{p[0], p[1]};
     }
+};
+struct LdsTwS : LdsTw {  // with the split-input Shoup words (entry k of arow)
+    static constexpr bool kSplit = true;
+    const u64 *arow;
+    __device__ u64 a(int s, int i) const { return arow[(1 << s) - 1 + i]; }
 };
 
 // The D = S1 - S0 stages of one element group (NQ = 2^D registers): group g of a round, hi = its index above
@@ -392,7 +399,7 @@ __device__ __forceinline__ void ntt_round_g(u64 *lds, const AddrF &addr, int ts,
         const int lo = g & ((1 << (LOGP - S1)) - 1);
         const int hi = g >> (LOGP - S1);
         const int xb = (hi << (LOGP - S0)) | lo;
-        GroupTw<S0, D, FP> gt;
+        GroupTw<S0, D, FP, !FP && HasSplitTw<TwG>::value> gt;
         gt.load(hi, twg);
         u64 v[NQ];
 #pragma unroll
@@ -2061,7 +2068,7 @@ __device__ __forceinline__ void ntt_round_x(u64 *row, int ts, const TwG &twg, co
         const int lo = g & ((1 << (LOGP - S1)) - 1);
         const int hi = g >> (LOGP - S1);
         const int xb = bswz<LOGP>((hi << (LOGP - S0)) | lo);
-        GroupTw<S0, D, FP> gt;
+        GroupTw<S0, D, FP, !FP && HasSplitTw<TwG>::value> gt;
         gt.load(hi, twg);
         u64 v[NQ];
         if constexpr (PAIRS) {
@@ -2084,8 +2091,10 @@ __device__ __forceinline__ void ntt_round_x(u64 *row, int ts, const TwG &twg, co
     }
 }
 
-template <int LOGP, int NSEG, int EPT, bool FP>
-__device__ __forceinline__ void bmac_body(u64 *lds, u64 *ltw, PolyArr T, const u64 *__restrict__ E, const u64 *__restrict__ key,
+// SPL (integer targets): the pass-B butterflies as split-input Shoup, their extra twiddle words staged in ltwa
+template <int LOGP, int NSEG, int EPT, bool FP, bool SPL = false>
+__device__ __forceinline__ void bmac_body(u64 *lds, u64 *ltw, u64 *ltwa, PolyArr T, const u64 *__restrict__ E,
+                                          const u64 *__restrict__ key,
                                           u64 *__restrict__ ACC, const TwTables &tt, const DevPrime &pr, int I, int kI,
                                           int b, int xb, int logN, int l, int K, u32 elt)
 {
@@ -2101,6 +2110,7 @@ __device__ __forceinline__ void bmac_body(u64 *lds, u64 *ltw, PolyArr T, const u
     const u64 base = (u64)seg0 << LOGP;
     const ulonglong2 *tw = tt.b + ((u64)kI << logN);
     const double *twf = tt.fb + ((u64)kI << logN);
+    const u64 *twa = SPL ? tt.sb + ((u64)kI << logN) : nullptr;
     const int ts = (int)threadIdx.x % (P / EPT), sg = (int)threadIdx.x / (P / EPT);
     auto addr = [sg](int x) { return sg * LD + x + (x >> 4); };
     const u64 R = 1ull << (logN - LOGP);
@@ -2116,9 +2126,11 @@ __device__ __forceinline__ void bmac_body(u64 *lds, u64 *ltw, PolyArr T, const u
             const ulonglong2 w = tw[gi];
             ltw[sl * TWS + 2 * k] = w.x;
             ltw[sl * TWS + 2 * k + 1] = w.y;
+            if constexpr (SPL) ltwa[sl * P + k] = twa[gi];
         }
     }
-    const LdsTw twg{ltw + sg * TWS};
+    const LdsTw twg0{ltw + sg * TWS};
+    const LdsTwS twgs{{ltw + sg * TWS}, ltwa + sg * P};
     const u64 g0 = ((u64)(seg0 + sg) << LOGP) + (u64)ts * EPT;  // first of this thread's outputs
     auto src = [&](int J) -> const u64 * {
         return J == I ? T.p + b * T.sb + (u64)J * N : E + (((u64)((b * (l + 1) + I) * l + J)) << logN);
@@ -2191,7 +2203,7 @@ __device__ __forceinline__ void bmac_body(u64 *lds, u64 *ltw, PolyArr T, const u
         if (J + 1 < l) load_tile(J + 1);
         __syncthreads();
         u64 v[EPT];
-        if (ntt) {
+        auto rounds = [&](const auto &twg) {
             static_assert(LOGP >= 5 && LOGP <= 8, "pass-B sizes 2^5 .. 2^8");
             static_assert(EPT == 4, "rounds of 2 stages");
             if constexpr (SWZ) {
@@ -2209,6 +2221,10 @@ __device__ __forceinline__ void bmac_body(u64 *lds, u64 *ltw, PolyArr T, const u
                 __syncthreads();
                 ntt_round_g<LOGP, 4, LOGP, EPT, false, FP, true>(lds, addr, ts, twg, pr, v);
             }
+        };
+        if (ntt) {
+            if constexpr (!FP && SPL) rounds(twgs);
+            else rounds(twg0);
         } else if constexpr (SWZ) {
             const int xb = bswz<LOGP>(ts * EPT);
 #pragma unroll
@@ -2252,14 +2268,15 @@ __device__ __forceinline__ void bmac_body(u64 *lds, u64 *ltw, PolyArr T, const u
 
 // one launch: Imap lists every target prime, the first nint integer ones (per-block branch; blocks of both
 // kinds overlap)
-template <int LOGP, int NSEG, int EPT>
-__global__ void __launch_bounds__(NSEG *(1 << LOGP) / EPT)
+template <int LOGP, int NSEG, int EPT, bool SPL>
+__global__ void __launch_bounds__(NSEG *(1 << LOGP) / EPT, 4)  // 4 waves per SIMD (<= 128 VGPRs), as without SPL
     k_bmac(PolyArr T, const u64 *__restrict__ E, const u64 *__restrict__ key, u64 *__restrict__ ACC, TwTables tt,
            const DevPrime *__restrict__ primes, const int *__restrict__ Imap, int nI, int logN, int l, int K,
            int nint, int gpad, u32 elt)
 {
     __shared__ __attribute__((aligned(16))) u64 lds[NSEG * bmac_ld(LOGP)];  // 16-B pair accesses
     __shared__ __attribute__((aligned(16))) u64 ltw[NSEG * (2 * (1 << LOGP) + 2)];  // rows of 2P + 2 words: 16-B pairs
+    __shared__ u64 ltwa[SPL ? NSEG * (1 << LOGP) : 1];  // SPL: the integer twiddles' split-input words
     // 1-D grid, XCD-aware: workgroup w runs on XCD w % 8.  The B blocks of one (chunk block, I) group
     // read the same key chunk, so they get ids G8*8*B + b*8 + (G % 8): one XCD, dispatched together,
     // and the key chunk is fetched into that XCD's L2 once instead of once per b.
@@ -2272,9 +2289,9 @@ __global__ void __launch_bounds__(NSEG *(1 << LOGP) / EPT)
     const int kI = I == l ? K - 1 : I;
     const DevPrime pr = primes[kI];
     if (yi < nint)
-        bmac_body<LOGP, NSEG, EPT, false>(lds, ltw, T, E, key, ACC, tt, pr, I, kI, b, xb, logN, l, K, elt);
+        bmac_body<LOGP, NSEG, EPT, false, SPL>(lds, ltw, ltwa, T, E, key, ACC, tt, pr, I, kI, b, xb, logN, l, K, elt);
     else
-        bmac_body<LOGP, NSEG, EPT, true>(lds, ltw, T, E, key, ACC, tt, pr, I, kI, b, xb, logN, l, K, elt);
+        bmac_body<LOGP, NSEG, EPT, true>(lds, ltw, ltwa, T, E, key, ACC, tt, pr, I, kI, b, xb, logN, l, K, elt);
 }
 
 // k_bmac: EPT = 4 elements per thread (rounds of 2 stages, 118 VGPRs, 4 waves/SIMD); 8 per thread (3-stage rounds,
@@ -2284,7 +2301,7 @@ static void run_modup_fused(Ctx &c, const u64 *D, u64 *E, PolyArr T, const u64 *
                             int part, u32 elt)
 {
     constexpr int R = 1 << LOGR, C = 1 << LOGC;
-    const TwTables fwd{c.tw, c.twb, c.twf, c.twbf};
+    const TwTables fwd{c.tw, c.twb, c.twf, c.twbf, c.tws, c.twbs};
     // (2a) pass A of every mod-up NTT (B * l * l jobs), output E[b][I][J] (lazy, pass-A domain)
     const int nint = c.imap_nint[l];
     const int *dm = c.imap_at(l);
@@ -2301,8 +2318,12 @@ static void run_modup_fused(Ctx &c, const u64 *D, u64 *E, PolyArr T, const u64 *
     constexpr int TB = NB2 * C / EPT;
     constexpr int X = R / NB2;
     const int gpad = (X * (l + 1) + 7) / 8 * 8;
-    k_bmac<LOGC, NB2, EPT><<<dim3(gpad * B), TB, 0, c.stream>>>(T, E, key, ACC, fwd, c.primes, dm, l + 1, c.logN, l,
-                                                                (int)c.K, nint, gpad, elt);
+    if (c.bmac_split)
+        k_bmac<LOGC, NB2, EPT, true><<<dim3(gpad * B), TB, 0, c.stream>>>(T, E, key, ACC, fwd, c.primes, dm, l + 1,
+                                                                          c.logN, l, (int)c.K, nint, gpad, elt);
+    else
+        k_bmac<LOGC, NB2, EPT, false><<<dim3(gpad * B), TB, 0, c.stream>>>(T, E, key, ACC, fwd, c.primes, dm, l + 1,
+                                                                           c.logN, l, (int)c.K, nint, gpad, elt);
     HEC_HIP(hipGetLastError());
 }
 

@@ -414,7 +414,7 @@ def test_cfg5_params_matvec_bitexact(orc, hecdna):
                                  {"HEC_HMAC": "0"}, {"HEC_HMAC": "0", "HEC_HOIST_MIN": "1"},
                                  {"HEC_HMAC": "1"}, {"HEC_HMAC": "1", "HEC_HMAC_ODD3": "0"},
                                  {"HEC_HOIST_SCAN": "0"}, {"HEC_KERNEL_MEMOPS": "0"}, {"HEC_SPLIT_BFLY": "0"},
-                                 {"HEC_SPLIT_BFLY": "1"}, {"HEC_SPLIT_BFLY": "3"}])
+                                 {"HEC_SPLIT_BFLY": "1"}, {"HEC_SPLIT_BFLY": "3"}, {"HEC_BMAC_SPLIT": "0"}])
 def test_keyswitch_variants_bitexact(orc, hecdna, env):
     """The engine's alternative key-switch schedules (separate mod-up pass B + MAC kernels; the fused
     kernel's key-load placements) give the same bits as the oracle."""
