@@ -830,18 +830,6 @@ void ks_modup(Ctx &c, const u64 *D, u64 *E, int B, int l, int stages)
     ModUpMap m{l, c.logN, (int)c.K - 1};
     ModUpIO_A a{m, D, E, c.primes};
     ModUpIO_B b{m, E};
-    if (stages == 2 && c.logN == 15 && c.modup_nb != 16) {  // HEC_MODUP_NB: pass-B chunks per block (A/B knob)
-        const TwTables fwd{c.tw, c.twb, c.twf, c.twbf};
-        const int nj = B * l * l;
-        switch (c.modup_nb) {
-        case 4: k_ntt<7, 4, false, false, true><<<dim3(256 / 4, nj), 4 * 128 / 16, 0, c.stream>>>(b, fwd, c.primes, c.logN); break;
-        case 8: k_ntt<7, 8, false, false, true><<<dim3(256 / 8, nj), 8 * 128 / 16, 0, c.stream>>>(b, fwd, c.primes, c.logN); break;
-        case 32: k_ntt<7, 32, false, false, true><<<dim3(256 / 32, nj), 32 * 128 / 16, 0, c.stream>>>(b, fwd, c.primes, c.logN); break;
-        default: throw std::invalid_argument("HEC_MODUP_NB: 4, 8, 16 or 32");
-        }
-        HEC_HIP(hipGetLastError());
-        return;
-    }
     ntt_dispatch<false>(c, B * l * l, a, b, stages);
 }
 
