@@ -67,7 +67,6 @@ struct Ctx {
     // the fan-out kernels, hec_device.h shoup_split_lazy), 0 at FP64 primes
     u64 *tws = nullptr, *itws = nullptr;
     u64 *twbs = nullptr;           // the same words for twb (pass-B layout; k_bmac's integer targets)
-    bool passb_w4 = false;         // HEC_PASSB_W4=1: the mod-up pass B capped at 128 VGPRs (4 waves/SIMD; A/B knob)
     bool bmac_split = true;        // HEC_BMAC_SPLIT=0: k_bmac's integer-target pass B on plain Shoup butterflies
     int split_bfly = 4;            // HEC_SPLIT_BFLY: 0 plain Shoup in the fan-out kernels, 1 split-input Shoup in
                                    // k_fan2, 2 also k_fan2j's per-thread-twiddle rounds, 3 all of k_fan2j, 4 k_fan2 and

@@ -750,8 +750,8 @@ __device__ __forceinline__ void ntt_pass_body_rd(u64 *lds, const Bound &bio, con
 
 // A per-block branch on the prime's arithmetic class.  RD: the register-direct pass (ntt_pass_body_rd); otherwise
 // every round through LDS (ntt_pass_body: the forward pass B, where register-direct measured slower)
-template <int LOGP, int NSEG, bool INV, bool PASS_A, bool FINAL, class IO, bool RD = false, int MINW = 1>
-__global__ void __launch_bounds__(NSEG *(1 << LOGP) / 16, MINW)
+template <int LOGP, int NSEG, bool INV, bool PASS_A, bool FINAL, class IO, bool RD = false>
+__global__ void __launch_bounds__(NSEG *(1 << LOGP) / 16)
     k_ntt(const IO io, TwTables tt, const DevPrime *__restrict__ primes, int logN)
 {
     static_assert(LOGP >= 5 && LOGP <= 8, "two rounds of 4 stages");
@@ -780,18 +780,7 @@ static void run_ntt2(Ctx &c, int njobs, const IO1 &first, const IO2 &second, int
                            // SQ counters: a third fewer LDS and VMEM instructions, no bank conflicts either way,
                            // but 2.2x the cycles waiting on load dependencies and 15 % more wave cycles)
         if (stages & 1) k_ntt<LOGR, NA, false, true, false, IO1, true><<<gA, TA, 0, c.stream>>>(first, fwd, c.primes, c.logN);
-        if (stages & 2) {
-            // HEC_PASSB_W4: the mod-up pass B (129 VGPRs, 3 waves/SIMD at N = 2^15) capped for a fourth wave (A/B knob)
-            if constexpr (std::is_same_v<IO2, ModUpIO_B>) {
-                if (c.passb_w4) {
-                    k_ntt<LOGC, NB, false, false, true, IO2, false, 4><<<gB, TB, 0, c.stream>>>(second, fwd, c.primes,
-                                                                                              c.logN);
-                    HEC_HIP(hipGetLastError());
-                    return;
-                }
-            }
-            k_ntt<LOGC, NB, false, false, true><<<gB, TB, 0, c.stream>>>(second, fwd, c.primes, c.logN);
-        }
+        if (stages & 2) k_ntt<LOGC, NB, false, false, true><<<gB, TB, 0, c.stream>>>(second, fwd, c.primes, c.logN);
     } else {
         if (stages & 1) k_ntt<LOGC, NB, true, false, false, IO1, true><<<gB, TB, 0, c.stream>>>(first, inv, c.primes, c.logN);
         if (stages & 2) k_ntt<LOGR, NA, true, true, true, IO2, true><<<gA, TA, 0, c.stream>>>(second, inv, c.primes, c.logN);
