@@ -460,25 +460,32 @@ def main():
     sharded_extra = None
     nsh = args.sharded_steps if args.sharded_steps is not None else (1 if world > 1 else 0)
     if not sharded and not ctpt and nsh > 0:
-        import hecdna.shard as shard
-        splan = shard.plan_diagonal_shards(N, args.n, world)
-        s0 = bench_seeds(0, False)["col"]
-        scols = cols if rank == 0 else [ctx.ciphertext().fill_uniform(2, L, scale, s0 + i)
-                                        for i in range(args.batch)]  # rank 0's batch on every rank
-        res = shard.sharded_matvec(ctx, diags, scols, rk, gk, rank, world, plan=splan)  # warmup
-        ctx.synchronize()
-        barrier()
-        t0 = time.perf_counter()
-        for _ in range(nsh):
-            res = shard.sharded_matvec(ctx, diags, scols, rk, gk, rank, world, plan=splan)
-        ctx.synchronize()
-        barrier()
-        sdt = max_over_ranks(time.perf_counter() - t0)
-        sharded_extra = {"value": round(args.batch * nsh / sdt, 6), "unit": "matvec/s", "steps": nsh,
-                         "ms_per_step": round(sdt / nsh * 1e3, 3), "scaling": "strong", "batch": args.batch,
-                         "key_switches_per_rank": [shard.trie_cost(N, p) for p in splan]}
-        if rank == 0:
-            sharded_extra["self_check"] = sharded_selfcheck(res, scols)
+        # the metric above is complete: an exception in this extra leg (raised on every rank, as the sharded path's
+        # status agreement makes its argument errors) is reported in the line instead of discarding the metric
+        try:
+            import hecdna.shard as shard
+            splan = shard.plan_diagonal_shards(N, args.n, world)
+            s0 = bench_seeds(0, False)["col"]
+            scols = cols if rank == 0 else [ctx.ciphertext().fill_uniform(2, L, scale, s0 + i)
+                                            for i in range(args.batch)]  # rank 0's batch on every rank
+            res = shard.sharded_matvec(ctx, diags, scols, rk, gk, rank, world, plan=splan)  # warmup
+            ctx.synchronize()
+            barrier()
+            t0 = time.perf_counter()
+            for _ in range(nsh):
+                res = shard.sharded_matvec(ctx, diags, scols, rk, gk, rank, world, plan=splan)
+            ctx.synchronize()
+            barrier()
+            sdt = max_over_ranks(time.perf_counter() - t0)
+            sharded_extra = {"value": round(args.batch * nsh / sdt, 6), "unit": "matvec/s", "steps": nsh,
+                             "ms_per_step": round(sdt / nsh * 1e3, 3), "scaling": "strong", "batch": args.batch,
+                             "key_switches_per_rank": [shard.trie_cost(N, p) for p in splan]}
+            if rank == 0:
+                sharded_extra["self_check"] = sharded_selfcheck(res, scols)
+        except Exception as e:  # noqa: BLE001 (reported, not swallowed: the line carries it)
+            import traceback
+            traceback.print_exc(file=sys.stderr)
+            sharded_extra = {"error": f"{type(e).__name__}: {e}"}
     if sharded and rank == 0 and last_sharded[0] is not None:
         sharded_extra = {"self_check": sharded_selfcheck(last_sharded[0], cols)}
 
