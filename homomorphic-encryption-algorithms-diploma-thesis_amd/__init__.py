@@ -156,6 +156,7 @@ def lib():
             "hec_ciphertext_save_seal": [vp, C.c_int, vp, C.c_uint64, u64p],
             "hec_kswitch_key_load_seal": [vp, vp, C.c_uint64, C.POINTER(vp), u64p],
             "hec_galois_keys_load_seal": [vp, vp, C.c_uint64, u64p],
+            "hec_galois_keys_load_seal_ex": [vp, vp, C.c_uint64, C.c_uint64, u64p],
         }
         for name, args in sig.items():
             fn = getattr(L, name)
@@ -170,6 +171,8 @@ def lib():
         L.hec_profile_classes.restype = C.c_uint64
         L.hec_seal_last_error.restype = C.c_char_p
         L.hec_seal_kswitch_keys_default_limit.restype = C.c_uint64
+        L.hec_galois_keys_load_seal_default_lists.argtypes = [vp]
+        L.hec_galois_keys_load_seal_default_lists.restype = C.c_uint64
         _lib = L
     return _lib
 
@@ -841,10 +844,14 @@ class GaloisKeys:
         _check(lib().hec_galois_keys_download(self.h, int(elt), _p(a)))
         return a
 
-    def load_seal(self, b: bytes):
-        """GaloisKeys::load(context, in, size): every key list of a SEAL-serialized GaloisKeys."""
+    def load_seal(self, b: bytes, max_lists=None):
+        """GaloisKeys::load(context, in, size): every key list of a SEAL-serialized GaloisKeys (at most max_lists
+        non-empty lists; None: the library's fixed default, hec_galois_keys_load_seal_default_lists)."""
         used = C.c_uint64()
-        _check(lib().hec_galois_keys_load_seal(self.h, C.c_char_p(b), len(b), C.byref(used)))
+        if max_lists is None:
+            _check(lib().hec_galois_keys_load_seal(self.h, C.c_char_p(b), len(b), C.byref(used)))
+        else:
+            _check(lib().hec_galois_keys_load_seal_ex(self.h, C.c_char_p(b), len(b), int(max_lists), C.byref(used)))
         return used.value
 
     def __del__(self):

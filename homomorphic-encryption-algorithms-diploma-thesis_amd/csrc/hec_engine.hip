@@ -24,10 +24,12 @@
 #include <mutex>
 #include <set>
 #include <thread>
+#include <tuple>
 
 #include "hec_internal.h"
 
 #include <dlfcn.h>
+#include <unistd.h>
 #include <rccl/rccl.h>
 #include "hecdna.h"
 
@@ -1020,11 +1022,22 @@ void free_lane(hec_context *l)
 
 // HEC_DEBUG_LANES: a checksum of every key's sign-mask NTTs W and key sums KW at this level, compared with the first one
 // seen (they are built once and must never change)
+// first-seen checksums of the per-key tables, keyed by (key set, Galois element, level, table) -- not by device
+// address, which a freed table hands on to another key set; a key set's entries leave with it
+// (debug_key_tables_forget from hec_galois_keys_destroy)
+static std::mutex g_dbg_mu;
+static std::map<std::tuple<const hec_galois_keys *, u32, int, int>, u64> g_dbg_first;
+
+static void debug_key_tables_forget(const hec_galois_keys *gk)
+{
+    std::lock_guard<std::mutex> lock(g_dbg_mu);
+    for (auto it = g_dbg_first.begin(); it != g_dbg_first.end();)
+        it = std::get<0>(it->first) == gk ? g_dbg_first.erase(it) : std::next(it);
+}
+
 void debug_key_tables(hec_context *ctx, const hec_galois_keys &gk, int l)
 {
-    static std::mutex mu;
-    static std::map<std::pair<const void *, int>, u64> first;
-    std::lock_guard<std::mutex> lock(mu);
+    std::lock_guard<std::mutex> lock(g_dbg_mu);
     Ctx &c = ctx->c;
     HEC_HIP(hipDeviceSynchronize());
     auto sum = [&](const u64 *d, std::size_t words) {
@@ -1038,11 +1051,13 @@ void debug_key_tables(hec_context *ctx, const hec_galois_keys &gk, int l)
     for (const auto &kv : gk.negw) {
         const u64 sw = sum(kv.second, c.K * c.N);
         auto it = gk.kw.find({kv.first, l});
-        const u64 sk = it == gk.kw.end() ? 0 : sum(it->second, (std::size_t)2 * (l + 1) * c.N);
-        for (auto [key, v] : {std::pair{std::pair{(const void *)kv.second, 0}, sw},
-                              std::pair{std::pair{(const void *)(it == gk.kw.end() ? nullptr : it->second), l}, sk}}) {
-            auto f = first.find(key);
-            if (f == first.end()) first[key] = v;
+        const bool has_kw = it != gk.kw.end();
+        const u64 sk = has_kw ? sum(it->second, (std::size_t)2 * (l + 1) * c.N) : 0;
+        for (auto [key, v] : {std::pair{std::tuple{&gk, (u32)kv.first, 0, 0}, sw},
+                              std::pair{std::tuple{&gk, (u32)kv.first, l, 1}, sk}}) {
+            if (std::get<3>(key) == 1 && !has_kw) continue;
+            auto f = g_dbg_first.find(key);
+            if (f == g_dbg_first.end()) g_dbg_first[key] = v;
             else if (f->second != v) ++changed;
             ++n;
         }
@@ -1612,6 +1627,13 @@ int hec_context_set_option(hec_context *ctx, const char *name, int64_t value)
         need(ctx && name, "null argument");
         set_device(ctx);
         const std::string n(name);
+        // the enumerated knobs take only their listed values (a typo in an A/B value must not pass as
+        // another schedule)
+        auto in = [&](int64_t lo, int64_t hi) {
+            if (value < lo || value > hi)
+                throw std::invalid_argument("option " + n + " takes " + std::to_string(lo) + ".." + std::to_string(hi));
+            return (int)value;
+        };
         auto apply = [&](Ctx &c) {
             if (n == "lanes") c.lanes = (int)std::max<int64_t>(1, value);
             else if (n == "lane_min_batch") c.lane_min_batch = (int)std::max<int64_t>(1, value);
@@ -1619,13 +1641,13 @@ int hec_context_set_option(hec_context *ctx, const char *name, int64_t value)
             else if (n == "lane_serial") c.lane_serial = value != 0;
             else if (n == "debug_lanes") c.debug_lanes = value != 0;
             else if (n == "kernel_memops") c.kernel_memops = value != 0;
-            else if (n == "split_bfly") c.split_bfly = (int)value;
+            else if (n == "split_bfly") c.split_bfly = in(0, 4);
             else if (n == "bmac_split") c.bmac_split = value != 0;
             else if (n == "hoist") c.hoist = value != 0;
             else if (n == "hoist_min") c.hoist_min_children = (int)std::max<int64_t>(1, value);
-            else if (n == "hmac") c.hmac_cfg = (int)value;
-            else if (n == "hmac_odd3") c.hmac_odd3 = (int)value;
-            else if (n == "hoist_scan") c.hoist_scan = (int)value;
+            else if (n == "hmac") c.hmac_cfg = in(0, 2);
+            else if (n == "hmac_odd3") c.hmac_odd3 = in(0, 1);
+            else if (n == "hoist_scan") c.hoist_scan = in(0, 1);
             else if (n == "fan") c.fan_out = value != 0;
             else if (n == "fuse_galois") c.fuse_galois = value != 0;
             else if (n == "fused_modup_mac") c.fused_modup_mac = value != 0;
@@ -2150,6 +2172,7 @@ int hec_galois_keys_destroy(hec_galois_keys *gk)
 {
     return guard([&] {
         if (!gk) return;
+        debug_key_tables_forget(gk);
         (void)hipStreamSynchronize(gk->ctx->c.stream);
         for (auto &kv : gk->keys) (void)hipFree(kv.second);
         for (auto &kv : gk->negw) (void)hipFree(kv.second);
@@ -2207,17 +2230,22 @@ int hec_ciphertext_save_seal(const hec_ciphertext *ct, int compr_mode, void *out
 
 // Decompressed-size limit of a KSwitchKeys object loaded into this context (the bytes come from a client socket,
 // server.cpp:110-122): `lists` key lists of L PublicKeys of u64[2][K][N], the object's N list-length words, and at
-// most 256 B of SEALHeader / parms_id / ciphertext metadata per PublicKey.  GaloisKeys are accepted with as many
-// non-empty lists as there are Galois elements (N: the odd residues mod 2N) and as fit in the device's free memory
-// at load time, the same bound whether the object is compressed (the inflate budget) or not (counted as the lists
-// are parsed).  SEAL's default set (create_galois_keys(), the reference's only form: matrix_operations.cpp:771,
-// 872,1064) holds 2 log2(N) - 1.
-static uint64_t galois_lists_that_fit(const Ctx &c)
+// most 256 B of SEALHeader / parms_id / ciphertext metadata per PublicKey.  The loader inflates the whole object into
+// host memory before parsing it, so the default number of non-empty GaloisKeys lists is a fixed cap that does not
+// depend on the device: four times SEAL's default set (create_galois_keys(), the reference's only form:
+// matrix_operations.cpp:771,872,1064, holds 2 log2(N) - 1 lists), at least 64, at most N, and no more than half of the
+// host's available physical memory can hold.  The same bound applies whether the object is compressed (the inflate
+// budget) or not (counted as the lists are parsed).  hec_galois_keys_load_seal_ex takes an explicit limit instead.
+static uint64_t galois_lists_default(const Ctx &c)
 {
-    std::size_t free_b = 0, total_b = 0;
-    HEC_HIP(hipMemGetInfo(&free_b, &total_b));
-    const uint64_t per = c.L * 2 * c.K * c.N * 8;
-    return std::max<uint64_t>(1, std::min<uint64_t>(c.N, free_b / per));
+    const uint64_t logn = (uint64_t)__builtin_ctzll(c.N);
+    uint64_t lists = std::min<uint64_t>(c.N, std::max<uint64_t>(64, 4 * (2 * logn - 1)));
+    const long pages = sysconf(_SC_AVPHYS_PAGES), psz = sysconf(_SC_PAGESIZE);
+    if (pages > 0 && psz > 0) {
+        const uint64_t per = c.L * (2 * c.K * c.N * 8 + 256);
+        lists = std::min<uint64_t>(lists, std::max<uint64_t>(1, (uint64_t)pages * (uint64_t)psz / 2 / per));
+    }
+    return lists;
 }
 static uint64_t seal_keys_max_bytes(const Ctx &c, uint64_t lists)
 {
@@ -2242,17 +2270,19 @@ int hec_kswitch_key_load_seal(hec_context *ctx, const void *bytes, uint64_t nbyt
     });
 }
 
-int hec_galois_keys_load_seal(hec_galois_keys *gk, const void *bytes, uint64_t nbytes, uint64_t *consumed)
+int hec_galois_keys_load_seal_ex(hec_galois_keys *gk, const void *bytes, uint64_t nbytes, uint64_t max_lists,
+                                 uint64_t *consumed)
 {
     return guard([&] {
         need(gk && bytes, "null argument");
+        need(gk->ctx, "null argument");
         set_device(gk->ctx);
         struct Visit {
             hec_galois_keys *gk;
             uint64_t max_lists, seen = 0;
             std::string err;
             int rc = HEC_OK;
-        } v{gk, galois_lists_that_fit(gk->ctx->c)};
+        } v{gk, max_lists ? std::min<uint64_t>(max_lists, gk->ctx->c.N) : galois_lists_default(gk->ctx->c)};
         // one pass over the object: GaloisKeys::get_index(elt) = (elt - 1) / 2, every non-empty list uploaded as it
         // is parsed
         auto cb = [](void *user, uint64_t index, const uint64_t *words, uint64_t nwords) -> int {
@@ -2280,6 +2310,16 @@ int hec_galois_keys_load_seal(hec_galois_keys *gk, const void *bytes, uint64_t n
         seal_rc(rc);
         if (consumed) *consumed = used;
     });
+}
+
+int hec_galois_keys_load_seal(hec_galois_keys *gk, const void *bytes, uint64_t nbytes, uint64_t *consumed)
+{
+    return hec_galois_keys_load_seal_ex(gk, bytes, nbytes, 0, consumed);
+}
+
+uint64_t hec_galois_keys_load_seal_default_lists(const hec_context *ctx)
+{
+    return ctx ? galois_lists_default(ctx->c) : 0;
 }
 
 int hec_negate_inplace(hec_context *ctx, hec_ciphertext *a)

@@ -225,15 +225,16 @@ def sharded_matvec(ctx, diags, cols, rk, gk, rank: int, world: int, plan=None, g
     N, n, p = ctx.N, len(diags), len(cols)
     plan = plan or plan_diagonal_shards(N, n, world)
     dev = torch.device("cuda", ctx.device)
-    accs, err = None, None
+    accs, err, scales = None, None, [0.0] * p
     try:
         accs = ctx.matmul_diag_col_partial_set(diags, plan[rank], cols, gk)
-    except hecdna.HecError as e:
-        err = e
+        scales = [a.info()[2] for a in accs]
+    except Exception as e:  # noqa: BLE001 -- any failure (a HecError, a bad handle or plan, ctypes) must reach
+        err = e             # the agreement step, or the other ranks wait in the exchange
+        scales = [0.0] * p
     import torch.distributed as dist
     on_dev = world > 1 and dist.get_backend(group) == "nccl"
-    err = agree(err, [a.info()[2] for a in accs] if accs else [0.0] * p, rank, world, group,
-                dev if on_dev else None)
+    err = agree(err, scales, rank, world, group, dev if on_dev else None)
     if err is not None:
         raise err
     size, level, scale = accs[0].info()

@@ -21,8 +21,9 @@
  *
  * Objects are device-resident on the context's GPU; every call is ordered on the context's HIP
  * stream (hec_context_set_stream), downloads synchronise.  One context per device, one host
- * thread per context (a matvec over >= 32 vectors runs as concurrent lanes on engine-owned threads and
- * streams, joined before it returns).  No torch types cross this boundary.
+ * thread per context.  A matvec runs its whole batch on the context's stream by default (one lane); the
+ * option "lanes" > 1 (HEC_LANES) splits a batch of >= 32 vectors into concurrent lanes on engine-owned threads
+ * and streams, joined before it returns (opt-in).  No torch types cross this boundary.
  */
 #ifndef HECDNA_H
 #define HECDNA_H
@@ -66,7 +67,8 @@ int hec_context_synchronize(hec_context *ctx);
  * "poison" (every workspace carve and fresh output buffer is filled with 0xFF bytes before use, so a read of
  * memory the call never wrote becomes a deterministic wrong result), "lane_serial" (batch lanes run one after
  * another) and "debug_lanes" (per-call zero-list and key-table reports on stderr).  Every schedule is
- * bit-identical.  Applies to the context and its batch lanes; HEC_EINVAL for an unknown name. */
+ * bit-identical.  Applies to the context and its batch lanes; HEC_EINVAL for an unknown name, and for a value
+ * outside an enumerated knob's range ("split_bfly" 0..4, "hmac" 0..2, "hmac_odd3" 0..1, "hoist_scan" 0..1). */
 int hec_context_set_option(hec_context *ctx, const char *name, int64_t value);
 uint64_t hec_context_poly_degree(const hec_context *ctx);
 uint64_t hec_context_key_moduli(const hec_context *ctx); /* K */
@@ -236,8 +238,9 @@ int hec_context_comm(const hec_context *ctx, int *rank, int *world);
 /* BatchedMatrix::matmul diag x col over the world (every rank calls it with the same arguments): rank r
  * computes the partial sums over its planned diagonals (hec_plan_diagonal_shards with the keys of gk): only those
  * diags[j] are read and checked, every other entry is never dereferenced and may be NULL or any handle.  The
- * ranks then agree on the argument checks (a one-int RCCL all-reduce, so an error on one rank is returned on all
- * ranks instead of leaving the others in the exchange; hec_shard_agree), run one all-reduce of the partials (RCCL,
+ * ranks then agree on the argument checks (hec_shard_agree's protocol: two all-reduces of p + 1 doubles, min and
+ * max, over the RCCL or the host communicator, so an error on one rank is returned on all ranks instead of leaving
+ * the others in the exchange), run one all-reduce of the partials (RCCL,
  * or the host communicator of hec_comm_init_ops; u64 sum, exact
  * for world <= 8 and 60-bit primes) + reduction mod q, and every rank relinearizes and rescales all p outputs:
  * out[i] is bit-identical to hec_matmul_diag_col on one GPU. */
@@ -255,8 +258,8 @@ int hec_matmul_diag_col_sharded(hec_context *ctx, const hec_ciphertext *const *d
  * loader hec_ciphertext_load_seal (Ciphertext::expand_seed); hec_seal_ciphertext_load, which has no moduli,
  * rejects them (HEC_EINVAL).  Decompressed objects are bounded, since the bytes come from a client socket
  * (server.cpp:110-122): 2 GiB per ciphertext; a key object (with every compressed member nested in it) by the
- * caller's max_bytes in the *_ex forms, by 16 GiB in the others, and by the size of the key lists the context
- * accepts in the device loaders.  A payload over its limit is HEC_EINVAL ("decompressed SEAL object exceeds the
+ * caller's max_bytes in the *_ex forms, by 16 GiB in the others, and by a fixed count of key lists in the device
+ * loaders (hec_galois_keys_load_seal_ex; it does not depend on the device's free memory).  A payload over its limit is HEC_EINVAL ("decompressed SEAL object exceeds the
  * size limit"); a payload must also hold the words it announces. */
 #define HEC_COMPR_NONE 0
 #define HEC_COMPR_ZLIB 1
@@ -322,6 +325,13 @@ int hec_ciphertext_save_seal(const hec_ciphertext *ct, int compr_mode, void *out
 int hec_kswitch_key_load_seal(hec_context *ctx, const void *bytes, uint64_t nbytes, hec_kswitch_key **out,
                               uint64_t *consumed);
 int hec_galois_keys_load_seal(hec_galois_keys *gk, const void *bytes, uint64_t nbytes, uint64_t *consumed);
+/* ... with at most max_lists non-empty key lists (0: the default, hec_galois_keys_load_seal_default_lists: four times
+ * SEAL's default set of 2 log2(N) - 1, at least 64, at most N, bounded by half the host's available memory; it does
+ * not depend on the device).  More lists, or a compressed object that inflates beyond them, is invalid_argument
+ * "decompressed SEAL object exceeds the size limit" (the object is inflated in host memory before it is parsed). */
+int hec_galois_keys_load_seal_ex(hec_galois_keys *gk, const void *bytes, uint64_t nbytes, uint64_t max_lists,
+                                 uint64_t *consumed);
+uint64_t hec_galois_keys_load_seal_default_lists(const hec_context *ctx);
 
 /* ---------------------------------------------------------------- primitives (cfg2) ------- */
 /* In-place batched negacyclic NTT over device data u64[npolys][nlimbs][N]; limb j uses prime

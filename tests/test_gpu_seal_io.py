@@ -134,9 +134,11 @@ def test_server_flow_on_seeded_client_ciphertext(env, hecdna, tmp_path):
 
 
 def test_galois_keys_load_more_than_64_lists_both_modes(orc, hecdna):
-    """the device GaloisKeys loader accepts as many non-empty lists as there are Galois elements and as fit
-    in device memory, the same bound for an uncompressed and a zlib-compressed object (it used to reject more than 64
-    lists only when compressed).  80 keys at N = 2^10, every one loaded and used."""
+    """the device GaloisKeys loader applies one bound to an uncompressed and a zlib-compressed object.
+    The default is a fixed list count that does not depend on the device (the object is inflated in host
+    memory, so a device-sized budget let a small payload from the socket allocate hundreds of GB): 4 (2 log2 N - 1)
+    = 76 lists at N = 2^10.  80 keys are rejected by the default in both modes (the compressed object larger than the
+    cap included), and loaded and used with an explicit limit (hec_galois_keys_load_seal_ex)."""
     N = 1 << 10
     m = orc.Oracle.create_coeff_modulus(N, [40, 30, 40])
     o = orc.Oracle(N, m)
@@ -147,12 +149,19 @@ def test_galois_keys_load_more_than_64_lists_both_modes(orc, hecdna):
     for elt in elts:
         lists[(elt - 1) // 2] = gk_h[elt]
     ctx = hecdna.Context(N, m)
+    assert hecdna.lib().hec_galois_keys_load_seal_default_lists(ctx.h) == 76
     rng = np.random.default_rng(63)
     a = orc.Ct(np.stack([np.stack([rng.integers(0, m[i], N, dtype=np.uint64) for i in range(2)]) for _ in range(2)]),
                2.0**30)
     for compr in (0, 1):
+        blob = sf.kswitch_keys(N, m, lists, compr=compr)
+        with pytest.raises(hecdna.HecError) as e:
+            hecdna.GaloisKeys(ctx).load_seal(blob)
+        assert "exceeds the size limit" in str(e.value), compr
+        with pytest.raises(hecdna.HecError):
+            hecdna.GaloisKeys(ctx).load_seal(blob, max_lists=79)
         gk = hecdna.GaloisKeys(ctx)
-        gk.load_seal(sf.kswitch_keys(N, m, lists, compr=compr))
+        gk.load_seal(blob, max_lists=80)
         assert all(gk.has(elt) for elt in elts)
         for step in (1, 37, 80):
             g = ctx.rotate_vector(ctx.ciphertext(a.data, a.scale), step, gk)
