@@ -54,11 +54,11 @@ def algorithmic_bytes_per_matvec(N, l, n, B, ks):
 
 def pmc_traffic(kernel, B, logn, level, n, variant="ctct"):
     """HBM bytes per launch of the roofline kernel from the committed rocprofv3 PMC passes
-    (profiles/r04_pmc_<kernel>_B<B>[_ctpt].json, else r03_ / r02_ / r01_; written by tools/pmc_summary.py: FETCH_SIZE and
+    (profiles/r06_pmc_<kernel>_B<B>[_ctpt].json, else the newest earlier round's; written by tools/pmc_summary.py: FETCH_SIZE and
     WRITE_SIZE in separate passes, gfx950 FETCH x2 correction for 16-B/lane reads) when they were taken on this
     configuration and matvec variant; else None."""
     sfx = "" if variant == "ctct" else f"_{variant}"
-    for tag in ("r05", "r04", "r03", "r02", "r01"):  # the newest round's pass for this kernel
+    for tag in ("r06", "r05", "r04", "r03", "r02", "r01"):  # the newest round's pass for this kernel
         path = os.path.join(ROOT, "profiles", f"{tag}_pmc_{kernel}_B{B}{sfx}.json")
         if os.path.exists(path):
             break
@@ -181,7 +181,7 @@ def run_cfg2(args, hec, world, rank, local, barrier, max_over_ranks):
     the cfg2-4 chain {60, 40 x 9, 60} (the primitives of math_operations.cpp:316-354's per-primitive
     timing).  One step = forward NTT of --batch polynomials x 10 limbs in place, their dyadic product with a second
     NTT-form batch, inverse NTT of the product.  value = limb-NTTs per second (forward + inverse); the roofline uses
-    SURVEY §8(d)'s 524,288 B (2 N 8) per limb and pass."""
+    SURVEY §8(d)'s 524,288 B (2 N 8) per limb-NTT (both passes together)."""
     N = 1 << 15
     moduli = hec.create_coeff_modulus(N, [60] + [40] * 9 + [60])
     nl, npolys = 10, args.batch
@@ -226,14 +226,21 @@ def run_cfg2(args, hec, world, rank, local, barrier, max_over_ranks):
         ctx.profile(0)
         ntt = [v for k, v in kernels.items() if k.startswith("k_ntt/")]
         ms = sum(v["ms"] for v in ntt)
-        nb = sum(v["bytes_per_launch"] * v["launches"] for v in ntt)
+        nb_pass = sum(v["bytes_per_launch"] * v["launches"] for v in ntt)
         nlaunch = sum(v["launches"] for v in ntt)
+        # SURVEY 8(d)'s unit: one limb-NTT = 2 N 8 = 524,288 B (the limb read once and written once, twiddles
+        # amortised), whatever the number of passes the kernel takes; a step runs 2 nl npolys limb-NTTs in nlaunch
+        # pass launches, so a launch is credited with its share of those bytes
+        nb = 2 * nl * npolys * 2 * N * 8
         gbs = nb / (ms * 1e-3) / 1e9
         roof = {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None, "kernel": "k_ntt", "avg_ms": round(ms / nlaunch, 4),
                 "algorithmic_bytes_per_launch": int(nb / nlaunch), "launches_per_step": nlaunch,
                 "us_per_limb_ntt": round(ms * 1e3 / (2 * nl * npolys), 4),
-                "note": "per pass: every limb read and written once (2 N 8 = 524,288 B per limb and pass)"}
+                "per_pass_GBps": round(nb_pass / (ms * 1e-3) / 1e9, 1),
+                "note": "SURVEY 8(d) unit: 524,288 B per limb-NTT (one read and one write of the limb); the transform "
+                        "takes two passes, each reading and writing every limb, so the kernels move twice these bytes "
+                        "(per_pass_GBps counts both passes' in + out)"}
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -260,6 +267,56 @@ def run_cfg2(args, hec, world, rank, local, barrier, max_over_ranks):
             "roofline": roof, "kernels_one_step": kernels, "cpu_baseline": cpu}))
 
 
+def any_failed_over(dist, failed, device):
+    """One all-reduce (MAX) of (rank + 1 if this rank failed else 0): the highest failing rank, or None."""
+    if dist is None:
+        return 0 if failed else None
+    import torch
+    t = torch.tensor([float(dist.get_rank() + 1) if failed else 0.0], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    v = int(t.item())
+    return v - 1 if v else None
+
+
+def sharded_extra_leg(prepare, run, selfcheck, barrier, max_over_ranks, any_failed, rank, nsh, batch):
+    """Control flow of the cfg4 sharded leg that follows the metric's timed steps at N > 1: every
+    collective is reached by every rank, whatever fails where.
+      prepare() -> state: per-rank setup (plan, the rank-0 batch on every rank); a failure on any rank is agreed by
+        any_failed(flag) (one all-reduce) and every rank skips the leg with the same error;
+      run(state) -> result: one sharded matvec (shard.sharded_matvec: its own argument agreement before the exchange,
+        so an argument error on one rank is raised on every rank); one warmup call, then nsh timed calls between
+        barriers, max over ranks;
+      selfcheck(result): rank 0 only, local (no collective).
+    The metric is complete before this leg runs: an exception here is reported in the line, not raised."""
+    try:
+        state, err = prepare(), None
+    except Exception as e:  # noqa: BLE001 (reported in the line)
+        state, err = None, e
+    bad = any_failed(err is not None)
+    if bad is not None:
+        return {"error": f"preparation failed on rank {bad}" + (f": {type(err).__name__}: {err}" if err else "")}
+    try:
+        res = run(state)  # warmup
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(nsh):
+            res = run(state)
+        barrier()
+        sdt = max_over_ranks(time.perf_counter() - t0)
+        out = {"value": round(batch * nsh / sdt, 6), "unit": "matvec/s", "steps": nsh,
+               "ms_per_step": round(sdt / nsh * 1e3, 3), "scaling": "strong", "batch": batch}
+    except Exception as e:  # noqa: BLE001 (raised on every rank by the agreement inside run)
+        import traceback
+        traceback.print_exc(file=sys.stderr)
+        return {"error": f"{type(e).__name__}: {e}"}
+    if rank == 0:
+        try:
+            out["self_check"] = selfcheck(res)
+        except Exception as e:  # noqa: BLE001
+            out["self_check"] = {"error": f"{type(e).__name__}: {e}", "bitexact": None}  # not run, not failed
+    return out
+
+
 def dry_run(args, world, rank):
     """--dry-run: the launcher, the process group, the max-over-ranks timing and the rank-0 line over gloo,
     with no GPU and no engine (tests/test_bench_measurement.py runs it at world size 2 on the CPU)."""
@@ -272,15 +329,59 @@ def dry_run(args, world, rank):
         if world > 1:
             dist.barrier()
     dt = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    def max_over_ranks(x):
+        if world == 1:
+            return x
+        t = torch.tensor([x], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+        return float(t.item())
+
+    dt = max_over_ranks(dt)
+    # the sharded extra leg's control flow over gloo with stand-in work: --dry-run-fail <where>:<rank> injects an
+    # exception on one rank in the preparation, in the sharded call before its agreement, or in rank 0's self-check
+    where, _, frank = (args.dry_run_fail or "none:-1").partition(":")
+    frank = int(frank)
+
+    def prepare():
+        if where == "prepare" and rank == frank:
+            raise RuntimeError("injected preparation failure")
+        return torch.arange(4, dtype=torch.int64)
+
+    def run_stub(state):
+        err = RuntimeError("injected failure before the agreement") if where == "run" and rank == frank else None
+        flag = torch.tensor([1.0 if err else 0.0], dtype=torch.float64)
+        if world > 1:  # shard.agree's all-reduce, then the exchange
+            dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+        if flag.item():
+            raise err or RuntimeError("the arguments failed the checks on another rank")
+        buf = state.clone()
+        if world > 1:
+            dist.all_reduce(buf)
+        return buf
+
+    def selfcheck(res):
+        if where == "selfcheck":
+            raise RuntimeError("injected self-check failure")
+        return {"outputs_checked": 1, "bitexact": bool(res[1].item() == world)}
+
+    sharded = None
+    if world > 1 or args.sharded_steps:
+        sharded = sharded_extra_leg(prepare, run_stub, selfcheck, barrier, max_over_ranks,
+                                    lambda f: any_failed_over(dist if world > 1 else None, f, torch.device("cpu")),
+                                    rank, args.sharded_steps or 1, 4)
+    ok = torch.tensor([0.0], dtype=torch.float64)  # the post-leg all_ranks_bitexact all-reduce
+    if world > 1:
+        dist.all_reduce(ok, op=dist.ReduceOp.MAX)
     if rank == 0:
         print(json.dumps({"metric": "CKKS matvec ciphertexts/sec (N=2^15, L=10)", "value": 0.0, "unit": "matvec/s",
                           "n_gpus": world, "rccl_world": dist.get_world_size() if world > 1 else 1,
                           "dist_backend": "gloo", "dry_run": True, "steps": args.steps, "warmup": args.warmup,
-                          "ms_per_step": round(dt / max(1, args.steps) * 1e3, 3)}))
+                          "ms_per_step": round(dt / max(1, args.steps) * 1e3, 3), "sharded": sharded}))
     if world > 1:
         dist.destroy_process_group()
 
@@ -290,11 +391,12 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--batch", type=int, default=192,
-                    help="input vectors per GPU per step (p), run as one batch on the context stream (round 4 sweep, "
-                         "profiles/r04i_*, r04j_*: 10.62 matvec/s at 192 vs 10.38 at 96 and 10.64 at 288; 384 does not "
-                         "fit the workspaces in 288 GB; HEC_LANES=3 splits it into 3 concurrent lanes, +1.3 %, "
-                         "profiles/r05b_lanes_ab.json)")
+    ap.add_argument("--batch", type=int, default=128,
+                    help="input vectors per GPU per step (p), run as one batch on the context stream.  Round 6 one-lane "
+                         "sweep on one box (profiles/r06a_batch_sweep.json): 10.47 / 10.53 / 10.59 / 10.70 matvec/s at "
+                         "96 / 128 / 144 / 192.  128 keeps the driver's --steps 20 --warmup 5 run well inside its "
+                         "600 s limit (192 took 542 s in BENCH_r05) for 1.6 %% of throughput; 384 does not fit the "
+                         "workspaces in 288 GB; HEC_LANES=3 splits it into 3 concurrent lanes (opt-in)")
     ap.add_argument("--n", type=int, default=4096, help="matrix dimension (diagonals)")
     ap.add_argument("--logn", type=int, default=15)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -319,8 +421,12 @@ def main():
     ap.add_argument("--no-self-check", action="store_true",
                     help="skip the self-check after the timed steps (PMC passes, which must count one step only)")
     ap.add_argument("--dry-run", action="store_true",
-                    help="exercise the launcher and the rank-0 line over gloo without touching a GPU (CPU tests)")
+                    help="exercise the launcher, the rank-0 line and the sharded extra leg's control flow over gloo "
+                         "without touching a GPU (CPU tests)")
+    ap.add_argument("--dry-run-fail", default=None,
+                    help="dry run only: inject an exception <prepare|run|selfcheck>:<rank> into the sharded leg")
     args = ap.parse_args()
+    wall0 = time.perf_counter()
     if args.config == "cfg5":
         args.logn, args.n = 16, 1024
         if args.batch == ap.get_default("batch"):
@@ -405,6 +511,7 @@ def main():
     ctx.synchronize()
 
     last_sharded = [None]
+    wall = {"setup_s": time.perf_counter() - wall0}
 
     def step():
         if sharded:
@@ -414,16 +521,50 @@ def main():
         else:
             ctx.matmul_diag_col(diags, cols, rk, gk, out=outs)
 
-    for _ in range(args.warmup):
+    # per-phase breakdown and per-kernel table: one untimed step with asynchronous HIP event pairs recorded on the
+    # context's stream around every launch (no host synchronisation inside the step).  With two or more warmup steps
+    # it is the LAST WARMUP step (warm workspaces, the same batch and inputs as the timed steps), so it costs no extra
+    # step; its outputs are kept and the timed steps' outputs must equal them (self_check.profile_step_bitexact).
+    # With fewer warmup steps it is an extra step after the timed ones.
+    breakdown = {}
+    classes = ("ks_intt", "ks_modup", "ks_mac", "ks_modup_a", "ks_bmac", "ks_modup_h", "ks_hmac", "ks_moddown",
+               "galois", "tensor", "relin", "rescale")
+    prof = {"classes": [], "ex": {}, "where": None}
+
+    def profile_step(where):
+        ctx.profile(2)
         step()
+        ctx.synchronize()
+        for cls in classes:
+            ms, cnt = ctx.profile_read(cls)
+            if cnt:
+                breakdown[cls] = {"ms": round(ms, 3), "launch_groups": cnt}
+        prof["classes"] = ctx.profile_classes()
+        prof["ex"] = {c: ctx.profile_read_ex(c) for c in prof["classes"]}
+        prof["where"] = where
+        ctx.profile(0)
+
+    keep = sorted({0, args.batch // 2, args.batch - 1})
+    prof_in_warmup = not args.no_profile and args.warmup >= 2 and not sharded
+    prof_saved = None
+    tw = time.perf_counter()
+    for w in range(args.warmup):
+        if prof_in_warmup and w == args.warmup - 1:
+            profile_step("last warmup step")
+            prof_saved = [(outs[i].download(), outs[i].info()) for i in keep]
+        else:
+            step()
     ctx.synchronize()
     barrier()
+    wall["warmup_s"] = time.perf_counter() - tw
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
     ctx.synchronize()
     barrier()
     dt = max_over_ranks(time.perf_counter() - t0)
+    wall["timed_s"] = dt
+    tc = time.perf_counter()
 
     # self-check of the timed outputs, after the timer: three outputs of the last timed step (the
     # first, middle and last vector of the batch), recomputed as ONE call with just those three vectors (another batch
@@ -431,13 +572,15 @@ def main():
     # on rank 0 at N = 1, the CPU leg's oracle matvec of input vector 0 on the same inputs are compared with them too
     check = None
     if not sharded and not args.no_self_check:
-        keep = sorted({0, args.batch // 2, args.batch - 1})
         saved = [(outs[i].download(), outs[i].info()) for i in keep]
         alone = (ctx.matmul_diagpt_col(diags, [cols[i] for i in keep], gk) if ctpt else
                  ctx.matmul_diag_col(diags, [cols[i] for i in keep], rk, gk))
         same = [bool(np.array_equal(a.download(), d) and a.info() == inf) for a, (d, inf) in zip(alone, saved)]
         del alone
         check = {"outputs_checked": keep, "single_call_bitexact": all(same)}
+        if prof_saved is not None:  # the profiled warmup step ran the same batch on the same inputs
+            check["profile_step_bitexact"] = all(np.array_equal(a, d) and ia == inf
+                                                 for (a, ia), (d, inf) in zip(prof_saved, saved))
 
     ms_per_step = dt / args.steps * 1e3
     total = args.batch * (1 if sharded else world) * args.steps
@@ -460,55 +603,40 @@ def main():
     sharded_extra = None
     nsh = args.sharded_steps if args.sharded_steps is not None else (1 if world > 1 else 0)
     if not sharded and not ctpt and nsh > 0:
-        # the metric above is complete: an exception in this extra leg (raised on every rank, as the sharded path's
-        # status agreement makes its argument errors) is reported in the line instead of discarding the metric
-        try:
-            import hecdna.shard as shard
+        import hecdna.shard as shard
+        splan_box = {}
+
+        def prepare():
             splan = shard.plan_diagonal_shards(N, args.n, world)
             s0 = bench_seeds(0, False)["col"]
             scols = cols if rank == 0 else [ctx.ciphertext().fill_uniform(2, L, scale, s0 + i)
                                             for i in range(args.batch)]  # rank 0's batch on every rank
-            res = shard.sharded_matvec(ctx, diags, scols, rk, gk, rank, world, plan=splan)  # warmup
+            splan_box["plan"] = splan
+            return splan, scols
+
+        def run(state):
+            splan, scols = state
+            res = shard.sharded_matvec(ctx, diags, scols, rk, gk, rank, world, plan=splan)
             ctx.synchronize()
-            barrier()
-            t0 = time.perf_counter()
-            for _ in range(nsh):
-                res = shard.sharded_matvec(ctx, diags, scols, rk, gk, rank, world, plan=splan)
-            ctx.synchronize()
-            barrier()
-            sdt = max_over_ranks(time.perf_counter() - t0)
-            sharded_extra = {"value": round(args.batch * nsh / sdt, 6), "unit": "matvec/s", "steps": nsh,
-                             "ms_per_step": round(sdt / nsh * 1e3, 3), "scaling": "strong", "batch": args.batch,
-                             "key_switches_per_rank": [shard.trie_cost(N, p) for p in splan]}
-            if rank == 0:
-                sharded_extra["self_check"] = sharded_selfcheck(res, scols)
-        except Exception as e:  # noqa: BLE001 (reported, not swallowed: the line carries it)
-            import traceback
-            traceback.print_exc(file=sys.stderr)
-            sharded_extra = {"error": f"{type(e).__name__}: {e}"}
+            return res, scols
+
+        sharded_extra = sharded_extra_leg(
+            prepare, run, lambda r: sharded_selfcheck(r[0], r[1]), barrier, max_over_ranks,
+            lambda f: any_failed_over(dist, f, torch.device("cuda", local)), rank, nsh, args.batch)
+        if "plan" in splan_box and "error" not in sharded_extra:
+            sharded_extra["key_switches_per_rank"] = [shard.trie_cost(N, p) for p in splan_box["plan"]]
     if sharded and rank == 0 and last_sharded[0] is not None:
         sharded_extra = {"self_check": sharded_selfcheck(last_sharded[0], cols)}
 
-    # per-phase breakdown: one extra (untimed) step with asynchronous HIP event pairs recorded on the
-    # context's stream around every phase (no host synchronisation inside the step)
-    breakdown = {}
-    classes = ("ks_intt", "ks_modup", "ks_mac", "ks_modup_a", "ks_bmac", "ks_modup_h", "ks_hmac", "ks_moddown",
-               "galois", "tensor", "relin", "rescale")
-    prof_classes, prof_ex = [], {}
-    if not args.no_profile:
-        ctx.profile(2)
-        step()
-        ctx.synchronize()
-        for cls in classes:
-            ms, cnt = ctx.profile_read(cls)
-            if cnt:
-                breakdown[cls] = {"ms": round(ms, 3), "launch_groups": cnt}
-        prof_classes = ctx.profile_classes()
-        prof_ex = {c: ctx.profile_read_ex(c) for c in prof_classes}
-        ctx.profile(0)
+    wall["self_check_and_sharded_s"] = time.perf_counter() - tc
+    if not args.no_profile and prof["where"] is None:
+        tp = time.perf_counter()
+        profile_step("extra step after the timed steps")
         if check is not None:  # the profile step reran the whole batch into the same outputs
             check["profile_step_bitexact"] = all(np.array_equal(outs[i].download(), d) and outs[i].info() == inf
                                                   for i, (d, inf) in zip(check["outputs_checked"], saved))
+        wall["profile_step_s"] = time.perf_counter() - tp
+    prof_classes, prof_ex = prof["classes"], prof["ex"]
 
     # per-kernel table and roofline.  Every kernel launch of the profile step sits in a "k:<kernel>/<role>"
     # scope that carries its algorithmic bytes (compulsory reads + writes of that kernel given the engine's
@@ -546,6 +674,7 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not ctpt:
+        tcpu = time.perf_counter()
         model, host_cpus, share, threads, why = cpu_info()
         # the GPU run's own inputs: every diagonal, input vector 0, the relinearization and Galois keys
         data = {"A": [d.download() for d in diags], "X": [cols[0].download()], "rk": rk.download(),
@@ -567,6 +696,7 @@ def main():
                "one_core": {"value": round(1.0 / res["one_core_s"], 6), "cores": 1, "extrapolated": True,
                             "sample": f"diagonals j<{args.cpu_sample_diags} ({res['ks_sample']} key switches) "
                                       f"on 1 thread, scaled to {ks} key switches"}}
+        wall["cpu_leg_s"] = time.perf_counter() - tcpu
 
     if check is not None:
         check["bitexact"] = all(v for k, v in check.items() if k.endswith("bitexact"))
@@ -602,10 +732,11 @@ def main():
             "whole_step_algorithmic_GBps": round(algo_mv * total / dt / 1e9, 2),
             "breakdown_ms_one_step": breakdown,
             "profile_schedule": (None if args.no_profile else
-                                 f"one extra untimed step after the timed ones, the batch of {args.batch} as one lane "
-                                 f"on the context stream (the default schedule; with HEC_LANES > 1 profiling turns the "
+                                 f"one untimed step ({prof['where']}), the batch of {args.batch} as one lane on the "
+                                 f"context stream (the default schedule; with HEC_LANES > 1 profiling turns the "
                                  f"concurrent lanes off so each launch has the GPU to itself); asynchronous HIP event "
                                  f"pairs per launch"),
+            "wall_s": {k: round(v, 2) for k, v in {**wall, "total_s": time.perf_counter() - wall0}.items()},
         }
         print(json.dumps(line))
     if dist is not None:
@@ -614,7 +745,7 @@ def main():
         print("bench.py: self-check: the timed outputs are NOT bit-exact (single call / profile step / oracle)",
               file=sys.stderr)
         sys.exit(1)
-    if sharded_extra is not None and "self_check" in sharded_extra and not sharded_extra["self_check"]["bitexact"]:
+    if sharded_extra is not None and (sharded_extra.get("self_check") or {}).get("bitexact") is False:
         # a sharded step whose outputs differ from the 1-rank matvec is no valid measurement: fail the run
         print("bench.py: sharded self-check is NOT bit-exact against the 1-rank matvec", file=sys.stderr)
         sys.exit(1)

@@ -97,3 +97,28 @@ def test_profile_step_tool(tmp_path):
     r = json.load(open(out))
     assert r["profile_step_dispatches"] == 2 and r["profile_step_avg_us"] == 10.0
     assert r["all_dispatches"] == 8 and r["event_timed_avg_us"] == 10.1
+
+
+@pytest.mark.parametrize("fail", [None, "prepare:1", "prepare:0", "run:1", "selfcheck:0"])
+def test_dry_run_sharded_leg_never_strands_a_rank(fail):
+    """the sharded extra leg after the metric (bench.sharded_extra_leg, the same control flow the
+    GPU run uses) reaches every collective on every rank whatever fails where: an exception on one rank in the
+    preparation, in the sharded call before its agreement, or in rank 0's self-check.  World 2 over gloo; the run must
+    end (timeout) with exactly one line, the metric intact and the failure reported in 'sharded'."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR",
+                                                             "MASTER_PORT")}
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run", "--steps", "1", "--warmup", "1"]
+    if fail:
+        cmd += ["--dry-run-fail", fail]
+    out = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=240, check=True)
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    sh = json.loads(lines[0])["sharded"]
+    if fail is None:
+        assert sh["value"] > 0 and sh["self_check"]["bitexact"] is True
+    elif fail.startswith("prepare"):
+        assert sh["error"].startswith("preparation failed on rank " + fail[-1])
+    elif fail.startswith("run"):
+        assert "error" in sh and "value" not in sh
+    else:
+        assert sh["value"] > 0 and "injected" in sh["self_check"]["error"] and sh["self_check"]["bitexact"] is None

@@ -5,14 +5,14 @@
 # gpurun_out/<tag>/pmc_<kernel>_B<batch>[_<variant>].json; profile_step.json = the rocprof average of the
 # roofline kernel over the profile step (tools/profile_step.py).
 # usage: [PMC_DIMS="<batch> <logN> <level> <n>"] [PMC_VARIANT=ctpt] bash tools/gpu_profile.sh <tag> [bench args...]
-#   cfg3 (default dims 192 15 10 4096, the bench batch):  bash tools/gpu_profile.sh r03_v1
+#   cfg3 (default dims 128 15 10 4096, the bench batch):  bash tools/gpu_profile.sh r03_v1
 #   ct x pt:  PMC_VARIANT=ctpt bash tools/gpu_profile.sh r03_ctpt --variant ctpt --no-cpu-baseline
 #   cfg5:     PMC_DIMS="32 16 16 1024" bash tools/gpu_profile.sh r03_cfg5 --config cfg5 --no-cpu-baseline
 set -o pipefail
 TAG=${1:-r03}
 shift
 ARGS="$*"
-DIMS=${PMC_DIMS:-"192 15 10 4096"}
+DIMS=${PMC_DIMS:-"128 15 10 4096"}
 export PMC_VARIANT=${PMC_VARIANT:-ctct}
 OUT=$GRAFT_REPO_ROOT/gpurun_out/$TAG
 mkdir -p $OUT
