@@ -564,6 +564,18 @@ def main():
     barrier()
     dt = max_over_ranks(time.perf_counter() - t0)
     wall["timed_s"] = dt
+    hbm = {"total_GB": None, "in_use_after_timed_GB": None, "in_use_max_GB": None}
+
+    def hbm_probe(key):
+        """Device-wide HBM in use (hipMemGetInfo: the engine's own allocations and torch's alike), the max over
+        ranks: the 8-GPU run's per-rank footprint is the replicated matrix and keys plus one batch's workspace."""
+        free, tot = torch.cuda.mem_get_info(local)
+        used = max_over_ranks((tot - free) / 1e9)
+        hbm["total_GB"] = round(tot / 1e9, 1)
+        hbm[key] = round(used, 2)
+        hbm["in_use_max_GB"] = max(hbm["in_use_max_GB"] or 0.0, round(used, 2))
+
+    hbm_probe("in_use_after_timed_GB")
     tc = time.perf_counter()
 
     # self-check of the timed outputs (VERDICT r04 item 2), after the timer: three outputs of the last timed step (the
@@ -629,6 +641,7 @@ def main():
         sharded_extra = {"self_check": sharded_selfcheck(last_sharded[0], cols)}
 
     wall["self_check_and_sharded_s"] = time.perf_counter() - tc
+    hbm_probe("in_use_after_checks_GB")
     if not args.no_profile and prof["where"] is None:
         tp = time.perf_counter()
         profile_step("extra step after the timed steps")
@@ -730,6 +743,7 @@ def main():
             "kernels_one_step": kernels,
             "cpu_baseline": cpu,
             "whole_step_algorithmic_GBps": round(algo_mv * total / dt / 1e9, 2),
+            "hbm": hbm,
             "breakdown_ms_one_step": breakdown,
             "profile_schedule": (None if args.no_profile else
                                  f"one untimed step ({prof['where']}), the batch of {args.batch} as one lane on the "

@@ -192,10 +192,10 @@ __device__ __forceinline__ void gs_bfly_fp(double &X, double &Y, double w, doubl
 // exact u64 <-> double for 0 <= x < 2^52 through the 2^52 magic number
 __device__ __forceinline__ double u2d(u64 x) { return __longlong_as_double((long long)(x | 0x4330000000000000ull)) - 4503599627370496.0; }
 __device__ __forceinline__ u64 d2u(double x) { return (u64)__double_as_longlong(x + 4503599627370496.0) - 0x4330000000000000ull; }
-// integer-valued double with |x| < 2^52 -> canonical residue as u64
-__device__ __forceinline__ u64 fp_canon(double x, double q, double qinv)
+// integer-valued double with |x| < 2^52 -> canonical residue, as a double and as u64
+__device__ __forceinline__ double fp_canon_d(double x, double q, double qinv)
 {
-    double r = fp_reduce(x, q, qinv);
-    r = r < 0 ? r + q : r;
-    return d2u(r);
+    const double r = fp_reduce(x, q, qinv);
+    return r < 0 ? r + q : r;
 }
+__device__ __forceinline__ u64 fp_canon(double x, double q, double qinv) { return d2u(fp_canon_d(x, q, qinv)); }

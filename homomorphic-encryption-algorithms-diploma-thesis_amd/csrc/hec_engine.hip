@@ -85,8 +85,13 @@ struct hec_galois_keys {
     // hoisted MAC: KW[elt, l][k][I] = sum_{J<l, J!=I} (q_J mod q_I) key_elt[J][k][I] mod q_I, built on first
     // use per level, dropped when the key is replaced
     std::map<std::pair<u32, int>, u64 *> kw;
-    void drop_kw(u32 elt)
+    std::map<u32, u64 *> mkey;  // hoisted MAC: the key in MAC form and source order (mac_key_table), first use
+    void drop_kw(u32 elt)  // the tables derived from the key's words (KW at every level, MK)
     {
+        if (auto m = mkey.find(elt); m != mkey.end()) {
+            (void)hipFree(m->second);
+            mkey.erase(m);
+        }
         for (auto it = kw.begin(); it != kw.end();) {
             if (it->first.first == elt) {
                 (void)hipFree(it->second);
@@ -507,7 +512,7 @@ void hoist_node(Ctx &c, PolyArr X, int B, int l, const Hoist &h)
             fan_modup(c, h.D, h.E, B, l, false, h.zl);
         }
         ProfScope k(c, "k:k_ntt/modup_h_b", 2.0 * B * l * l);
-        ks_modup(c, h.D, h.E, B, l, 2);  // pass B, canonical NTT-form digits
+        ks_modup(c, h.D, h.E, B, l, 2, c.hmac_cfg != 0);  // pass B: NTT-form digits (k_hmacm: MAC form)
         return;
     }
     {
@@ -529,7 +534,7 @@ void hoist_node(Ctx &c, PolyArr X, int B, int l, const Hoist &h)
         fan_modup(c, h.D, h.E, B, l, true);  // pass A of every NTT_I(D_J mod q_I), from the canonical D
     }
     ProfScope k(c, "k:k_ntt/modup_h_b", 2.0 * B * l * l);
-    ks_modup(c, h.D, h.E, B, l, 2);      // pass B, canonical NTT-form digits
+    ks_modup(c, h.D, h.E, B, l, 2, c.hmac_cfg != 0);  // pass B: NTT-form digits (k_hmacm: MAC form)
 }
 // one child of a hoisted node: OUT = key switch of apply_galois(X, elt) (X: the node's ciphertexts)
 void hoisted_child(Ctx &c, Scratch &s, PolyArr X, const Hoist &h, const u64 *W, const u64 *key, PolyArr OUT, int B,
@@ -582,6 +587,18 @@ const u64 *galois_kw(hec_context *ctx, hec_galois_keys &gk, u32 elt, int l)
     key_wsum(c, gk.keys.at(elt), KW, l);
     gk.kw[{elt, l}] = KW;
     return KW;
+}
+
+// the MAC-form key table of a Galois key (built on first use, see mac_key_table)
+const u64 *galois_mkey(hec_context *ctx, hec_galois_keys &gk, u32 elt)
+{
+    auto it = gk.mkey.find(elt);
+    if (it != gk.mkey.end()) return it->second;
+    Ctx &c = ctx->c;
+    u64 *MK = dalloc((std::size_t)c.L * 2 * c.K * c.N);
+    mac_key_table(c, gk.keys.at(elt), MK, (u32)invm(elt, 2 * c.N));
+    gk.mkey[elt] = MK;
+    return MK;
 }
 
 // X (size 2) -> OUT = apply_galois(X, elt) followed by key switching (SEAL apply_galois_inplace).
@@ -758,7 +775,7 @@ void walk_trie_hoisted(Ctx &c, Scratch &s, const RotTrie &t, int node, PolyArr s
         for (int q = 0; q < ng; ++q) {
             const u32 e = t.nodes[ch[g0 + q]].elt;
             kids[q] = HChildSpec{e, (u32)invm(e, 2 * N), gk.keys.at(e), galois_negw(ctx, gk, e), h.acc(q),
-                                 galois_kw(ctx, gk, e, l)};
+                                 galois_kw(ctx, gk, e, l), fold ? galois_mkey(ctx, gk, e) : nullptr};
         }
         const double K = l + 1;  // per child: key (2 l K), W (K), KW (2 K), ACC (2 B K)
         for (int q0 = 0, nk = 0; q0 < ng; q0 += nk) {  // one profile scope per launch (bench.py's roofline)
@@ -927,6 +944,7 @@ void matvec_core(hec_context *ctx, const hec_ciphertext *const *diags, const hec
         for (std::size_t nd = 1; nd < trie.nodes.size(); ++nd) {
             galois_negw(ctx, gkm, trie.nodes[nd].elt);
             galois_kw(ctx, gkm, trie.nodes[nd].elt, (int)l);
+            if (c.hmac_cfg != 0) galois_mkey(ctx, gkm, trie.nodes[nd].elt);
         }
         std::vector<Hoist> hs(D);
         for (int d = 0; d < D; ++d) hs[d] = hoist_alloc(c, s, (int)p, (int)l);
@@ -1088,6 +1106,7 @@ void matvec_lanes(hec_context *ctx, const hec_ciphertext *const *diags, const he
         for (auto &kv : gkm.keys) {
             galois_negw(ctx, gkm, kv.first);
             galois_kw(ctx, gkm, kv.first, (int)cols[0]->level);
+            if (c.hmac_cfg != 0) galois_mkey(ctx, gkm, kv.first);
         }
     }
     // the outputs are sized here, on the calling thread, so no lane thread frees or allocates them (matvec_core's
@@ -1420,6 +1439,7 @@ int hec_context_create(uint64_t N, const uint64_t *mod, uint64_t K, int device, 
         if (const char *f = std::getenv("HEC_DEBUG_LANES")) c.debug_lanes = f[0] != '0';
         if (const char *f = std::getenv("HEC_KERNEL_MEMOPS")) c.kernel_memops = f[0] != '0';
         if (const char *f = std::getenv("HEC_SPLIT_BFLY")) c.split_bfly = std::atoi(f);
+        if (const char *f = std::getenv("HEC_NTTB_SHFL")) c.nttb_shfl = std::min(2, std::max(0, std::atoi(f)));
         if (const char *f = std::getenv("HEC_BMAC_SPLIT")) c.bmac_split = f[0] != '0';
         c.N = N;
         c.logN = __builtin_ctzll(N);
@@ -1642,6 +1662,7 @@ int hec_context_set_option(hec_context *ctx, const char *name, int64_t value)
             else if (n == "debug_lanes") c.debug_lanes = value != 0;
             else if (n == "kernel_memops") c.kernel_memops = value != 0;
             else if (n == "split_bfly") c.split_bfly = in(0, 4);
+            else if (n == "nttb_shfl") c.nttb_shfl = in(0, 2);
             else if (n == "bmac_split") c.bmac_split = value != 0;
             else if (n == "hoist") c.hoist = value != 0;
             else if (n == "hoist_min") c.hoist_min_children = (int)std::max<int64_t>(1, value);
@@ -2177,6 +2198,7 @@ int hec_galois_keys_destroy(hec_galois_keys *gk)
         for (auto &kv : gk->keys) (void)hipFree(kv.second);
         for (auto &kv : gk->negw) (void)hipFree(kv.second);
         for (auto &kv : gk->kw) (void)hipFree(kv.second);
+        for (auto &kv : gk->mkey) (void)hipFree(kv.second);
         delete gk;
     });
 }

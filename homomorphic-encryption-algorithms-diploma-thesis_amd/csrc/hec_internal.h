@@ -68,6 +68,8 @@ struct Ctx {
     u64 *tws = nullptr, *itws = nullptr;
     u64 *twbs = nullptr;           // the same words for twb (pass-B layout; k_bmac's integer targets)
     bool bmac_split = true;        // HEC_BMAC_SPLIT=0: k_bmac's integer-target pass B on plain Shoup butterflies
+    int nttb_shfl = 0;             // HEC_NTTB_SHFL=1: the forward NTT's pass B at N = 2^15 as k_nttb_shfl (exchanges
+                                   // between lanes of a wavefront, no LDS tile), round 6
     int split_bfly = 4;            // HEC_SPLIT_BFLY: 0 plain Shoup in the fan-out kernels, 1 split-input Shoup in
                                    // k_fan2, 2 also k_fan2j's per-thread-twiddle rounds, 3 all of k_fan2j, 4 k_fan2 and
                                    // k_fan2j's scalar-twiddle round (hec_kernels.hip run_fan; profiles/r05s_*)
@@ -146,7 +148,8 @@ struct Ctx {
 void ntt_strided(Ctx &c, bool inverse, const u64 *src, u64 ps_src, u64 *dst, u64 ps_dst, int nl, const int *pmap,
                  int njobs, u32 elt = 1, int stages = 3);
 // Key-switch phases (B targets at level l; see hec_engine.hip for the dataflow)
-void ks_modup(Ctx &c, const u64 *D, u64 *E, int B, int l, int stages = 3);  // stages as ntt_strided
+void ks_modup(Ctx &c, const u64 *D, u64 *E, int B, int l, int stages = 3,
+              bool mform = false);  // stages as ntt_strided; mform: E in the MAC form k_hmacm reads
 void ks_mac(Ctx &c, PolyArr T, const u64 *E, const u64 *key, u64 *ACC, int B, int l, u32 elt);
 // fused: pass A of the mod-up NTTs (part & 1), then (pass B + key MAC) per target prime -> ACC[b][k][I]
 // (part & 2)
@@ -185,7 +188,11 @@ struct HChildSpec {
     const u64 *key, *W;
     u64 *ACC;
     const u64 *KW;  // key_wsum of the child's key at this level
+    const u64 *MK;  // the child's key in MAC form and source order (mac_key_table)
 };
+// MK[J][k][I][s] = the key word at the child's output position galois_src(s, einv), FP64-class limbs as double bits,
+// 60-bit limbs as lo30 | hi30 << 32 (hec_kernels.hip, the MAC form of k_hmacm)
+void mac_key_table(Ctx &c, const u64 *key, u64 *MK, u32 einv);
 constexpr int HMAC_MAX_CHILDREN = 6;  // largest hoisted_group()
 // KW[k][I] = sum_{J<l, J!=I} (q_J mod q_I) key[J][k][I] mod q_I, I in [0, l] (I == l: P), k in {0, 1}
 void key_wsum(Ctx &c, const u64 *key, u64 *KW, int l);

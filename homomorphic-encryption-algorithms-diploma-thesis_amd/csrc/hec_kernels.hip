@@ -122,11 +122,14 @@ struct ModUpIO_A {  // load digit J (coefficient form, canonical mod q_J) reduce
 struct ModUpIO_B {
     ModUpMap m;
     u64 *E;
+    int mform = 0;  // 1: the final store writes the MAC form k_hmacm reads (mform(), round 6)
     struct Bound {
         u64 *p;
         int prime;
         bool valid = true;
+        bool mform = false;
         static constexpr bool kPair = true;
+        static constexpr bool kMForm = true;
         struct Pre {};
         __device__ Pre pre(u64) const { return {}; }
         __device__ u64 load(u64 g) const { return p[g]; }
@@ -139,7 +142,7 @@ struct ModUpIO_B {
     {
         int b, I, J;
         m.map(job, b, I, J);
-        return Bound{E + m.eoff(b, I, J), I == m.l ? m.kP : I, I != J};
+        return Bound{E + m.eoff(b, I, J), I == m.l ? m.kP : I, I != J, mform != 0};
     }
 };
 
@@ -189,6 +192,11 @@ template <class T, class = void>
 struct HasLatePre : std::false_type {};
 template <class T>
 struct HasLatePre<T, std::void_t<decltype(T::kLatePre)>> : std::bool_constant<T::kLatePre> {};
+// Bound types whose final store may write the MAC form (a run-time flag `mform`, HasMForm)
+template <class T, class = void>
+struct HasMForm : std::false_type {};
+template <class T>
+struct HasMForm<T, std::void_t<decltype(T::kMForm)>> : std::bool_constant<T::kMForm> {};
 // Bound types with a store_fp(g, double, Pre, prime) post-op for FP64 primes (HasFpStore)
 template <class T, class = void>
 struct HasFpStore : std::false_type {};
@@ -464,14 +472,27 @@ __device__ __forceinline__ void ntt_pass_body(u64 *lds, const Bound &bio, const 
     constexpr bool PAIR = !PASS_A && HasPair<Bound>::value;
     constexpr int PB2 = P / 2;
     if constexpr (!PAIR) {
+        // every tile load issued before the first LDS store (round 6, VERDICT r05 item 5: with a load and its LDS
+        // store per iteration the compiler waited for each load in turn whenever the IO's load has a branch, as
+        // StridedIO's Galois permutation does: the plain forward pass B at cfg2 ran 0.0757-0.0794 instead of
+        // 0.064 ms per launch, the round-4 code's rate, on one box)
+        constexpr int NIT = P * NSEG / THREADS;
+        u64 tv[NIT];
 #pragma unroll
-        for (int it = 0; it < P * NSEG / THREADS; ++it) {
+        for (int it = 0; it < NIT; ++it) {
+            const int li = threadIdx.x + it * THREADS;
+            u64 g;
+            if constexpr (PASS_A) g = ((u64)(li / NSEG) << lc) + seg0 + li % NSEG;
+            else g = ((u64)(seg0 + li / P) << LOGP) + li % P;
+            tv[it] = bio.load(g);
+        }
+#pragma unroll
+        for (int it = 0; it < NIT; ++it) {
             const int li = threadIdx.x + it * THREADS;
             int x, sg;
-            u64 g;
-            if constexpr (PASS_A) { x = li / NSEG; sg = li % NSEG; g = ((u64)x << lc) + seg0 + sg; }
-            else { sg = li / P; x = li % P; g = ((u64)(seg0 + sg) << LOGP) + x; }
-            u64 v = bio.load(g);
+            if constexpr (PASS_A) { x = li / NSEG; sg = li % NSEG; }
+            else { sg = li / P; x = li % P; }
+            u64 v = tv[it];
             if constexpr (FP && FIRST) v = (u64)__double_as_longlong(u2d(v));  // integer input -> double bits
             lds[PASS_A ? x * LD + sg : sg * LD + x] = v;
         }
@@ -558,6 +579,14 @@ __device__ __forceinline__ void ntt_pass_body(u64 *lds, const Bound &bio, const 
                     if constexpr (INV) {
                         da = fp_mulmod(da, pr.ninv_d, pr.qd, pr.qinv);
                         db = fp_mulmod(db, pr.ninv_d, pr.qd, pr.qinv);
+                    }
+                    if constexpr (HasMForm<Bound>::value) {
+                        if (bio.mform) {  // MAC form: the canonical integer-valued double itself
+                            a = (u64)__double_as_longlong(fp_canon_d(da, pr.qd, pr.qinv));
+                            b = (u64)__double_as_longlong(fp_canon_d(db, pr.qd, pr.qinv));
+                            bio.store2(g, a, b, pre[2 * it], pre[2 * it + 1]);
+                            continue;
+                        }
                     }
                     a = fp_canon(da, pr.qd, pr.qinv);
                     b = fp_canon(db, pr.qd, pr.qinv);
@@ -748,6 +777,167 @@ __device__ __forceinline__ void ntt_pass_body_rd(u64 *lds, const Bound &bio, con
     }
 }
 
+// ------------------------------------------------------------------ wave-shuffle forward pass B (round 6)
+// The forward NTT's pass B at P = 128 (N = 2^15: stages 8..14, contiguous chunks of 128 words) with every exchange
+// inside the wavefront (the north-star's "wavefront shuffles"): a chunk's 8 lanes hold 16 elements each, and the three
+// stages whose butterfly distance is a lane bit are brought into registers by three exchange steps between partner
+// lanes (DPP moves of the 32-bit halves), not through an LDS tile: no LDS, no workgroup barrier, every wave runs on
+// its own.  Element x of the chunk (bits 0..6):
+//   loaded:   lane L (0..7) holds x = 16 j + 2 L + h in v[2 j + h]   (16-B word pairs: coalesced 128-B runs)
+//   stages 0..2 (distance bits 6, 5, 4 = register bits 3, 2, 1): in registers, two groups of 8 (h = 0, 1)
+//   3 swaps (register bit 3 <-> lane bit 2, bit 2 <-> lane bit 1, bit 1 <-> lane bit 0): lane L' then holds
+//             x = 16 L' + r in v[r]
+//   stages 3..6 (distance bits 3..0 = register bits 3..0): in registers, one group of 16 (GroupTw<3, 4>)
+//   stored:   16 consecutive words per lane (8 x 16-B pairs)
+// A swap step trades 8 of a lane's 16 words with its partner lane: 16 dword DPP moves (xor 1 and 2: quad_perm;
+// xor 4: row_shl:4 and row_shr:4 and a select by the lane bit) and selects on fixed register indices, no LDS access.
+template <int M>
+__device__ __forceinline__ u32 xor_lane32(u32 v)
+{
+    static_assert(M == 1 || M == 2 || M == 4, "partner lanes within 8");
+    if constexpr (M == 1) return (u32)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+    else if constexpr (M == 2) return (u32)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);  // [2,3,0,1]
+    else {
+        const u32 hi = (u32)__builtin_amdgcn_mov_dpp((int)v, 0x104, 0xF, 0xF, false);  // row_shl:4: lane i <- i + 4
+        const u32 lo = (u32)__builtin_amdgcn_mov_dpp((int)v, 0x114, 0xF, 0xF, false);  // row_shr:4: lane i <- i - 4
+        return (threadIdx.x & 4) ? lo : hi;
+    }
+}
+template <int M>
+__device__ __forceinline__ u64 xor_lane64(u64 v)
+{
+    return (u64)xor_lane32<M>((u32)v) | ((u64)xor_lane32<M>((u32)(v >> 32)) << 32);
+}
+// swap register bit RB with lane bit LB (lane = threadIdx.x & 7 within the chunk's 8 lanes); every register is
+// assigned on both sides of the select, so v[] keeps fixed indices and stays in VGPRs
+template <int RB, int LB>
+__device__ __forceinline__ void swap_bits(u64 *v, int lane)
+{
+    const bool up = (lane >> LB) & 1;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        if (r & (1 << RB)) continue;
+        const int ra = r, rb = r | (1 << RB);           // register bit RB = 0 / 1
+        const u64 a = v[ra], b = v[rb];
+        const u64 recv = xor_lane64<1 << LB>(up ? a : b);  // the lower lane keeps its ra, the upper lane its rb
+        v[ra] = up ? recv : a;
+        v[rb] = up ? b : recv;
+    }
+}
+
+// CO: the three swaps again after the last stages, back to the load layout (lane L holds x = 16 j + 2 L + h), so the
+// stores are coalesced 128-B runs like the loads instead of 16 consecutive words per lane
+template <bool FP, bool CO, class Bound>
+__device__ __forceinline__ void nttb_shfl_body(const Bound &bio, const DevPrime &pr, const TwTables &tt, int logN)
+{
+    constexpr int LOGP = 7;
+    const u64 q = pr.q, two_q = 2 * q;
+    const int lane = threadIdx.x & 7;
+    const u64 chunk = (u64)blockIdx.x * 32 + (threadIdx.x >> 3);
+    const u64 base = chunk << LOGP;
+    const u64 R = 1ull << (logN - LOGP);
+    const ulonglong2 *tw = tt.b + ((u64)bio.prime << logN);
+    const double *twf = tt.fb + ((u64)bio.prime << logN);
+    auto twidx = [=](int s, int i) -> u64 { return R * ((1ull << s) - 1) + (u64)i * R + chunk; };
+    const GlobalTw<decltype(twidx)> twg{twidx, tw, twf};
+    u64 v[16];
+    GroupTw<0, 3, FP> g0;
+    g0.load(0, twg);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const u64 g = base + 16 * j + 2 * lane;
+        if constexpr (HasPair<Bound>::value) {
+            const ulonglong2 w = bio.load2(g);
+            v[2 * j] = w.x;
+            v[2 * j + 1] = w.y;
+        } else {
+            v[2 * j] = bio.load(g);
+            v[2 * j + 1] = bio.load(g + 1);
+        }
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        u64 grp[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) grp[j] = v[2 * j + h];
+        g0.template run<false>(grp, pr);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[2 * j + h] = grp[j];
+    }
+    swap_bits<3, 2>(v, lane);
+    swap_bits<2, 1>(v, lane);
+    swap_bits<1, 0>(v, lane);
+    // output position of v[r]: 16 consecutive words per lane, or (CO) the load layout
+    auto opos = [&](int r) -> u64 {
+        return CO ? base + 16 * (u64)(r >> 1) + 2 * (u64)lane + (r & 1) : base + 16 * (u64)lane + r;
+    };
+    constexpr bool LATE = HasLatePre<Bound>::value;
+    typename Bound::Pre pre[16];
+    if constexpr (!LATE) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) pre[r] = bio.pre(opos(r));
+    }
+    GroupTw<3, 4, FP> g1;
+    g1.load(lane, twg);
+    g1.template run<false>(v, pr);
+    if constexpr (CO) {
+        swap_bits<1, 0>(v, lane);
+        swap_bits<2, 1>(v, lane);
+        swap_bits<3, 2>(v, lane);
+    }
+    if constexpr (LATE) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) pre[r] = bio.pre(opos(r));
+    }
+#pragma unroll
+    for (int r = 0; r < 16; r += 2) {
+        u64 a = v[r], b = v[r + 1];
+        const u64 g = opos(r);
+        if constexpr (FP) {
+            const double da = __longlong_as_double((long long)a), db = __longlong_as_double((long long)b);
+            if constexpr (HasFpStore<Bound>::value) {
+                if (bio.fpstore) {
+                    bio.store_fp(g, da, pre[r], pr);
+                    bio.store_fp(g + 1, db, pre[r + 1], pr);
+                    continue;
+                }
+            }
+            if constexpr (HasMForm<Bound>::value) {
+                if (bio.mform) {
+                    a = (u64)__double_as_longlong(fp_canon_d(da, pr.qd, pr.qinv));
+                    b = (u64)__double_as_longlong(fp_canon_d(db, pr.qd, pr.qinv));
+                } else {
+                    a = fp_canon(da, pr.qd, pr.qinv);
+                    b = fp_canon(db, pr.qd, pr.qinv);
+                }
+            } else {
+                a = fp_canon(da, pr.qd, pr.qinv);
+                b = fp_canon(db, pr.qd, pr.qinv);
+            }
+        } else {
+            a = csub(csub(a, two_q), q);
+            b = csub(csub(b, two_q), q);
+        }
+        if constexpr (HasPair<Bound>::value) {
+            bio.store2(g, a, b, pre[r], pre[r + 1]);
+        } else {
+            bio.store(g, a, pre[r]);
+            bio.store(g + 1, b, pre[r + 1]);
+        }
+    }
+}
+
+template <class IO, bool CO>
+__global__ void __launch_bounds__(256) k_nttb_shfl(const IO io, TwTables tt, const DevPrime *__restrict__ primes,
+                                                   int logN)
+{
+    const auto bio = io.bind(blockIdx.y);
+    if (!bio.valid) return;  // uniform per block
+    const DevPrime pr = primes[bio.prime];
+    if (pr.fp) nttb_shfl_body<true, CO>(bio, pr, tt, logN);
+    else nttb_shfl_body<false, CO>(bio, pr, tt, logN);
+}
+
 // A per-block branch on the prime's arithmetic class.  RD: the register-direct pass (ntt_pass_body_rd); otherwise
 // every round through LDS (ntt_pass_body: the forward pass B, where register-direct measured slower)
 template <int LOGP, int NSEG, bool INV, bool PASS_A, bool FINAL, class IO, bool RD = false>
@@ -780,7 +970,22 @@ static void run_ntt2(Ctx &c, int njobs, const IO1 &first, const IO2 &second, int
                            // SQ counters: a third fewer LDS and VMEM instructions, no bank conflicts either way,
                            // but 2.2x the cycles waiting on load dependencies and 15 % more wave cycles)
         if (stages & 1) k_ntt<LOGR, NA, false, true, false, IO1, true><<<gA, TA, 0, c.stream>>>(first, fwd, c.primes, c.logN);
-        if (stages & 2) k_ntt<LOGC, NB, false, false, true><<<gB, TB, 0, c.stream>>>(second, fwd, c.primes, c.logN);
+        if (stages & 2) {
+            // the wave-shuffle pass B (k_nttb_shfl: 32 chunks per 256-thread block) for the plain transform and the
+            // mod-up digits; the divide-and-round post-op keeps the LDS pass (its 16 outputs and post-op operands
+            // in registers at once would cost it a wave per SIMD)
+            if constexpr (LOGC == 7 && (std::is_same_v<IO2, StridedIO> || std::is_same_v<IO2, ModUpIO_B>)) {
+                if (c.nttb_shfl) {
+                    if (c.nttb_shfl == 2)
+                        k_nttb_shfl<IO2, true><<<dim3(R / 32, njobs), 256, 0, c.stream>>>(second, fwd, c.primes, c.logN);
+                    else
+                        k_nttb_shfl<IO2, false><<<dim3(R / 32, njobs), 256, 0, c.stream>>>(second, fwd, c.primes, c.logN);
+                    HEC_HIP(hipGetLastError());
+                    return;
+                }
+            }
+            k_ntt<LOGC, NB, false, false, true><<<gB, TB, 0, c.stream>>>(second, fwd, c.primes, c.logN);
+        }
     } else {
         if (stages & 1) k_ntt<LOGC, NB, true, false, false, IO1, true><<<gB, TB, 0, c.stream>>>(first, inv, c.primes, c.logN);
         if (stages & 2) k_ntt<LOGR, NA, true, true, true, IO2, true><<<gA, TA, 0, c.stream>>>(second, inv, c.primes, c.logN);
@@ -825,11 +1030,11 @@ void ntt_strided(Ctx &c, bool inverse, const u64 *src, u64 ps_src, u64 *dst, u64
     else ntt_dispatch<false>(c, njobs, first, second, stages);
 }
 
-void ks_modup(Ctx &c, const u64 *D, u64 *E, int B, int l, int stages)
+void ks_modup(Ctx &c, const u64 *D, u64 *E, int B, int l, int stages, bool mform)
 {
     ModUpMap m{l, c.logN, (int)c.K - 1};
     ModUpIO_A a{m, D, E, c.primes};
-    ModUpIO_B b{m, E};
+    ModUpIO_B b{m, E, mform ? 1 : 0};
     ntt_dispatch<false>(c, B * l * l, a, b, stages);
 }
 
@@ -1620,6 +1825,7 @@ struct HChild {
     const u64 *key, *W;
     u64 *ACC;
     const u64 *KW;
+    const u64 *MK;  // the key in MAC form and source order (mac_key_table)
 };
 template <int CG>
 struct HChildren {
@@ -1635,14 +1841,183 @@ struct HChildren {
 // the mod-down's (ACC - r) P^-1 already carries the IN term and its pass B reads one operand less (DivRoundIOB<false>).
 // The output position k of child c has source position gal_c(k) = s (hmacm's thread positions), so the term is the
 // same word X0[s] for every child.
+// MAC form (round 6): the FP64-class operands of the hoisted MAC as the k_hmacm loop consumes them, so it converts
+// nothing: the canonical residue as the bits of its integer-valued double.  The digits E of a hoisted node are stored
+// this way at the FP64 targets by their pass B (ModUpIO_B mform), the children's keys by mac_key_table (per Galois
+// key, also permuted into the node's source order, below).  (A split form for the 60-bit targets, lo30 | hi30 << 32
+// with four v_mad_u64_u32 per product and no carry chain, fit the register budget only at one batch entry per thread
+// and lost: k_hmacm 2,699-2,720 vs 2,501-2,540 ms per step at B = 128; the 60-bit targets keep the u64 loop.)
+__device__ __forceinline__ u64 mform(u64 v, bool fp) { return fp ? (u64)__double_as_longlong(u2d(v)) : v; }
+
+// The digit loop of k_hmacm at the FP64 targets on MAC-form operands (round 6).  The thread's two source positions
+// s0, s0 + 1 read the digit words E[b][I][J][s0..] and each child's key words MK_c[J][k][I][s0..] (mac_key_table:
+// key_c at gal_c(s) = galois_src(s, einv_c), so both streams are contiguous and in the same order, and no pair swap
+// happens inside the loop); the accumulators stay in source order and take the child's output order (kc, sw) at the
+// store.  The loop is unrolled by two with explicit double buffers (digit J + 1's words load while digit J
+// multiplies), so no register is copied per digit; exact fp_mulmod products summed as doubles.  The J == I digit is
+// the child's own NTT-form c1 (canonical u64, converted once).  The zero corrections are k_hmacm_zfix's.
+template <int BT, int CG>
+__device__ __forceinline__ void hmacm_body(PolyArr X1, PolyArr X0, const u64 *__restrict__ E, const HChildren<CG> &ch,
+                                           int B, int l, int K, int logN, const DevPrime &pr, u64 Pq, int I, int kI,
+                                           u64 s0, int b0)
+{
+    const u64 N = 1ull << logN;
+    u64 kc[CG];         // even slot of child c's output pair
+    bool sw[CG];        // output pair swapped
+    double f[CG][BT][4];
+#pragma unroll
+    for (int q = 0; q < CG; ++q) {
+        double wk[4] = {0, 0, 0, 0};  // W KW in source order: (k = 0: s0, s0 + 1), (k = 1: s0, s0 + 1)
+        if (q < ch.n) {
+            const u32 t = galois_src((u32)s0, ch.c[q].einv, logN);
+            kc[q] = t & ~1u;
+            sw[q] = t & 1;
+            const ulonglong2 w = *(const ulonglong2 *)(ch.c[q].W + ((u64)kI << logN) + kc[q]);
+            const ulonglong2 m0 = *(const ulonglong2 *)(ch.c[q].KW + ((u64)I << logN) + kc[q]);
+            const ulonglong2 m1 = *(const ulonglong2 *)(ch.c[q].KW + ((u64)(l + 1 + I) << logN) + kc[q]);
+            // the exact FP64 products (residues in [-0.53 q, 0.53 q]) start the sums
+            const double wx = u2d(w.x), wy = u2d(w.y);
+            wk[0] = fp_mulmod(wx, u2d(m0.x), pr.qd, pr.qinv);
+            wk[1] = fp_mulmod(wy, u2d(m0.y), pr.qd, pr.qinv);
+            wk[2] = fp_mulmod(wx, u2d(m1.x), pr.qd, pr.qinv);
+            wk[3] = fp_mulmod(wy, u2d(m1.y), pr.qd, pr.qinv);
+            if (sw[q]) {
+                double x = wk[0]; wk[0] = wk[1]; wk[1] = x;
+                x = wk[2]; wk[2] = wk[3]; wk[3] = x;
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < BT; ++t)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) f[q][t][r] = wk[r];
+    }
+    if (X0.p != nullptr && I < l) {  // + X0 (P mod q_I) on the c0 accumulators (exact residues, as every other term)
+        const double pmd = u2d(barrett64(Pq, pr.q, pr.r1));
+#pragma unroll
+        for (int t = 0; t < BT; ++t) {
+            const ulonglong2 x0 = *(const ulonglong2 *)(X0.p + min(b0 + t, B - 1) * X0.sb + ((u64)I << logN) + s0);
+            const double t0 = fp_mulmod(u2d(x0.x), pmd, pr.qd, pr.qinv);
+            const double t1 = fp_mulmod(u2d(x0.y), pmd, pr.qd, pr.qinv);
+#pragma unroll
+            for (int q = 0; q < CG; ++q) {
+                f[q][t][0] += t0;
+                f[q][t][1] += t1;
+            }
+        }
+    }
+    // The digit and key streams as buffer loads: a block-uniform descriptor per stream (E of batch entry t at (b, I),
+    // digit 0; MK of child q at limb kI, digit 0), the digit's uniform byte offset in an SGPR (soffset) and the
+    // thread's source offset so = 8 s0 as the one VGPR offset of every load: no per-load address arithmetic, and
+    // no address registers beside the double buffers.  A missing batch entry (b >= B, last batch group only) reads
+    // entry B - 1's words and stores nothing.
+    const u32 so = (u32)s0 * 8u, NB = (u32)(N * 8), KNB = (u32)(((u64)K << logN) * 8);
+    __amdgpu_buffer_rsrc_t rE[BT], rK[CG];
+#pragma unroll
+    for (int t = 0; t < BT; ++t) {
+        const int b = min(b0 + t, B - 1);
+        rE[t] = __builtin_amdgcn_make_buffer_rsrc((void *)(E + (((u64)((b * (l + 1) + I) * l)) << logN)), (short)0,
+                                                  (int)((u32)l * NB), 0x00020000);
+    }
+#pragma unroll
+    for (int q = 0; q < CG; ++q)
+        rK[q] = __builtin_amdgcn_make_buffer_rsrc((void *)(ch.c[q < ch.n ? q : 0].MK + ((u64)kI << logN)), (short)0,
+                                                  (int)((u32)(2 * l) * KNB), 0x00020000);
+    auto ld = [](__amdgpu_buffer_rsrc_t r, u32 vo, u32 soff) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, vo, soff, 0);
+        return ulonglong2{(u64)v[1] << 32 | v[0], (u64)v[3] << 32 | v[2]};
+    };
+    // every load is issued unconditionally (a missing child reads child 0's words, unused): a load under a branch
+    // would make every later wait count the loads of the path without it, and the waits would drain the prefetch
+    auto load = [&](int J, ulonglong2 *e, ulonglong2 (*k)[2]) {
+#pragma unroll
+        for (int t = 0; t < BT; ++t) e[t] = ld(rE[t], so, (u32)J * NB);
+#pragma unroll
+        for (int q = 0; q < CG; ++q) {
+            k[q][0] = ld(rK[q], so, (u32)(2 * J) * KNB);
+            k[q][1] = ld(rK[q], so, (u32)(2 * J + 1) * KNB);
+        }
+    };
+    // one product's dependency chain at a time (A/B round 6: the products interleaved two by two, with one key buffer
+    // reloaded per child as its products issue, measured slower: k_hmacm 2,405-2,440 vs 2,378-2,398 ms per step)
+    auto mac = [&](const ulonglong2 *e, ulonglong2 (*k)[2]) {
+#pragma unroll
+        for (int q = 0; q < CG; ++q) {
+            if (q >= ch.n) break;
+#pragma unroll
+            for (int t = 0; t < BT; ++t) {
+                if (b0 + t >= B) break;
+                const double d0 = __longlong_as_double((long long)e[t].x);
+                const double d1 = __longlong_as_double((long long)e[t].y);
+                f[q][t][0] += fp_mulmod(d0, __longlong_as_double((long long)k[q][0].x), pr.qd, pr.qinv);
+                f[q][t][1] += fp_mulmod(d1, __longlong_as_double((long long)k[q][0].y), pr.qd, pr.qinv);
+                f[q][t][2] += fp_mulmod(d0, __longlong_as_double((long long)k[q][1].x), pr.qd, pr.qinv);
+                f[q][t][3] += fp_mulmod(d1, __longlong_as_double((long long)k[q][1].y), pr.qd, pr.qinv);
+            }
+        }
+    };
+    ulonglong2 eA[BT], eB[BT], kA[CG][2], kB[CG][2];
+    // the digits J != I of the loop (I == l, the special prime, has no J == I digit)
+    const int nd = I < l ? l - 1 : l;
+    auto dig = [I](int k) { return k + (k >= I ? 1 : 0); };
+    if (I < l) {  // the J == I digit: the child's own NTT-form c1 (canonical u64), converted here
+#pragma unroll
+        for (int t = 0; t < BT; ++t) {
+            const ulonglong2 v = *(const ulonglong2 *)(X1.p + min(b0 + t, B - 1) * X1.sb + ((u64)I << logN) + s0);
+            eB[t] = ulonglong2{mform(v.x, true), mform(v.y, true)};
+        }
+#pragma unroll
+        for (int q = 0; q < CG; ++q) {
+            kB[q][0] = ld(rK[q], so, (u32)(2 * I) * KNB);
+            kB[q][1] = ld(rK[q], so, (u32)(2 * I + 1) * KNB);
+        }
+        if (nd > 0) load(dig(0), eA, kA);
+        mac(eB, kB);
+    } else if (nd > 0) {
+        load(dig(0), eA, kA);
+    }
+    // the loop body's loads are unconditional (the tail is peeled): a load under a branch would make the waits after
+    // it count the loads of the path without it, and they would drain the prefetch
+    int k = 0;
+    for (; k + 2 < nd; k += 2) {
+        load(dig(k + 1), eB, kB);
+        mac(eA, kA);
+        load(dig(k + 2), eA, kA);
+        mac(eB, kB);
+    }
+    if (k + 1 < nd) {  // two digits left
+        load(dig(k + 1), eB, kB);
+        mac(eA, kA);
+        mac(eB, kB);
+    } else if (k < nd) {
+        mac(eA, kA);
+    }
+#pragma unroll
+    for (int q = 0; q < CG; ++q) {
+        if (q >= ch.n) break;
+#pragma unroll
+        for (int t = 0; t < BT; ++t) {
+            const int b = b0 + t;
+            if (b >= B) break;
+            u64 r[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) r[i] = fp_canon(f[q][t][i], pr.qd, pr.qinv);
+            u64 *o0 = ch.c[q].ACC + (((u64)((b * 2 + 0) * (l + 1) + I)) << logN) + kc[q];
+            u64 *o1 = ch.c[q].ACC + (((u64)((b * 2 + 1) * (l + 1) + I)) << logN) + kc[q];
+            *(ulonglong2 *)o0 = sw[q] ? ulonglong2{r[1], r[0]} : ulonglong2{r[0], r[1]};
+            *(ulonglong2 *)o1 = sw[q] ? ulonglong2{r[3], r[2]} : ulonglong2{r[2], r[3]};
+        }
+    }
+}
+
+// The round-5 digit loop on canonical u64 operands (the original key gathered at the child's output slots, 128-bit
+// lazy sums), kept for the 60-bit targets: a thread owns BT batch entries (A/B round 6: the MAC-form split MAC at one
+// batch entry per thread, which fits the kernel's register budget, measured slower at the integer targets).
 template <int BT, int CG, bool FP>
-__device__ __forceinline__ void hmacm_body(PolyArr X1, PolyArr X0, const u64 *__restrict__ E,
+__device__ __forceinline__ void hmacm_body_u64(PolyArr X1, PolyArr X0, const u64 *__restrict__ E,
                                            const int *__restrict__ zl, const HChildren<CG> &ch, int B, int l, int K,
                                            int logN, const DevPrime &pr, u64 Pq, int I, int kI, u64 s0, int b0,
                                            const u64 *__restrict__ cji, const u64 *__restrict__ psipow)
 {
-    const bool zeros = zl[0] != 0;
-    const u64 *pp = psipow + ((u64)kI << (logN + 1));
     u64 kc[CG];       // even slot of child c's output pair
     bool sw[CG];      // output pair swapped
     u64 wk[CG][4];    // W KW in source order: (k = 0: s0, s0 + 1), (k = 1: s0, s0 + 1)
@@ -1787,55 +2162,6 @@ __device__ __forceinline__ void hmacm_body(PolyArr X1, PolyArr X0, const u64 *__
             }
         }
     }
-    if (zeros) {  // the rare zero corrections (only zeros of D_J that a child negates), after the digit loop as
-                  // + (q - corr) key_J at the child's output slots kc ^ sw, kc ^ !sw: the MAC is linear, every term exact
-        const u64 N = 1ull << logN;
-        for (int J = 0; J < l; ++J) {
-            if (J == I) continue;
-            const u64 cj = cji[J * K + kI];
-#pragma unroll
-            for (int t = 0; t < BT; ++t) {
-                if (b0 + t >= B) break;
-                const int *z = zl + 1 + ((b0 + t) * l + J) * (HEC_ZCAP + 1);
-                const int nz = min(z[0], HEC_ZCAP);
-                if (nz == 0) continue;
-#pragma unroll
-                for (int q = 0; q < CG; ++q) {
-                    if (q >= ch.n) break;
-                    const u64 ko0 = kc[q] | (u64)sw[q], ko1 = kc[q] | (u64)!sw[q];
-                    u64 c0 = 0, c1 = 0;
-                    for (int zi = 0; zi < nz; ++zi) {
-                        u64 tt = ((u64)z[1 + zi] * ch.c[q].elt) & (2 * N - 1);
-                        if (tt < N) continue;
-                        tt -= N;
-                        const u64 ex0 = ((2 * (u64)bitrev((u32)ko0, logN) + 1) * tt) & (2 * N - 1);
-                        const u64 ex1 = ((2 * (u64)bitrev((u32)ko1, logN) + 1) * tt) & (2 * N - 1);
-                        c0 = addmod(c0, mulmod(cj, pp[ex0], pr), pr.q);
-                        c1 = addmod(c1, mulmod(cj, pp[ex1], pr), pr.q);
-                    }
-                    if (c0 == 0 && c1 == 0) continue;
-                    const u64 n0 = c0 ? pr.q - c0 : 0, n1 = c1 ? pr.q - c1 : 0;
-                    const u64 *kp = ch.c[q].key + (((u64)(J * 2) * K + kI) << logN) + kc[q];
-                    ulonglong2 k0 = *(const ulonglong2 *)kp, k1 = *(const ulonglong2 *)(kp + ((u64)K << logN));
-                    if (sw[q]) {
-                        k0 = ulonglong2{k0.y, k0.x};
-                        k1 = ulonglong2{k1.y, k1.x};
-                    }
-                    if constexpr (FP) {
-                        f[q][t][0] += fp_mulmod(u2d(n0), u2d(k0.x), pr.qd, pr.qinv);
-                        f[q][t][1] += fp_mulmod(u2d(n1), u2d(k0.y), pr.qd, pr.qinv);
-                        f[q][t][2] += fp_mulmod(u2d(n0), u2d(k1.x), pr.qd, pr.qinv);
-                        f[q][t][3] += fp_mulmod(u2d(n1), u2d(k1.y), pr.qd, pr.qinv);
-                    } else {
-                        mac128(a[q][t][0], n0, k0.x);
-                        mac128(a[q][t][1], n1, k0.y);
-                        mac128(a[q][t][2], n0, k1.x);
-                        mac128(a[q][t][3], n1, k1.y);
-                    }
-                }
-            }
-        }
-    }
 #pragma unroll
     for (int q = 0; q < CG; ++q) {
         if (q >= ch.n) break;
@@ -1855,6 +2181,27 @@ __device__ __forceinline__ void hmacm_body(PolyArr X1, PolyArr X0, const u64 *__
             *(ulonglong2 *)o1 = sw[q] ? ulonglong2{r[3], r[2]} : ulonglong2{r[2], r[3]};
         }
     }
+}
+
+// The MAC-form key table of one Galois key for the hoisted MAC: MK[J][k][I][s] = mform(key[J][k][I][galois_src(s,
+// einv)]) over the key's L digits, 2 polys and K limbs (einv = elt^-1 mod 2N: the child's output position of source s)
+__global__ void __launch_bounds__(256) k_mac_key(const u64 *__restrict__ key, u64 *__restrict__ MK, u32 einv, int K,
+                                                 int logN, const DevPrime *__restrict__ primes)
+{
+    const u64 N = 1ull << logN;
+    const u64 s = (u64)blockIdx.x * 256 + threadIdx.x;
+    const int row = blockIdx.y, I = row % K;  // row = (J 2 + k) K + I
+    if (s >= N) return;
+    const bool fp = cprime(primes, I).fp != 0;
+    const u64 v = key[((u64)row << logN) + galois_src((u32)s, einv, logN)];
+    MK[((u64)row << logN) + s] = mform(v, fp);
+}
+
+void mac_key_table(Ctx &c, const u64 *key, u64 *MK, u32 einv)
+{
+    k_mac_key<<<dim3((unsigned)((c.N + 255) / 256), (unsigned)(c.L * 2 * c.K)), 256, 0, c.stream>>>(
+        key, MK, einv, (int)c.K, c.logN, c.primes);
+    HEC_HIP(hipGetLastError());
 }
 
 // KW[k][I][t] = sum_{J<l, J != I} (q_J mod q_I) key[J][k][I][t] mod q_I (128-bit lazy sum, one Barrett)
@@ -1920,9 +2267,65 @@ __global__ void __launch_bounds__(256, MINW)  // MINW waves per SIMD: 3 -> <= 16
     const u64 s0 = (u64)xb * 512 + 2 * threadIdx.x;
     const u64 Pq = cprime(primes, K - 1).q;
     if (!integer)
-        hmacm_body<BTF, CG, true>(X1, X0, E, zl, ch, B, l, K, logN, pr, Pq, I, kI, s0, bg * BTF, cji, psipow);
+        hmacm_body<BTF, CG>(X1, X0, E, ch, B, l, K, logN, pr, Pq, I, kI, s0, bg * BTF);
     else
-        hmacm_body<BTI, CG, false>(X1, X0, E, zl, ch, B, l, K, logN, pr, Pq, I, kI, s0, bg * BTI, cji, psipow);
+        hmacm_body_u64<BTI, CG, false>(X1, X0, E, zl, ch, B, l, K, logN, pr, Pq, I, kI, s0, bg * BTI, cji, psipow);
+}
+
+// The zero corrections of the sibling-fused hoisted MAC (§4.6 of DESIGN.md), as their own pass over the children's
+// accumulators (round 6; they were a branch after k_hmacm's digit loop, whose registers every thread carried):
+//   ACC_c[b][k][I][o] -= sum_{J != I} C_J(o) key_c[J][k][I][o]  (mod q_I),
+//   C_J(o) = sum over the zeros z of D_J[b] that child c negates (tt = z elt mod 2N >= N) of
+//            (q_J mod q_I) psi_I^((2 bitrev(o) + 1)(tt - N)).
+// The MAC is linear and every term is exact mod q_I, so subtracting them from the canonical MAC gives the same bits as
+// adding them inside it.  Uniform residues almost never have a zero coefficient: a small fixed grid that exits at once
+// when the node has none (zl[0] == 0), else strides over (child, b, I, o).
+template <int CG, int NS>
+__global__ void __launch_bounds__(256)
+    k_hmacm_zfix(const HSlots<CG, NS> S, const int *__restrict__ zl, int B, int l, int K, int logN,
+                 const DevPrime *__restrict__ primes, const int *__restrict__ Imap, int nI, const u64 *__restrict__ cji,
+                 const u64 *__restrict__ psipow)
+{
+    if (zl[0] == 0) return;
+    const u64 N = 1ull << logN, N2 = 2 * N;
+    const int ns = NS == 1 ? 1 : S.ns;
+    const u64 total = (u64)ns * CG * B * nI * N;
+    for (u64 w = (u64)blockIdx.x * 256 + threadIdx.x; w < total; w += (u64)gridDim.x * 256) {
+        const u64 o = w % N;
+        u64 r = w / N;
+        const int yi = (int)(r % nI);
+        r /= nI;
+        const int b = (int)(r % B), ci = (int)(r / B);
+        const HChildren<CG> &ch = S.s[ci / CG];
+        if (ci % CG >= ch.n) continue;
+        const HChild &c = ch.c[ci % CG];
+        const int I = Imap[yi], kI = I == l ? K - 1 : I;
+        const DevPrime pr = primes[kI];
+        const u64 *pp = psipow + ((u64)kI << (logN + 1));
+        const u64 bo = 2 * (u64)bitrev((u32)o, logN) + 1;
+        u64 corr0 = 0, corr1 = 0;
+        for (int J = 0; J < l; ++J) {
+            if (J == I) continue;
+            const int *z = zl + 1 + (b * l + J) * (HEC_ZCAP + 1);
+            const int nz = min(z[0], HEC_ZCAP);
+            if (nz == 0) continue;
+            const u64 cj = cji[J * K + kI];
+            u64 cc = 0;
+            for (int zi = 0; zi < nz; ++zi) {
+                u64 tt = ((u64)z[1 + zi] * c.elt) & (N2 - 1);
+                if (tt < N) continue;
+                cc = addmod(cc, mulmod(cj, pp[(bo * (tt - N)) & (N2 - 1)], pr), pr.q);
+            }
+            if (cc == 0) continue;
+            corr0 = addmod(corr0, mulmod(cc, c.key[(((u64)(J * 2 + 0) * K + kI) << logN) + o], pr), pr.q);
+            corr1 = addmod(corr1, mulmod(cc, c.key[(((u64)(J * 2 + 1) * K + kI) << logN) + o], pr), pr.q);
+        }
+        if ((corr0 | corr1) == 0) continue;
+        u64 *a0 = c.ACC + (((u64)((b * 2 + 0) * (l + 1) + I)) << logN) + o;
+        u64 *a1 = c.ACC + (((u64)((b * 2 + 1) * (l + 1) + I)) << logN) + o;
+        *a0 = submod(*a0, corr0, pr.q);
+        *a1 = submod(*a1, corr1, pr.q);
+    }
 }
 
 // nkids children in slots of CG (the last slot may hold fewer), at most NS slots
@@ -1935,7 +2338,7 @@ static void launch_hmacm(Ctx &c, PolyArr X1, PolyArr X0, const u64 *E, const int
     if (nkids < 1 || S.ns > NS) throw std::invalid_argument("hoisted MAC: children per launch");
     for (int q = 0; q < nkids; ++q) {
         HChildren<CG> &ch = S.s[q / CG];
-        ch.c[q % CG] = HChild{kids[q].elt, kids[q].einv, kids[q].key, kids[q].W, kids[q].ACC, kids[q].KW};
+        ch.c[q % CG] = HChild{kids[q].elt, kids[q].einv, kids[q].key, kids[q].W, kids[q].ACC, kids[q].KW, kids[q].MK};
         ch.n = q % CG + 1;
     }
     const int nint = c.imap_nint[l], X = (int)(c.N / 512);
@@ -1943,6 +2346,9 @@ static void launch_hmacm(Ctx &c, PolyArr X1, PolyArr X0, const u64 *E, const int
     const int wsplit = gI * ((B + BTI - 1) / BTI), total = wsplit + gF * ((B + BTF - 1) / BTF);
     k_hmacm<BTF, BTI, CG, MINW, NS><<<dim3((unsigned)(total * S.ns)), 256, 0, c.stream>>>(
         X1, X0, E, zl, S, B, l, (int)c.K, c.logN, c.primes, c.imap_at(l), l + 1, nint, c.cji, c.psipow, wsplit);
+    HEC_HIP(hipGetLastError());
+    k_hmacm_zfix<CG, NS><<<256, 256, 0, c.stream>>>(S, zl, B, l, (int)c.K, c.logN, c.primes, c.imap_at(l), l + 1, c.cji,
+                                                    c.psipow);
     HEC_HIP(hipGetLastError());
 }
 

@@ -88,6 +88,47 @@ def test_ntt_bitexact(orc, hecdna, logN):
     assert np.array_equal(ctx.ntt(sub, limb0=1), exp[:, 1:])
 
 
+@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("logN", [13, 14, 15, 16])
+def test_ntt_pass_b_shuffle_bitexact(orc, hecdna, logN, mode):
+    """The opt-in wave-shuffle forward pass B (hec_context_set_option "nttb_shfl"; k_nttb_shfl, 128-point columns
+    exchanged through DPP lane moves instead of LDS; mode 2 swaps back to coalesced stores) gives the oracle's bits
+    wherever it applies (128-point pass B), and the LDS pass elsewhere."""
+    N = 1 << logN
+    bits = [60, 40, 50, 60] if logN < 16 else [60, 40, 60]
+    m = orc.Oracle.create_coeff_modulus(N, bits)
+    o = orc.Oracle(N, m)
+    ctx = hecdna.Context(N, m)
+    ctx.set_option("nttb_shfl", mode)
+    rng = np.random.default_rng(700 + logN)
+    a = np.stack([np.stack([rng.integers(0, q, N, dtype=np.uint64) for q in m]) for _ in range(2)])
+    exp = np.stack([np.stack([o.ntt_fwd(i, a[p, i]) for i in range(len(m))]) for p in range(2)])
+    fwd = ctx.ntt(a)
+    assert np.array_equal(fwd, exp)
+    assert np.array_equal(ctx.ntt(fwd, inverse=True), a)
+    assert np.array_equal(ctx.ntt(np.ascontiguousarray(a[:, 1:]), limb0=1), exp[:, 1:])
+
+
+@pytest.mark.parametrize("mode", [1, 2])
+def test_cfg3_shuffle_pass_b_keyswitch_bitexact(env15, mode):
+    """cfg3 parameters with the wave-shuffle pass B on (the mod-up digits' forward transforms): rotations and a small
+    hoisted matvec equal the oracle's bits."""
+    e = env15
+    e.ctx.set_option("nttb_shfl", mode)
+    try:
+        a = e.enc(seed=5)
+        for steps in (1, 4095):
+            e.same(e.ctx.rotate_vector(e.up(a), steps, e.gk), e.o.rotate(a, steps, e.gk_h))
+        A = [e.enc(seed=60 + j) for j in range(5)]
+        X = [e.enc(seed=90 + i) for i in range(2)]
+        exp = e.o.matmul_diag_col(A, X, e.rk_h, e.gk_h, nthreads=8)
+        got = e.ctx.matmul_diag_col([e.up(x) for x in A], [e.up(x) for x in X], e.rk, e.gk)
+        for g, c in zip(got, exp):
+            e.same(g, c)
+    finally:
+        e.ctx.set_option("nttb_shfl", 0)
+
+
 def test_ntt_cfg2_golden(orc, hecdna):
     fx = json.load(open(os.path.join(GOLD, "cfg2_ntt.json")))
     N, m = fx["N"], fx["moduli"]
