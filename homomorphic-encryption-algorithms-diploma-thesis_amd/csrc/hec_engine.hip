@@ -1440,6 +1440,8 @@ int hec_context_create(uint64_t N, const uint64_t *mod, uint64_t K, int device, 
         if (const char *f = std::getenv("HEC_KERNEL_MEMOPS")) c.kernel_memops = f[0] != '0';
         if (const char *f = std::getenv("HEC_SPLIT_BFLY")) c.split_bfly = std::atoi(f);
         if (const char *f = std::getenv("HEC_NTTB_SHFL")) c.nttb_shfl = std::min(2, std::max(0, std::atoi(f)));
+        if (const char *f = std::getenv("HEC_NTTB_SHFL_DR")) c.nttb_shfl_dr = std::atoi(f) != 0;
+        if (const char *f = std::getenv("HEC_HMAC_INT")) c.hmac_int = std::atoi(f) != 0;
         if (const char *f = std::getenv("HEC_BMAC_SPLIT")) c.bmac_split = f[0] != '0';
         c.N = N;
         c.logN = __builtin_ctzll(N);
@@ -1663,6 +1665,8 @@ int hec_context_set_option(hec_context *ctx, const char *name, int64_t value)
             else if (n == "kernel_memops") c.kernel_memops = value != 0;
             else if (n == "split_bfly") c.split_bfly = in(0, 4);
             else if (n == "nttb_shfl") c.nttb_shfl = in(0, 2);
+            else if (n == "nttb_shfl_dr") c.nttb_shfl_dr = in(0, 1);
+            else if (n == "hmac_int") c.hmac_int = in(0, 1);
             else if (n == "bmac_split") c.bmac_split = value != 0;
             else if (n == "hoist") c.hoist = value != 0;
             else if (n == "hoist_min") c.hoist_min_children = (int)std::max<int64_t>(1, value);

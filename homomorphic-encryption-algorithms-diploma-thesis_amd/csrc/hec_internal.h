@@ -70,6 +70,8 @@ struct Ctx {
     bool bmac_split = true;        // HEC_BMAC_SPLIT=0: k_bmac's integer-target pass B on plain Shoup butterflies
     int nttb_shfl = 0;             // HEC_NTTB_SHFL=1: the forward NTT's pass B at N = 2^15 as k_nttb_shfl (exchanges
                                    // between lanes of a wavefront, no LDS tile), round 6
+    int hmac_int = 1;              // HEC_HMAC_INT=0: k_hmacm's 60-bit targets on the round-5 loop (gathered keys)
+    int nttb_shfl_dr = 0;          // HEC_NTTB_SHFL_DR=1: the same for the divide-and-round pass B (A/B only)
     int split_bfly = 4;            // HEC_SPLIT_BFLY: 0 plain Shoup in the fan-out kernels, 1 split-input Shoup in
                                    // k_fan2, 2 also k_fan2j's per-thread-twiddle rounds, 3 all of k_fan2j, 4 k_fan2 and
                                    // k_fan2j's scalar-twiddle round (hec_kernels.hip run_fan; profiles/r05s_*)

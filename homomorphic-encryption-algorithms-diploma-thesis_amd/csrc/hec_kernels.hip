@@ -974,8 +974,9 @@ static void run_ntt2(Ctx &c, int njobs, const IO1 &first, const IO2 &second, int
             // the wave-shuffle pass B (k_nttb_shfl: 32 chunks per 256-thread block) for the plain transform and the
             // mod-up digits; the divide-and-round post-op keeps the LDS pass (its 16 outputs and post-op operands
             // in registers at once would cost it a wave per SIMD)
-            if constexpr (LOGC == 7 && (std::is_same_v<IO2, StridedIO> || std::is_same_v<IO2, ModUpIO_B>)) {
-                if (c.nttb_shfl) {
+            constexpr bool kDR = std::is_same_v<IO2, DivRoundIOB<false>> || std::is_same_v<IO2, DivRoundIOB<true>>;
+            if constexpr (LOGC == 7 && (std::is_same_v<IO2, StridedIO> || std::is_same_v<IO2, ModUpIO_B> || kDR)) {
+                if (c.nttb_shfl && (!kDR || c.nttb_shfl_dr)) {
                     if (c.nttb_shfl == 2)
                         k_nttb_shfl<IO2, true><<<dim3(R / 32, njobs), 256, 0, c.stream>>>(second, fwd, c.primes, c.logN);
                     else
@@ -2183,6 +2184,145 @@ __device__ __forceinline__ void hmacm_body_u64(PolyArr X1, PolyArr X0, const u64
     }
 }
 
+// The 60-bit targets on the MAC-form streams (round 6): the FP64 body's loads (source-ordered key table MK, canonical
+// u64 at these limbs; buffer loads; the J == I digit before the loop; unconditional double-buffered loads) with SEAL's
+// 128-bit lazy sums, one Barrett reduction per output word.  HEC_HMAC_INT=0: the round-5 loop above.
+template <int BT, int CG>
+__device__ __forceinline__ void hmacm_body_int(PolyArr X1, PolyArr X0, const u64 *__restrict__ E, const HChildren<CG> &ch,
+                                               int B, int l, int K, int logN, const DevPrime &pr, u64 Pq, int I,
+                                               int kI, u64 s0, int b0)
+{
+    const u64 N = 1ull << logN;
+    u64 kc[CG];
+    bool sw[CG];
+    U128 a[CG][BT][4];
+#pragma unroll
+    for (int q = 0; q < CG; ++q) {
+        u64 wk[4] = {0, 0, 0, 0};
+        if (q < ch.n) {
+            const u32 t = galois_src((u32)s0, ch.c[q].einv, logN);
+            kc[q] = t & ~1u;
+            sw[q] = t & 1;
+            const ulonglong2 w = *(const ulonglong2 *)(ch.c[q].W + ((u64)kI << logN) + kc[q]);
+            const ulonglong2 m0 = *(const ulonglong2 *)(ch.c[q].KW + ((u64)I << logN) + kc[q]);
+            const ulonglong2 m1 = *(const ulonglong2 *)(ch.c[q].KW + ((u64)(l + 1 + I) << logN) + kc[q]);
+            wk[0] = mulmod(w.x, m0.x, pr);
+            wk[1] = mulmod(w.y, m0.y, pr);
+            wk[2] = mulmod(w.x, m1.x, pr);
+            wk[3] = mulmod(w.y, m1.y, pr);
+            if (sw[q]) {
+                u64 x = wk[0]; wk[0] = wk[1]; wk[1] = x;
+                x = wk[2]; wk[2] = wk[3]; wk[3] = x;
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < BT; ++t)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) a[q][t][r] = U128{wk[r], 0};
+    }
+    if (X0.p != nullptr && I < l) {  // + X0 (P mod q_I) on the c0 accumulators
+        const u64 pm = barrett64(Pq, pr.q, pr.r1);
+#pragma unroll
+        for (int t = 0; t < BT; ++t) {
+            const ulonglong2 x0 = *(const ulonglong2 *)(X0.p + min(b0 + t, B - 1) * X0.sb + ((u64)I << logN) + s0);
+            const u64 t0 = mulmod(x0.x, pm, pr), t1 = mulmod(x0.y, pm, pr);
+#pragma unroll
+            for (int q = 0; q < CG; ++q) {
+                a[q][t][0].lo += t0;
+                a[q][t][0].hi += a[q][t][0].lo < t0;
+                a[q][t][1].lo += t1;
+                a[q][t][1].hi += a[q][t][1].lo < t1;
+            }
+        }
+    }
+    const u32 so = (u32)s0 * 8u, NB = (u32)(N * 8), KNB = (u32)(((u64)K << logN) * 8);
+    __amdgpu_buffer_rsrc_t rE[BT], rK[CG];
+#pragma unroll
+    for (int t = 0; t < BT; ++t) {
+        const int b = min(b0 + t, B - 1);
+        rE[t] = __builtin_amdgcn_make_buffer_rsrc((void *)(E + (((u64)((b * (l + 1) + I) * l)) << logN)), (short)0,
+                                                  (int)((u32)l * NB), 0x00020000);
+    }
+#pragma unroll
+    for (int q = 0; q < CG; ++q)
+        rK[q] = __builtin_amdgcn_make_buffer_rsrc((void *)(ch.c[q < ch.n ? q : 0].MK + ((u64)kI << logN)), (short)0,
+                                                  (int)((u32)(2 * l) * KNB), 0x00020000);
+    auto ld = [](__amdgpu_buffer_rsrc_t r, u32 vo, u32 soff) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, vo, soff, 0);
+        return ulonglong2{(u64)v[1] << 32 | v[0], (u64)v[3] << 32 | v[2]};
+    };
+    auto load = [&](int J, ulonglong2 *e, ulonglong2 (*k)[2]) {
+#pragma unroll
+        for (int t = 0; t < BT; ++t) e[t] = ld(rE[t], so, (u32)J * NB);
+#pragma unroll
+        for (int q = 0; q < CG; ++q) {
+            k[q][0] = ld(rK[q], so, (u32)(2 * J) * KNB);
+            k[q][1] = ld(rK[q], so, (u32)(2 * J + 1) * KNB);
+        }
+    };
+    auto mac = [&](const ulonglong2 *e, ulonglong2 (*k)[2]) {
+#pragma unroll
+        for (int q = 0; q < CG; ++q) {
+            if (q >= ch.n) break;
+#pragma unroll
+            for (int t = 0; t < BT; ++t) {
+                if (b0 + t >= B) break;
+                mac128(a[q][t][0], e[t].x, k[q][0].x);
+                mac128(a[q][t][1], e[t].y, k[q][0].y);
+                mac128(a[q][t][2], e[t].x, k[q][1].x);
+                mac128(a[q][t][3], e[t].y, k[q][1].y);
+            }
+        }
+    };
+    ulonglong2 eA[BT], eB[BT], kA[CG][2], kB[CG][2];
+    const int nd = I < l ? l - 1 : l;
+    auto dig = [I](int k) { return k + (k >= I ? 1 : 0); };
+    if (I < l) {  // the J == I digit: the child's own NTT-form c1
+#pragma unroll
+        for (int t = 0; t < BT; ++t)
+            eB[t] = *(const ulonglong2 *)(X1.p + min(b0 + t, B - 1) * X1.sb + ((u64)I << logN) + s0);
+#pragma unroll
+        for (int q = 0; q < CG; ++q) {
+            kB[q][0] = ld(rK[q], so, (u32)(2 * I) * KNB);
+            kB[q][1] = ld(rK[q], so, (u32)(2 * I + 1) * KNB);
+        }
+        if (nd > 0) load(dig(0), eA, kA);
+        mac(eB, kB);
+    } else if (nd > 0) {
+        load(dig(0), eA, kA);
+    }
+    int k = 0;
+    for (; k + 2 < nd; k += 2) {
+        load(dig(k + 1), eB, kB);
+        mac(eA, kA);
+        load(dig(k + 2), eA, kA);
+        mac(eB, kB);
+    }
+    if (k + 1 < nd) {
+        load(dig(k + 1), eB, kB);
+        mac(eA, kA);
+        mac(eB, kB);
+    } else if (k < nd) {
+        mac(eA, kA);
+    }
+#pragma unroll
+    for (int q = 0; q < CG; ++q) {
+        if (q >= ch.n) break;
+#pragma unroll
+        for (int t = 0; t < BT; ++t) {
+            const int b = b0 + t;
+            if (b >= B) break;
+            u64 r[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) r[i] = barrett128(a[q][t][i].lo, a[q][t][i].hi, pr.q, pr.r0, pr.r1);
+            u64 *o0 = ch.c[q].ACC + (((u64)((b * 2 + 0) * (l + 1) + I)) << logN) + kc[q];
+            u64 *o1 = ch.c[q].ACC + (((u64)((b * 2 + 1) * (l + 1) + I)) << logN) + kc[q];
+            *(ulonglong2 *)o0 = sw[q] ? ulonglong2{r[1], r[0]} : ulonglong2{r[0], r[1]};
+            *(ulonglong2 *)o1 = sw[q] ? ulonglong2{r[3], r[2]} : ulonglong2{r[2], r[3]};
+        }
+    }
+}
+
 // The MAC-form key table of one Galois key for the hoisted MAC: MK[J][k][I][s] = mform(key[J][k][I][galois_src(s,
 // einv)]) over the key's L digits, 2 polys and K limbs (einv = elt^-1 mod 2N: the child's output position of source s)
 __global__ void __launch_bounds__(256) k_mac_key(const u64 *__restrict__ key, u64 *__restrict__ MK, u32 einv, int K,
@@ -2246,7 +2386,7 @@ template <int BTF, int BTI, int CG, int MINW, int NS>
 __global__ void __launch_bounds__(256, MINW)  // MINW waves per SIMD: 3 -> <= 168 VGPRs, 2 -> <= 256
     k_hmacm(PolyArr X1, PolyArr X0, const u64 *__restrict__ E, const int *__restrict__ zl, const HSlots<CG, NS> S,
             int B, int l, int K, int logN, const DevPrime *__restrict__ primes, const int *__restrict__ Imap, int nI,
-            int nint, const u64 *__restrict__ cji, const u64 *__restrict__ psipow, int wsplit)
+            int nint, const u64 *__restrict__ cji, const u64 *__restrict__ psipow, int wsplit, int int_mform)
 {
     const u64 N = 1ull << logN;
     const int X = (int)(N / 512);
@@ -2268,6 +2408,8 @@ __global__ void __launch_bounds__(256, MINW)  // MINW waves per SIMD: 3 -> <= 16
     const u64 Pq = cprime(primes, K - 1).q;
     if (!integer)
         hmacm_body<BTF, CG>(X1, X0, E, ch, B, l, K, logN, pr, Pq, I, kI, s0, bg * BTF);
+    else if (int_mform)
+        hmacm_body_int<BTI, CG>(X1, X0, E, ch, B, l, K, logN, pr, Pq, I, kI, s0, bg * BTI);
     else
         hmacm_body_u64<BTI, CG, false>(X1, X0, E, zl, ch, B, l, K, logN, pr, Pq, I, kI, s0, bg * BTI, cji, psipow);
 }
@@ -2345,7 +2487,8 @@ static void launch_hmacm(Ctx &c, PolyArr X1, PolyArr X0, const u64 *E, const int
     const int gI = (X * nint + 7) / 8 * 8, gF = (X * (l + 1 - nint) + 7) / 8 * 8;
     const int wsplit = gI * ((B + BTI - 1) / BTI), total = wsplit + gF * ((B + BTF - 1) / BTF);
     k_hmacm<BTF, BTI, CG, MINW, NS><<<dim3((unsigned)(total * S.ns)), 256, 0, c.stream>>>(
-        X1, X0, E, zl, S, B, l, (int)c.K, c.logN, c.primes, c.imap_at(l), l + 1, nint, c.cji, c.psipow, wsplit);
+        X1, X0, E, zl, S, B, l, (int)c.K, c.logN, c.primes, c.imap_at(l), l + 1, nint, c.cji, c.psipow, wsplit,
+        c.hmac_int);
     HEC_HIP(hipGetLastError());
     k_hmacm_zfix<CG, NS><<<256, 256, 0, c.stream>>>(S, zl, B, l, (int)c.K, c.logN, c.primes, c.imap_at(l), l + 1, c.cji,
                                                     c.psipow);

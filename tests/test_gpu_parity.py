@@ -109,12 +109,13 @@ def test_ntt_pass_b_shuffle_bitexact(orc, hecdna, logN, mode):
     assert np.array_equal(ctx.ntt(np.ascontiguousarray(a[:, 1:]), limb0=1), exp[:, 1:])
 
 
-@pytest.mark.parametrize("mode", [1, 2])
-def test_cfg3_shuffle_pass_b_keyswitch_bitexact(env15, mode):
-    """cfg3 parameters with the wave-shuffle pass B on (the mod-up digits' forward transforms): rotations and a small
-    hoisted matvec equal the oracle's bits."""
+@pytest.mark.parametrize("mode,dr", [(1, 0), (2, 0), (2, 1)])
+def test_cfg3_shuffle_pass_b_keyswitch_bitexact(env15, mode, dr):
+    """cfg3 parameters with the wave-shuffle pass B on (the mod-up digits' forward transforms; dr: the mod-down's
+    divide-and-round pass B too): rotations and a small hoisted matvec equal the oracle's bits."""
     e = env15
     e.ctx.set_option("nttb_shfl", mode)
+    e.ctx.set_option("nttb_shfl_dr", dr)
     try:
         a = e.enc(seed=5)
         for steps in (1, 4095):
@@ -127,6 +128,7 @@ def test_cfg3_shuffle_pass_b_keyswitch_bitexact(env15, mode):
             e.same(g, c)
     finally:
         e.ctx.set_option("nttb_shfl", 0)
+        e.ctx.set_option("nttb_shfl_dr", 0)
 
 
 def test_ntt_cfg2_golden(orc, hecdna):
@@ -455,7 +457,8 @@ def test_cfg5_params_matvec_bitexact(orc, hecdna):
                                  {"HEC_HMAC": "0"}, {"HEC_HMAC": "0", "HEC_HOIST_MIN": "1"},
                                  {"HEC_HMAC": "1"}, {"HEC_HMAC": "1", "HEC_HMAC_ODD3": "0"},
                                  {"HEC_HOIST_SCAN": "0"}, {"HEC_KERNEL_MEMOPS": "0"}, {"HEC_SPLIT_BFLY": "0"},
-                                 {"HEC_SPLIT_BFLY": "1"}, {"HEC_SPLIT_BFLY": "3"}, {"HEC_BMAC_SPLIT": "0"}])
+                                 {"HEC_SPLIT_BFLY": "1"}, {"HEC_SPLIT_BFLY": "3"}, {"HEC_BMAC_SPLIT": "0"},
+                                 {"HEC_HMAC_INT": "0"}])
 def test_keyswitch_variants_bitexact(orc, hecdna, env):
     """The engine's alternative key-switch schedules (separate mod-up pass B + MAC kernels; the fused
     kernel's key-load placements) give the same bits as the oracle."""
@@ -615,7 +618,8 @@ def _env_with(orc, hecdna, env, *args, **kw):
 
 
 @pytest.mark.parametrize("nzeros", [3, 40])  # 40 > HEC_ZCAP: the hoisted walk recomputes without hoisting
-@pytest.mark.parametrize("variant", [{}, {"HEC_HMAC": "0"}, {"HEC_HMAC": "1"}, {"HEC_HMAC": "1", "HEC_HMAC_ODD3": "0"}])
+@pytest.mark.parametrize("variant", [{}, {"HEC_HMAC": "0"}, {"HEC_HMAC": "1"}, {"HEC_HMAC": "1", "HEC_HMAC_ODD3": "0"},
+                                     {"HEC_HMAC_INT": "0"}])
 def test_hoisted_modup_zero_coefficients(orc, hecdna, nzeros, variant):
     """The hoisted mod-up corrects for zero digit coefficients that the Galois automorphism negates
     (SEAL maps -0 to 0, not to q_J); a limb with more zeros than the kernels list falls back.  Every hoisted MAC
