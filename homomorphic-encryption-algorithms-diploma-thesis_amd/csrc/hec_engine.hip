@@ -59,9 +59,34 @@ struct hec_context {
     // multi-GPU (hec_comm_init): this process's rank in a world of one process per GPU, RCCL communicator
     int rank = 0, world = 1;
     HecComm *comm = nullptr;
+    u64 gen = 0;  // this context's entry in the live-context registry (ctx_alive)
 };
+// Objects may outlive their context (SEAL's objects hold their context by shared_ptr, so a caller may free them in
+// any order, and a garbage collector finalising a reference cycle picks its own order): every object records its
+// context's generation, and its destroy touches the context (device, stream) only while that context is alive.
+// An address reused by a later context carries a new generation, so it is never mistaken for the old one.
+static std::mutex g_live_mu;
+static std::map<const hec_context *, u64> g_live;
+static u64 g_live_gen = 0;
+static u64 ctx_register(const hec_context *c)
+{
+    std::lock_guard<std::mutex> lock(g_live_mu);
+    return g_live[c] = ++g_live_gen;
+}
+static void ctx_unregister(const hec_context *c)
+{
+    std::lock_guard<std::mutex> lock(g_live_mu);
+    g_live.erase(c);
+}
+static bool ctx_alive(const hec_context *c, u64 gen)
+{
+    std::lock_guard<std::mutex> lock(g_live_mu);
+    const auto it = g_live.find(c);
+    return c && it != g_live.end() && it->second == gen;
+}
 struct hec_ciphertext {
     hec_context *ctx = nullptr;
+    u64 ctx_gen = 0;
     u64 *d = nullptr;
     std::size_t cap = 0;  // words
     std::size_t size = 0, level = 0;
@@ -69,6 +94,7 @@ struct hec_ciphertext {
 };
 struct hec_plaintext {
     hec_context *ctx = nullptr;
+    u64 ctx_gen = 0;
     u64 *d = nullptr;
     std::size_t cap = 0;
     std::size_t level = 0;
@@ -76,10 +102,12 @@ struct hec_plaintext {
 };
 struct hec_kswitch_key {
     hec_context *ctx = nullptr;
+    u64 ctx_gen = 0;
     u64 *d = nullptr;
 };
 struct hec_galois_keys {
     hec_context *ctx = nullptr;
+    u64 ctx_gen = 0;
     std::map<u32, u64 *> keys;
     std::map<u32, u64 *> negw;  // hoisted mod-up: W_elt[I] = NTT_I(sign mask of elt), built on first use
     // hoisted MAC: KW[elt, l][k][I] = sum_{J<l, J!=I} (q_J mod q_I) key_elt[J][k][I] mod q_I, built on first
@@ -1590,6 +1618,7 @@ int hec_context_create(uint64_t N, const uint64_t *mod, uint64_t K, int device, 
         // the tables went up with blocking copies on the null stream, which the non-blocking context stream does
         // not wait for: finish them before any kernel can read them
         HEC_HIP(hipDeviceSynchronize());
+        ctx->gen = ctx_register(ctx);
         *out = ctx;
     });
 }
@@ -1598,6 +1627,7 @@ int hec_context_destroy(hec_context *ctx)
 {
     return guard([&] {
         if (!ctx) return;
+        ctx_unregister(ctx);
         Ctx &c = ctx->c;
         (void)hipSetDevice(c.device);
         (void)hipStreamSynchronize(c.stream);
@@ -1729,6 +1759,7 @@ int hec_ciphertext_create(hec_context *ctx, hec_ciphertext **out)
         need(ctx && out, "null argument");
         auto *ct = new hec_ciphertext();
         ct->ctx = ctx;
+        ct->ctx_gen = ctx->gen;
         *out = ct;
     });
 }
@@ -1737,8 +1768,10 @@ int hec_ciphertext_destroy(hec_ciphertext *ct)
     return guard([&] {
         if (!ct) return;
         if (ct->d) {
-            (void)hipSetDevice(ct->ctx->c.device);
-            (void)hipStreamSynchronize(ct->ctx->c.stream);
+            if (ctx_alive(ct->ctx, ct->ctx_gen)) {
+                (void)hipSetDevice(ct->ctx->c.device);
+                (void)hipStreamSynchronize(ct->ctx->c.stream);
+            }
             (void)hipFree(ct->d);
         }
         delete ct;
@@ -1836,6 +1869,7 @@ int hec_plaintext_create(hec_context *ctx, hec_plaintext **out)
         need(ctx && out, "null argument");
         auto *p = new hec_plaintext();
         p->ctx = ctx;
+        p->ctx_gen = ctx->gen;
         *out = p;
     });
 }
@@ -1844,7 +1878,7 @@ int hec_plaintext_destroy(hec_plaintext *pt)
     return guard([&] {
         if (!pt) return;
         if (pt->d) {
-            (void)hipStreamSynchronize(pt->ctx->c.stream);
+            if (ctx_alive(pt->ctx, pt->ctx_gen)) (void)hipStreamSynchronize(pt->ctx->c.stream);
             (void)hipFree(pt->d);
         }
         delete pt;
@@ -2096,6 +2130,7 @@ int hec_kswitch_key_upload(hec_context *ctx, const uint64_t *host, hec_kswitch_k
         set_device(ctx);
         auto *k = new hec_kswitch_key();
         k->ctx = ctx;
+        k->ctx_gen = ctx->gen;
         k->d = dalloc(key_words(ctx->c));
         // on the context stream, drained before the host buffer may go (a pageable hipMemcpy on the null stream is
         // not ordered with the non-blocking context stream)
@@ -2122,6 +2157,7 @@ int hec_kswitch_key_fill_uniform(hec_context *ctx, uint64_t seed, hec_kswitch_ke
         Ctx &c = ctx->c;
         auto *k = new hec_kswitch_key();
         k->ctx = ctx;
+        k->ctx_gen = ctx->gen;
         k->d = dalloc(key_words(c));
         fill_uniform(c, k->d, (int)(c.L * 2), (int)c.K, 0, 0, seed);
         HEC_HIP(hipStreamSynchronize(c.stream));
@@ -2132,7 +2168,7 @@ int hec_kswitch_key_destroy(hec_kswitch_key *key)
 {
     return guard([&] {
         if (!key) return;
-        (void)hipStreamSynchronize(key->ctx->c.stream);
+        if (ctx_alive(key->ctx, key->ctx_gen)) (void)hipStreamSynchronize(key->ctx->c.stream);
         (void)hipFree(key->d);
         delete key;
     });
@@ -2143,6 +2179,7 @@ int hec_galois_keys_create(hec_context *ctx, hec_galois_keys **out)
         need(ctx && out, "null argument");
         auto *g = new hec_galois_keys();
         g->ctx = ctx;
+        g->ctx_gen = ctx->gen;
         *out = g;
     });
 }
@@ -2198,7 +2235,7 @@ int hec_galois_keys_destroy(hec_galois_keys *gk)
     return guard([&] {
         if (!gk) return;
         debug_key_tables_forget(gk);
-        (void)hipStreamSynchronize(gk->ctx->c.stream);
+        if (ctx_alive(gk->ctx, gk->ctx_gen)) (void)hipStreamSynchronize(gk->ctx->c.stream);
         for (auto &kv : gk->keys) (void)hipFree(kv.second);
         for (auto &kv : gk->negw) (void)hipFree(kv.second);
         for (auto &kv : gk->kw) (void)hipFree(kv.second);
@@ -2759,7 +2796,7 @@ int hec_matmul_diag_col_sharded(hec_context *ctx, const hec_ciphertext *const *d
         // this rank's size-3 partials over its trie subtrees of diagonals
         std::vector<hec_ciphertext> acc(p);
         std::vector<hec_ciphertext *> accp(p);
-        for (uint64_t i = 0; i < p; ++i) { acc[i].ctx = ctx; accp[i] = &acc[i]; }
+        for (uint64_t i = 0; i < p; ++i) { acc[i].ctx = ctx; acc[i].ctx_gen = ctx->gen; accp[i] = &acc[i]; }
         struct Free {
             std::vector<hec_ciphertext> &a;
             ~Free() { for (auto &x : a) if (x.d) (void)hipFree(x.d); }

@@ -131,6 +131,35 @@ def test_cfg3_shuffle_pass_b_keyswitch_bitexact(env15, mode, dr):
         e.ctx.set_option("nttb_shfl_dr", 0)
 
 
+def test_objects_outlive_their_context(orc, hecdna):
+    """Objects destroyed after their context (SEAL's objects hold the context by shared_ptr, and a garbage collector
+    finalising a reference cycle picks its own order; r06 suite: a Galois key set finalised after its context read
+    the freed context): each destroy frees its own device memory and touches the context only while it is alive.
+    Then a new context (possibly at the same address) works, and its objects still sync on it."""
+    import gc
+    N = 1 << 11
+    m = orc.Oracle.create_coeff_modulus(N, [50, 36, 36, 50])
+    for round_ in range(3):
+        ctx = hecdna.Context(N, m)
+        rng = np.random.default_rng(round_)
+        data = np.stack([np.stack([rng.integers(0, q, N, dtype=np.uint64) for q in m[:3]]) for _ in range(2)])
+        ct = ctx.ciphertext(data, 2.0 ** 30)
+        pt = ctx.plaintext(data[0], 2.0 ** 30)
+        rk = ctx.relin_key(seed=11)
+        o = orc.Oracle(N, m)
+        gk = ctx.galois_keys(uniform_elts=[o.elt_from_step(1)], seed=5)
+        ctx.close()
+        del ct, pt, rk, gk
+        gc.collect()
+    ctx = hecdna.Context(N, m)
+    a = np.stack([np.stack([np.random.default_rng(9).integers(0, q, N, dtype=np.uint64) for q in m])])
+    o = orc.Oracle(N, m)
+    assert np.array_equal(ctx.ntt(a)[0], np.stack([o.ntt_fwd(i, a[0, i]) for i in range(len(m))]))
+    ct = ctx.ciphertext(np.zeros((2, 3, N), np.uint64), 1.0)
+    del ct
+    gc.collect()
+
+
 def test_ntt_cfg2_golden(orc, hecdna):
     fx = json.load(open(os.path.join(GOLD, "cfg2_ntt.json")))
     N, m = fx["N"], fx["moduli"]
