@@ -56,6 +56,9 @@ int hec_create_coeff_modulus(uint64_t poly_modulus_degree, const int *bit_sizes,
  * coeff_modulus[K-1] is the special (key) prime.  device = HIP device ordinal. */
 int hec_context_create(uint64_t poly_modulus_degree, const uint64_t *coeff_modulus, uint64_t K, int device,
                        hec_context **out);
+/* Objects (ciphertexts, plaintexts, keys) may be destroyed before or after their context, in any order, as SEAL's
+ * objects holding their context by shared_ptr allow: an object destroyed after its context frees its own device
+ * memory and touches nothing else. */
 int hec_context_destroy(hec_context *ctx);
 int hec_context_set_stream(hec_context *ctx, void *hip_stream); /* NULL = context-owned stream */
 int hec_context_synchronize(hec_context *ctx);
