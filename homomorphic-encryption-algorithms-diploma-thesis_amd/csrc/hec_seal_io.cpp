@@ -20,8 +20,10 @@
 // Parity status: no SEAL-written bytes exist under /root/reference and SEAL cannot run here, so this is
 // pinned by structure tests and round trips only.
 #include <dlfcn.h>
+#include <unistd.h>
 #include <zlib.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <cstring>
 #include <mutex>
@@ -371,11 +373,19 @@ const Zlib &zlib()
 // compressed payload must not expand without limit.  kMaxCtObject covers a ciphertext object (size <= 16 polys,
 // N <= 2^17, <= 64 limbs of u64: 1 GiB of words).  A KSwitchKeys object is bounded by its caller: the device
 // loaders know N, K and L and pass the size of the key lists they accept (hec_engine.hip); the context-free
-// entry points use kMaxKeysObjectDefault (16 GiB: SEAL's default GaloisKeys take 1.67 GB at N = 2^15, L = 10 and
-// 8.84 GB at the cfg5 size N = 2^16, L = 16, 31 lists), and the *_ex forms take an explicit limit.  The output buffer doubles from a small start, so a rejected payload has
+// entry points use keys_default_limit(): kMaxKeysObjectDefault (16 GiB: SEAL's default GaloisKeys take 1.67 GB at
+// N = 2^15, L = 10 and 8.84 GB at the cfg5 size N = 2^16, L = 16, 31 lists) bounded by half the host's available
+// memory (the object is inflated in host memory), at least 1 GiB; the *_ex forms take an explicit limit.  The output buffer doubles from a small start, so a rejected payload has
 // cost at most twice the limit.
 constexpr std::size_t kMaxCtObject = (std::size_t)1 << 31;
 constexpr std::size_t kMaxKeysObjectDefault = (std::size_t)1 << 34;
+std::size_t keys_default_limit()
+{
+    const long pages = sysconf(_SC_AVPHYS_PAGES), psz = sysconf(_SC_PAGESIZE);
+    std::size_t lim = kMaxKeysObjectDefault;
+    if (pages > 0 && psz > 0) lim = std::min(lim, (std::size_t)pages * (std::size_t)psz / 2);
+    return std::max(lim, (std::size_t)1 << 30);
+}
 void check_growth(std::size_t want, std::size_t max_out)
 {
     if (want > max_out) throw std::invalid_argument("decompressed SEAL object exceeds the size limit");
@@ -640,7 +650,7 @@ void walk_kswitch_keys(const void *bytes, uint64_t nbytes, uint64_t max_bytes, u
     Reader outer{static_cast<const u8 *>(bytes), static_cast<const u8 *>(bytes) + nbytes};
     Header h;
     std::memcpy(&h, bytes, std::min<uint64_t>(nbytes, sizeof(h)));
-    InflateBudget budget(max_bytes ? (std::size_t)max_bytes : kMaxKeysObjectDefault);
+    InflateBudget budget(max_bytes ? (std::size_t)max_bytes : keys_default_limit());
     std::vector<u8> m = open_object(outer, t_inflate_budget);
     Reader r{m.data(), m.data() + m.size()};
     u64 pid[4];
@@ -667,7 +677,7 @@ void walk_kswitch_keys(const void *bytes, uint64_t nbytes, uint64_t max_bytes, u
 extern "C" {
 
 const char *hec_seal_last_error(void) { return g_io_err.c_str(); }
-uint64_t hec_seal_kswitch_keys_default_limit(void) { return kMaxKeysObjectDefault; }
+uint64_t hec_seal_kswitch_keys_default_limit(void) { return keys_default_limit(); }
 
 int hec_seal_blake2b(const void *in, uint64_t n, uint64_t outlen, void *out)
 {

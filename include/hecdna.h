@@ -298,14 +298,15 @@ int hec_seal_parms_load(const void *bytes, uint64_t nbytes, uint64_t *poly_modul
                         uint64_t cap, uint64_t *count, uint64_t *consumed);
 int hec_seal_parms_save(uint64_t poly_modulus_degree, const uint64_t *coeff_modulus, uint64_t count, int compr_mode,
                         void *out, uint64_t cap, uint64_t *written);
-/* the decompressed-size limit of the context-free key loaders below (16 GiB: SEAL's default GaloisKeys at
- * N = 2^16 with 17 primes take 8.84 GB) */
+/* the decompressed-size limit of the context-free key loaders below: 16 GiB (SEAL's default GaloisKeys at
+ * N = 2^16 with 17 primes take 8.84 GB), bounded by half the host's available memory (the object is inflated in host
+ * memory), at least 1 GiB */
 uint64_t hec_seal_kswitch_keys_default_limit(void);
 /* KSwitchKeys (RelinKeys, GaloisKeys) load of key list `index` (RelinKeys 0, GaloisKeys (galois_elt - 1) / 2)
  * in the engine's key layout u64[L][2][K][N]; *lists = the object's list count, *words = that list's words */
 int hec_seal_kswitch_keys_load(const void *bytes, uint64_t nbytes, uint64_t index, uint64_t *lists, uint64_t *out,
                                uint64_t cap_words, uint64_t *words, uint64_t *consumed);
-/* ... with at most max_bytes decompressed (0: the 16 GiB default) */
+/* ... with at most max_bytes decompressed (0: hec_seal_kswitch_keys_default_limit) */
 int hec_seal_kswitch_keys_load_ex(const void *bytes, uint64_t nbytes, uint64_t index, uint64_t max_bytes,
                                   uint64_t *lists, uint64_t *out, uint64_t cap_words, uint64_t *words,
                                   uint64_t *consumed);
@@ -316,7 +317,7 @@ int hec_seal_kswitch_keys_load_ex(const void *bytes, uint64_t nbytes, uint64_t i
 int hec_seal_kswitch_keys_foreach(const void *bytes, uint64_t nbytes,
                                   int (*visit)(void *user, uint64_t index, const uint64_t *words, uint64_t nwords),
                                   void *user, uint64_t *lists, uint64_t *consumed);
-/* ... with at most max_bytes decompressed (0: the 16 GiB default) */
+/* ... with at most max_bytes decompressed (0: hec_seal_kswitch_keys_default_limit) */
 int hec_seal_kswitch_keys_foreach_ex(const void *bytes, uint64_t nbytes, uint64_t max_bytes,
                                      int (*visit)(void *user, uint64_t index, const uint64_t *words, uint64_t nwords),
                                      void *user, uint64_t *lists, uint64_t *consumed);
