@@ -2010,14 +2010,12 @@ __device__ __forceinline__ void hmacm_body(PolyArr X1, PolyArr X0, const u64 *__
     }
 }
 
-// The round-5 digit loop on canonical u64 operands (the original key gathered at the child's output slots, 128-bit
-// lazy sums), kept for the 60-bit targets: a thread owns BT batch entries (A/B round 6: the MAC-form split MAC at one
-// batch entry per thread, which fits the kernel's register budget, measured slower at the integer targets).
-template <int BT, int CG, bool FP>
+// The round-5 digit loop for the 60-bit targets (HEC_HMAC_INT=0; the default is hmacm_body_int below): canonical u64
+// operands, the original key gathered at the child's output slots, 128-bit lazy sums, BT batch entries per thread.
+template <int BT, int CG>
 __device__ __forceinline__ void hmacm_body_u64(PolyArr X1, PolyArr X0, const u64 *__restrict__ E,
-                                           const int *__restrict__ zl, const HChildren<CG> &ch, int B, int l, int K,
-                                           int logN, const DevPrime &pr, u64 Pq, int I, int kI, u64 s0, int b0,
-                                           const u64 *__restrict__ cji, const u64 *__restrict__ psipow)
+                                           const HChildren<CG> &ch, int B, int l, int K, int logN, const DevPrime &pr,
+                                           u64 Pq, int I, int kI, u64 s0, int b0)
 {
     u64 kc[CG];       // even slot of child c's output pair
     bool sw[CG];      // output pair swapped
@@ -2031,19 +2029,10 @@ __device__ __forceinline__ void hmacm_body_u64(PolyArr X1, PolyArr X0, const u64
         const ulonglong2 w = *(const ulonglong2 *)(ch.c[q].W + ((u64)kI << logN) + kc[q]);
         const ulonglong2 m0 = *(const ulonglong2 *)(ch.c[q].KW + ((u64)I << logN) + kc[q]);
         const ulonglong2 m1 = *(const ulonglong2 *)(ch.c[q].KW + ((u64)(l + 1 + I) << logN) + kc[q]);
-        if constexpr (FP) {  // FP64 class: the exact FP64 product (a residue in [-0.53 q, 0.53 q], as bits) starts
-                             // the accumulator, instead of a 128-bit Barrett product
-            const double wx = u2d(w.x), wy = u2d(w.y);
-            wk[q][0] = (u64)__double_as_longlong(fp_mulmod(wx, u2d(m0.x), pr.qd, pr.qinv));
-            wk[q][1] = (u64)__double_as_longlong(fp_mulmod(wy, u2d(m0.y), pr.qd, pr.qinv));
-            wk[q][2] = (u64)__double_as_longlong(fp_mulmod(wx, u2d(m1.x), pr.qd, pr.qinv));
-            wk[q][3] = (u64)__double_as_longlong(fp_mulmod(wy, u2d(m1.y), pr.qd, pr.qinv));
-        } else {
-            wk[q][0] = mulmod(w.x, m0.x, pr);
-            wk[q][1] = mulmod(w.y, m0.y, pr);
-            wk[q][2] = mulmod(w.x, m1.x, pr);
-            wk[q][3] = mulmod(w.y, m1.y, pr);
-        }
+        wk[q][0] = mulmod(w.x, m0.x, pr);
+        wk[q][1] = mulmod(w.y, m0.y, pr);
+        wk[q][2] = mulmod(w.x, m1.x, pr);
+        wk[q][3] = mulmod(w.y, m1.y, pr);
         if (sw[q]) {
             u64 x = wk[q][0]; wk[q][0] = wk[q][1]; wk[q][1] = x;
             x = wk[q][2]; wk[q][2] = wk[q][3]; wk[q][3] = x;
@@ -2059,40 +2048,24 @@ __device__ __forceinline__ void hmacm_body_u64(PolyArr X1, PolyArr X0, const u64
             x0v[t] = b0 + t < B ? *(const ulonglong2 *)(X0.p + (b0 + t) * X0.sb + ((u64)I << logN) + s0)
                                 : ulonglong2{0, 0};
     }
-    double f[FP ? CG : 1][FP ? BT : 1][4];
-    U128 a[FP ? 1 : CG][FP ? 1 : BT][4];
+    U128 a[CG][BT][4];
 #pragma unroll
     for (int q = 0; q < CG; ++q)
 #pragma unroll
         for (int t = 0; t < BT; ++t)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const u64 w0 = q < ch.n ? wk[q][r] : 0;  // FP64: double bits (0 is +0.0)
-                if constexpr (FP) f[q][t][r] = __longlong_as_double((long long)w0);
-                else a[q][t][r] = U128{w0, 0};
-            }
+            for (int r = 0; r < 4; ++r) a[q][t][r] = U128{q < ch.n ? wk[q][r] : 0, 0};
     if (fold) {  // + X0 (P mod q_I) on the c0 accumulators (exact residues, as every other term)
         const u64 pm = barrett64(Pq, pr.q, pr.r1);
 #pragma unroll
         for (int t = 0; t < BT; ++t) {
-            if constexpr (FP) {
-                const double pmd = u2d(pm);
-                const double t0 = fp_mulmod(u2d(x0v[t].x), pmd, pr.qd, pr.qinv);
-                const double t1 = fp_mulmod(u2d(x0v[t].y), pmd, pr.qd, pr.qinv);
+            const u64 t0 = mulmod(x0v[t].x, pm, pr), t1 = mulmod(x0v[t].y, pm, pr);
 #pragma unroll
-                for (int q = 0; q < CG; ++q) {
-                    f[q][t][0] += t0;
-                    f[q][t][1] += t1;
-                }
-            } else {
-                const u64 t0 = mulmod(x0v[t].x, pm, pr), t1 = mulmod(x0v[t].y, pm, pr);
-#pragma unroll
-                for (int q = 0; q < CG; ++q) {
-                    a[q][t][0].lo += t0;
-                    a[q][t][0].hi += a[q][t][0].lo < t0;
-                    a[q][t][1].lo += t1;
-                    a[q][t][1].hi += a[q][t][1].lo < t1;
-                }
+            for (int q = 0; q < CG; ++q) {
+                a[q][t][0].lo += t0;
+                a[q][t][0].hi += a[q][t][0].lo < t0;
+                a[q][t][1].lo += t1;
+                a[q][t][1].hi += a[q][t][1].lo < t1;
             }
         }
     }
@@ -2116,16 +2089,10 @@ __device__ __forceinline__ void hmacm_body_u64(PolyArr X1, PolyArr X0, const u64
         if (q < ch.n) kpf[q][0] = keyw(0, q, 0), kpf[q][1] = keyw(0, q, 1);
     for (int J = 0; J < l; ++J) {
         u64 ev[BT][2];
-        double dv[FP ? BT : 1][2];  // FP64 class: the digits as doubles, converted once for all children
 #pragma unroll
         for (int t = 0; t < BT; ++t) {
-            const ulonglong2 v = pf[t];
-            ev[t][0] = v.x;
-            ev[t][1] = v.y;
-            if constexpr (FP) {
-                dv[t][0] = u2d(v.x);
-                dv[t][1] = u2d(v.y);
-            }
+            ev[t][0] = pf[t].x;
+            ev[t][1] = pf[t].y;
         }
         if (J + 1 < l) {
 #pragma unroll
@@ -2144,22 +2111,10 @@ __device__ __forceinline__ void hmacm_body_u64(PolyArr X1, PolyArr X0, const u64
             for (int t = 0; t < BT; ++t) {
                 if (b0 + t >= B) break;
                 const u64 e0 = ev[t][0], e1 = ev[t][1];
-                double d0 = 0, d1 = 0;
-                if constexpr (FP) {
-                    d0 = dv[t][0];
-                    d1 = dv[t][1];
-                }
-                if constexpr (FP) {
-                    f[q][t][0] += fp_mulmod(d0, u2d(k0.x), pr.qd, pr.qinv);
-                    f[q][t][1] += fp_mulmod(d1, u2d(k0.y), pr.qd, pr.qinv);
-                    f[q][t][2] += fp_mulmod(d0, u2d(k1.x), pr.qd, pr.qinv);
-                    f[q][t][3] += fp_mulmod(d1, u2d(k1.y), pr.qd, pr.qinv);
-                } else {
-                    mac128(a[q][t][0], e0, k0.x);
-                    mac128(a[q][t][1], e1, k0.y);
-                    mac128(a[q][t][2], e0, k1.x);
-                    mac128(a[q][t][3], e1, k1.y);
-                }
+                mac128(a[q][t][0], e0, k0.x);
+                mac128(a[q][t][1], e1, k0.y);
+                mac128(a[q][t][2], e0, k1.x);
+                mac128(a[q][t][3], e1, k1.y);
             }
         }
     }
@@ -2172,10 +2127,7 @@ __device__ __forceinline__ void hmacm_body_u64(PolyArr X1, PolyArr X0, const u64
             if (b >= B) break;
             u64 r[4];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                if constexpr (FP) r[i] = fp_canon(f[q][t][i], pr.qd, pr.qinv);
-                else r[i] = barrett128(a[q][t][i].lo, a[q][t][i].hi, pr.q, pr.r0, pr.r1);
-            }
+            for (int i = 0; i < 4; ++i) r[i] = barrett128(a[q][t][i].lo, a[q][t][i].hi, pr.q, pr.r0, pr.r1);
             u64 *o0 = ch.c[q].ACC + (((u64)((b * 2 + 0) * (l + 1) + I)) << logN) + kc[q];
             u64 *o1 = ch.c[q].ACC + (((u64)((b * 2 + 1) * (l + 1) + I)) << logN) + kc[q];
             *(ulonglong2 *)o0 = sw[q] ? ulonglong2{r[1], r[0]} : ulonglong2{r[0], r[1]};
@@ -2411,7 +2363,7 @@ __global__ void __launch_bounds__(256, MINW)  // MINW waves per SIMD: 3 -> <= 16
     else if (int_mform)
         hmacm_body_int<BTI, CG>(X1, X0, E, ch, B, l, K, logN, pr, Pq, I, kI, s0, bg * BTI);
     else
-        hmacm_body_u64<BTI, CG, false>(X1, X0, E, zl, ch, B, l, K, logN, pr, Pq, I, kI, s0, bg * BTI, cji, psipow);
+        hmacm_body_u64<BTI, CG>(X1, X0, E, ch, B, l, K, logN, pr, Pq, I, kI, s0, bg * BTI);
 }
 
 // The zero corrections of the sibling-fused hoisted MAC (§4.6 of DESIGN.md), as their own pass over the children's
