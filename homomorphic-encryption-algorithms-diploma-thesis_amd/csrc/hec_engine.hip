@@ -401,8 +401,30 @@ std::size_t ks_words(const Ctx &c, std::size_t B, std::size_t l)
 
 // key-switch mod-down (SEAL switch_key_inplace step 4): the P-limb INTT's first pass, the fan-out that
 // finishes it and forms the rounding limbs, and divide_round's pass B (OUT = IN + (ACC_i - r) P^-1)
+// single-pass form (c.moddown1, N = 2^15): the P limbs' whole INTT in place, then k_moddown1 forms each data limb's
+// rounding limb, transforms it and divides-and-rounds in one kernel (no Z round trip, no fan-out, no pass B)
+static bool moddown_single(Ctx &c, u64 *ACC, PolyArr IN, int in_nk, const PolyArr *OUT, const u32 *elts, int ng, int B,
+                           int l)
+{
+    if (!c.moddown1 || c.logN != 15) return false;
+    const u64 N = c.N, sacc = (u64)B * 2 * (l + 1) * N;
+    ProfScope ps(c, "ks_moddown");
+    const int pP[1] = {(int)c.K - 1};
+    {  // both passes of the P limbs' INTT: read + write 2 B ng limbs per pass
+        ProfScope k(c, "k:k_ntt/moddown_intt", 8.0 * B * ng, 2);
+        ntt_strided(c, true, ACC + l * N, (l + 1) * N, ACC + l * N, (l + 1) * N, 1, pP, 2 * B * ng, 1, 3);
+    }
+    for (int q = 0; q < ng; ++q) {  // P limb (2B, once per (b, k)), ACC (2Bl), IN (in_nk B l), OUT (2Bl)
+        ProfScope k(c, "k:k_moddown1/moddown", (2.0 + (4.0 + in_nk) * l) * B, 2);  // one launch per class
+        moddown1(c, ACC + q * sacc + l * N, 2 * (l + 1) * N, (l + 1) * N, PolyArr{ACC + q * sacc, 2 * (l + 1) * N, (l + 1) * N},
+                 IN, in_nk, OUT[q], B, 2, l, (int)c.K - 1, elts[q]);
+    }
+    return true;
+}
+
 void moddown(Ctx &c, u64 *ACC, u64 *Z, PolyArr IN, int in_nk, PolyArr OUT, int B, int l, u32 elt)
 {
+    if (moddown_single(c, ACC, IN, in_nk, &OUT, &elt, 1, B, l)) return;
     const u64 N = c.N;
     const bool fan = c.fan_out;
     ProfScope ps(c, "ks_moddown");
@@ -429,6 +451,7 @@ void moddown_group(Ctx &c, u64 *ACC, u64 *Z, PolyArr IN, int in_nk, const PolyAr
                    int B, int l)
 {
     const u64 N = c.N, sacc = (u64)B * 2 * (l + 1) * N, sz = (u64)B * 2 * l * N;
+    if (moddown_single(c, ACC, IN, in_nk, OUT, elts, ng, B, l)) return;
     if (!c.fan_out || ng == 1) {
         for (int q = 0; q < ng; ++q) moddown(c, ACC + q * sacc, Z, IN, in_nk, OUT[q], B, l, elts[q]);
         return;
@@ -1470,6 +1493,7 @@ int hec_context_create(uint64_t N, const uint64_t *mod, uint64_t K, int device, 
         if (const char *f = std::getenv("HEC_NTTB_SHFL")) c.nttb_shfl = std::min(2, std::max(0, std::atoi(f)));
         if (const char *f = std::getenv("HEC_NTTB_SHFL_DR")) c.nttb_shfl_dr = std::atoi(f) != 0;
         if (const char *f = std::getenv("HEC_HMAC_INT")) c.hmac_int = std::atoi(f) != 0;
+        if (const char *f = std::getenv("HEC_MODDOWN1")) c.moddown1 = std::atoi(f) != 0;
         if (const char *f = std::getenv("HEC_BMAC_SPLIT")) c.bmac_split = f[0] != '0';
         c.N = N;
         c.logN = __builtin_ctzll(N);
@@ -1697,6 +1721,7 @@ int hec_context_set_option(hec_context *ctx, const char *name, int64_t value)
             else if (n == "nttb_shfl") c.nttb_shfl = in(0, 2);
             else if (n == "nttb_shfl_dr") c.nttb_shfl_dr = in(0, 1);
             else if (n == "hmac_int") c.hmac_int = in(0, 1);
+            else if (n == "moddown1") c.moddown1 = in(0, 1);
             else if (n == "bmac_split") c.bmac_split = value != 0;
             else if (n == "hoist") c.hoist = value != 0;
             else if (n == "hoist_min") c.hoist_min_children = (int)std::max<int64_t>(1, value);

@@ -70,6 +70,7 @@ struct Ctx {
     bool bmac_split = true;        // HEC_BMAC_SPLIT=0: k_bmac's integer-target pass B on plain Shoup butterflies
     int nttb_shfl = 0;             // HEC_NTTB_SHFL=1: the forward NTT's pass B at N = 2^15 as k_nttb_shfl (exchanges
                                    // between lanes of a wavefront, no LDS tile), round 6
+    int moddown1 = 0;              // HEC_MODDOWN1=1: the single-pass mod-down (hec_moddown1.hip, N = 2^15)
     int hmac_int = 1;              // HEC_HMAC_INT=0: k_hmacm's 60-bit targets on the round-5 loop (gathered keys)
     int nttb_shfl_dr = 0;          // HEC_NTTB_SHFL_DR=1: the same for the divide-and-round pass B (A/B only)
     int split_bfly = 4;            // HEC_SPLIT_BFLY: 0 plain Shoup in the fan-out kernels, 1 split-input Shoup in
@@ -207,6 +208,10 @@ void hoisted_mac_group(Ctx &c, PolyArr X1, PolyArr X0, const u64 *E, const int *
                        int B, int l);
 int hoisted_group(const Ctx &c);  // children per hoisted_mac_multi call for c.hmac_cfg
 void fan_divide_round(Ctx &c, const u64 *Y, u64 ysb, u64 ysk, u64 *Z, int B, int nk, int nl, int last_idx);
+// the single-pass mod-down (hec_moddown1.hip): Y the coefficient-form special-prime limbs, X the ACC data limbs;
+// false when it does not apply (N != 2^15)
+bool moddown1(Ctx &c, const u64 *Y, u64 ysb, u64 ysk, PolyArr X, PolyArr IN, int in_nk, PolyArr OUT, int B, int nk,
+              int nl, int last_idx, u32 elt);
 void galois_permute(Ctx &c, PolyArr in, PolyArr out, int B, int nk, int nl, u32 elt);
 void tensor_acc(Ctx &c, PolyArr R, const u64 *A, u64 a_sk, PolyArr ACC, int B, int l, bool assign);
 // deferred tensor products: ACC[b] (=|+=) sum_t R_t[b] (x) A_t, T <= TB_MAX rotated inputs

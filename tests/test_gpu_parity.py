@@ -131,6 +131,27 @@ def test_cfg3_shuffle_pass_b_keyswitch_bitexact(env15, mode, dr):
         e.ctx.set_option("nttb_shfl_dr", 0)
 
 
+def test_cfg3_single_pass_moddown_bitexact(env15):
+    """cfg3 parameters with the single-pass mod-down (hec_context_set_option "moddown1"; k_moddown1: the rounding limb,
+    its whole forward NTT and the divide-and-round in one kernel per data limb, FP64 and 60-bit classes): rotations
+    (the per-rotation path, IN read through the permutation) and a hoisted matvec (sibling-group mod-downs) equal the
+    oracle's bits."""
+    e = env15
+    e.ctx.set_option("moddown1", 1)
+    try:
+        a = e.enc(seed=7)
+        for steps in (1, 3, 4095):
+            e.same(e.ctx.rotate_vector(e.up(a), steps, e.gk), e.o.rotate(a, steps, e.gk_h))
+        A = [e.enc(seed=70 + j) for j in range(6)]
+        X = [e.enc(seed=95 + i) for i in range(3)]
+        exp = e.o.matmul_diag_col(A, X, e.rk_h, e.gk_h, nthreads=8)
+        got = e.ctx.matmul_diag_col([e.up(x) for x in A], [e.up(x) for x in X], e.rk, e.gk)
+        for g, c in zip(got, exp):
+            e.same(g, c)
+    finally:
+        e.ctx.set_option("moddown1", 0)
+
+
 def test_objects_outlive_their_context(orc, hecdna):
     """Objects destroyed after their context (SEAL's objects hold the context by shared_ptr, and a garbage collector
     finalising a reference cycle picks its own order; r06 suite: a Galois key set finalised after its context read
