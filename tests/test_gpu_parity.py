@@ -126,6 +126,8 @@ def test_cfg3_shuffle_pass_b_keyswitch_bitexact(env15, mode, dr):
         got = e.ctx.matmul_diag_col([e.up(x) for x in A], [e.up(x) for x in X], e.rk, e.gk)
         for g, c in zip(got, exp):
             e.same(g, c)
+        low = e.enc(seed=9, level=4)  # a lower level: fewer digits and targets
+        e.same(e.ctx.rotate_vector(e.up(low), 3, e.gk), e.o.rotate(low, 3, e.gk_h))
     finally:
         e.ctx.set_option("nttb_shfl", 0)
         e.ctx.set_option("nttb_shfl_dr", 0)
@@ -148,6 +150,10 @@ def test_cfg3_single_pass_moddown_bitexact(env15):
         got = e.ctx.matmul_diag_col([e.up(x) for x in A], [e.up(x) for x in X], e.rk, e.gk)
         for g, c in zip(got, exp):
             e.same(g, c)
+        # a lower level (l = 4: fewer data limbs, the same special prime)
+        low = e.enc(seed=8, level=4)
+        for steps in (1, 5):
+            e.same(e.ctx.rotate_vector(e.up(low), steps, e.gk), e.o.rotate(low, steps, e.gk_h))
     finally:
         e.ctx.set_option("moddown1", 0)
 
