@@ -458,7 +458,16 @@ __device__ __forceinline__ void ntt_pass_body(u64 *lds, const Bound &bio, const 
                                               int logN)
 {
     constexpr int P = 1 << LOGP, TPS = P / 16, THREADS = NSEG * TPS;
-    constexpr int LD = PASS_A ? (NSEG + 1) : (P + 1);
+    // PAIR: pass B moves word pairs (x, x + 1) of a chunk per lane: 16-B loads and stores (8 per thread instead
+    // of 16 8-B ones; the IO's load2 / pre2 / store2)
+    constexpr bool PAIR = !PASS_A && HasPair<Bound>::value;
+    // SWZ (the pair path, round 6): unpadded chunk rows with word x of segment sg at x ^ sg.  The padded rows (P + 1
+    // words) put an odd row's pairs at 8-B-aligned addresses, so each pair moved as two strided 8-B LDS accesses:
+    // 2.67 bank-conflict cycles per LDS instruction in the mod-up pass B (profiles/r06t_sq_final_by_instance_B128.json).
+    // Swizzled, a pair is one aligned 16-B slot (its two words swapped in odd rows), and the rounds' accesses (16
+    // segments at one x) still fall on 16 distinct bank pairs.
+    constexpr bool SWZ = PAIR && NSEG <= P;
+    constexpr int LD = PASS_A ? (NSEG + 1) : (SWZ ? P : P + 1);
     constexpr bool FIRST = !FINAL;  // forward: A then B; inverse: B then A
     (void)TPS;
     const u64 q = pr.q, two_q = 2 * q;
@@ -467,9 +476,6 @@ __device__ __forceinline__ void ntt_pass_body(u64 *lds, const Bound &bio, const 
     const ulonglong2 *tw = (PASS_A ? tt.a : tt.b) + ((u64)bio.prime << logN);
     const double *twf = (PASS_A ? tt.fa : tt.fb) + ((u64)bio.prime << logN);
 
-    // PAIR: pass B moves word pairs (x, x + 1) of a chunk per lane: 16-B loads and stores (8 per thread instead
-    // of 16 8-B ones; the IO's load2 / pre2 / store2)
-    constexpr bool PAIR = !PASS_A && HasPair<Bound>::value;
     constexpr int PB2 = P / 2;
     if constexpr (!PAIR) {
         // every tile load issued before the first LDS store (round 6, VERDICT r05 item 5: with a load and its LDS
@@ -507,8 +513,13 @@ __device__ __forceinline__ void ntt_pass_body(u64 *lds, const Bound &bio, const 
                 a = (u64)__double_as_longlong(u2d(a));
                 b = (u64)__double_as_longlong(u2d(b));
             }
-            lds[sg * LD + x] = a;
-            lds[sg * LD + x + 1] = b;
+            if constexpr (SWZ)
+                *reinterpret_cast<ulonglong2 *>(lds + sg * LD + (x ^ (sg & ~1))) = (sg & 1) ? ulonglong2{b, a}
+                                                                                        : ulonglong2{a, b};
+            else {
+                lds[sg * LD + x] = a;
+                lds[sg * LD + x + 1] = b;
+            }
         }
     }
     __syncthreads();
@@ -553,7 +564,7 @@ __device__ __forceinline__ void ntt_pass_body(u64 *lds, const Bound &bio, const 
             }
         }
     }
-    auto addr = [sg](int x) { return PASS_A ? x * LD + sg : sg * LD + x; };
+    auto addr = [sg](int x) { return PASS_A ? x * LD + sg : sg * LD + (SWZ ? (x ^ sg) : x); };
     if constexpr (!INV) {
         if constexpr (TW0) ntt_round_pre<LOGP, 0, 4, false, FP>(lds, addr, ts, gt0, pr);
         else ntt_round<LOGP, 0, false, FP>(lds, addr, ts, twidx, tw, twf, pr);
@@ -571,7 +582,15 @@ __device__ __forceinline__ void ntt_pass_body(u64 *lds, const Bound &bio, const 
         for (int it = 0; it < ITS / 2; ++it) {
             const int li = threadIdx.x + it * THREADS;
             const int s2 = li / PB2, x = 2 * (li % PB2);
-            u64 a = lds[s2 * LD + x], b = lds[s2 * LD + x + 1];
+            u64 a, b;
+            if constexpr (SWZ) {
+                const ulonglong2 w = *reinterpret_cast<const ulonglong2 *>(lds + s2 * LD + (x ^ (s2 & ~1)));
+                a = (s2 & 1) ? w.y : w.x;
+                b = (s2 & 1) ? w.x : w.y;
+            } else {
+                a = lds[s2 * LD + x];
+                b = lds[s2 * LD + x + 1];
+            }
             const u64 g = ((u64)(seg0 + s2) << LOGP) + x;
             if constexpr (FINAL) {
                 if constexpr (FP) {
@@ -947,7 +966,7 @@ __global__ void __launch_bounds__(NSEG *(1 << LOGP) / 16)
     static_assert(LOGP >= 5 && LOGP <= 8, "two rounds of 4 stages");
     constexpr int WORDS = !RD ? (PASS_A ? (1 << LOGP) * (NSEG + 1) : NSEG * ((1 << LOGP) + 1))
                               : (PASS_A ? (1 << LOGP) * (NSEG + 1) : NSEG * nttb_ld(LOGP));
-    __shared__ u64 lds[WORDS];
+    __shared__ __attribute__((aligned(16))) u64 lds[WORDS];  // 16-B pair accesses (SWZ)
     const auto bio = io.bind(blockIdx.y);
     if (!bio.valid) return;  // uniform per block
     const DevPrime pr = primes[bio.prime];
