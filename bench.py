@@ -70,6 +70,29 @@ def pmc_traffic(kernel, B, logn, level, n, variant="ctct"):
     return p["traffic_bytes_per_dispatch"]
 
 
+def pmc_step_traffic(kernels, B, logn, level, n, variant="ctct"):
+    """Whole-step HBM traffic per matvec from the committed PMC passes (the files pmc_traffic reads): the newest
+    round whose set covers every kernel of the step on this configuration, summed traffic_bytes_per_step / B
+    (VERDICT r05's whole-step figure: bytes actually moved, against SURVEY 8(d)'s algorithmic bytes); else None."""
+    sfx = "" if variant == "ctct" else f"_{variant}"
+    for tag in ("r06", "r05", "r04", "r03", "r02", "r01"):
+        per = {}
+        for k in kernels:
+            path = os.path.join(ROOT, "profiles", f"{tag}_pmc_{k}_B{B}{sfx}.json")
+            if not os.path.exists(path):
+                break
+            p = json.load(open(path))
+            if (p["batch"], p["logN"], p["level"], p.get("n"), p.get("variant", "ctct")) != (B, logn, level, n, variant):
+                break
+            per[k] = p["traffic_bytes_per_step"] / B / 1e9
+        else:
+            if per:
+                return {"GB_per_matvec": round(sum(per.values()), 1), "by_kernel": {k: round(v, 2) for k, v in per.items()},
+                        "source": f"profiles/{tag}_pmc_<kernel>_B{B}{sfx}.json (one PMC step each, FETCH_SIZE x 2 + "
+                                  f"WRITE_SIZE; the step's setup dispatches included)"}
+    return None
+
+
 def cgroup_cpu_quota():
     """CPUs granted by the cgroup's CPU quota (cgroup v2 cpu.max, else v1 cfs_quota/period), or None."""
     try:
@@ -743,6 +766,8 @@ def main():
             "kernels_one_step": kernels,
             "cpu_baseline": cpu,
             "whole_step_algorithmic_GBps": round(algo_mv * total / dt / 1e9, 2),
+            "whole_step_pmc_traffic": (pmc_step_traffic(list(kernels), args.batch, args.logn, L, args.n, args.variant)
+                                       if kernels else None),
             "hbm": hbm,
             "breakdown_ms_one_step": breakdown,
             "profile_schedule": (None if args.no_profile else

@@ -55,6 +55,18 @@ def test_gpus_n_launches_n_ranks_one_line(gpus):
     assert r["n_gpus"] == gpus and r["rccl_world"] == gpus and r["dry_run"] and r["steps"] == 2
 
 
+def test_whole_step_pmc_traffic(bench):
+    """The line's whole-step PMC figure: the committed round-6 passes at the bench shape sum to the per-kernel traffic
+    per matvec (399 GB); a kernel without a pass on that shape, or another shape, gives None rather than
+    a partial sum."""
+    ks = ["k_bmac", "k_fan2", "k_fan2j", "k_hmacm", "k_ntt", "k_tensor_multi2"]
+    t = bench.pmc_step_traffic(ks, 128, 15, 10, 4096)
+    assert t is not None and 390 < t["GB_per_matvec"] < 410 and set(t["by_kernel"]) == set(ks)
+    assert t["source"].startswith("profiles/r06_pmc_")
+    assert bench.pmc_step_traffic(ks + ["k_moddown1"], 128, 15, 10, 4096) is None
+    assert bench.pmc_step_traffic(ks, 128, 15, 10, 2048) is None
+
+
 def test_replicated_seeds_do_not_depend_on_rank(bench):
     """The keys and the matrix diagonals are the replicated state of every rank: their seeds must be the
     same on every rank, or a sharded step sums partials computed under different keys.  Throughput mode gives each rank
