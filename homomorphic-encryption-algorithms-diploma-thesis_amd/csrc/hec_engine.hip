@@ -1494,6 +1494,7 @@ int hec_context_create(uint64_t N, const uint64_t *mod, uint64_t K, int device, 
         if (const char *f = std::getenv("HEC_NTTB_SHFL_DR")) c.nttb_shfl_dr = std::atoi(f) != 0;
         if (const char *f = std::getenv("HEC_HMAC_INT")) c.hmac_int = std::atoi(f) != 0;
         if (const char *f = std::getenv("HEC_MODDOWN1")) c.moddown1 = std::atoi(f) != 0;
+        if (const char *f = std::getenv("HEC_NT_E")) c.nt_e = std::atoi(f) != 0;
         if (const char *f = std::getenv("HEC_BMAC_SPLIT")) c.bmac_split = f[0] != '0';
         c.N = N;
         c.logN = __builtin_ctzll(N);
@@ -1722,6 +1723,7 @@ int hec_context_set_option(hec_context *ctx, const char *name, int64_t value)
             else if (n == "nttb_shfl_dr") c.nttb_shfl_dr = in(0, 1);
             else if (n == "hmac_int") c.hmac_int = in(0, 1);
             else if (n == "moddown1") c.moddown1 = in(0, 1);
+            else if (n == "nt_e") c.nt_e = in(0, 1);
             else if (n == "bmac_split") c.bmac_split = value != 0;
             else if (n == "hoist") c.hoist = value != 0;
             else if (n == "hoist_min") c.hoist_min_children = (int)std::max<int64_t>(1, value);

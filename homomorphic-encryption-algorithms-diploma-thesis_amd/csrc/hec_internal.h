@@ -70,6 +70,7 @@ struct Ctx {
     bool bmac_split = true;        // HEC_BMAC_SPLIT=0: k_bmac's integer-target pass B on plain Shoup butterflies
     int nttb_shfl = 0;             // HEC_NTTB_SHFL=1: the forward NTT's pass B at N = 2^15 as k_nttb_shfl (exchanges
                                    // between lanes of a wavefront, no LDS tile), round 6
+    int nt_e = 1;                  // the hoisted digits E stored non-temporally (round 6, +0.7 %; HEC_NT_E=0: cached)
     int moddown1 = 0;              // HEC_MODDOWN1=1: the single-pass mod-down (hec_moddown1.hip, N = 2^15)
     int hmac_int = 1;              // HEC_HMAC_INT=0: k_hmacm's 60-bit targets on the round-5 loop (gathered keys)
     int nttb_shfl_dr = 0;          // HEC_NTTB_SHFL_DR=1: the same for the divide-and-round pass B (A/B only)

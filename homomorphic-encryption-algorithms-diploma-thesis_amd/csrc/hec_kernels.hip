@@ -27,6 +27,37 @@ __device__ __forceinline__ ulonglong2 ld2(const u64 *p, u64 g)
     const u64x2 w = *reinterpret_cast<const u64x2 *>(p + g);
     return make_ulonglong2(w.x, w.y);
 }
+// Non-temporal stores for the step's large streaming intermediates (round 6): each is written once and read by a
+// later kernel, and none fits the caches (GB per launch), so keeping their lines only delays write-back into the next
+// kernel's time.  Bits of HEC_NT_MASK: 1 the fan-outs' target tiles (Z, mod-up pass-A tiles), 2 the divide-and-round
+// output, 4 the hoisted MAC's accumulators; the hoisted digits E are Ctx::nt_e (ModUpIO_BT).
+#ifndef HEC_NT_MASK
+#define HEC_NT_MASK 0
+#endif
+constexpr int kNtMask = HEC_NT_MASK;
+template <int BIT>
+__device__ __forceinline__ void st1m(u64 *p, u64 v)
+{
+    if constexpr ((kNtMask & BIT) != 0) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+template <int BIT>
+__device__ __forceinline__ void st2m(u64 *p, ulonglong2 v)
+{
+    u64x2 w;
+    w.x = v.x;
+    w.y = v.y;
+    if constexpr ((kNtMask & BIT) != 0) __builtin_nontemporal_store(w, reinterpret_cast<u64x2 *>(p));
+    else *reinterpret_cast<u64x2 *>(p) = w;
+}
+// a non-temporal 16-B store (the nt cache policy: the line is not kept for reuse)
+__device__ __forceinline__ void st2_nt(u64 *p, u64 g, u64 a, u64 b)
+{
+    u64x2 w;
+    w.x = a;
+    w.y = b;
+    __builtin_nontemporal_store(w, reinterpret_cast<u64x2 *>(p + g));
+}
 __device__ __forceinline__ void st2(u64 *p, u64 g, u64 a, u64 b)
 {
     u64x2 w;
@@ -119,7 +150,9 @@ struct ModUpIO_A {  // load digit J (coefficient form, canonical mod q_J) reduce
         return Bound{D + ((u64)(b * m.l + J) << m.logN), E + m.eoff(b, I, J), primes[p].q, primes[p].r1, p, I != J};
     }
 };
-struct ModUpIO_B {
+// NT: the digits stored non-temporally (HEC_NT_E, A/B)
+template <bool NT>
+struct ModUpIO_BT {
     ModUpMap m;
     u64 *E;
     int mform = 0;  // 1: the final store writes the MAC form k_hmacm reads (mform(), round 6)
@@ -133,10 +166,18 @@ struct ModUpIO_B {
         struct Pre {};
         __device__ Pre pre(u64) const { return {}; }
         __device__ u64 load(u64 g) const { return p[g]; }
-        __device__ void store(u64 g, u64 v, Pre) const { p[g] = v; }
+        __device__ void store(u64 g, u64 v, Pre) const
+        {
+            if constexpr (NT) __builtin_nontemporal_store(v, p + g);
+            else p[g] = v;
+        }
         __device__ ulonglong2 load2(u64 g) const { return ld2(p, g); }
         __device__ void pre2(u64, Pre &, Pre &) const {}
-        __device__ void store2(u64 g, u64 a, u64 b, Pre, Pre) const { st2(p, g, a, b); }
+        __device__ void store2(u64 g, u64 a, u64 b, Pre, Pre) const
+        {
+            if constexpr (NT) st2_nt(p, g, a, b);
+            else st2(p, g, a, b);
+        }
     };
     __device__ Bound bind(int job) const
     {
@@ -145,6 +186,8 @@ struct ModUpIO_B {
         return Bound{E + m.eoff(b, I, J), I == m.l ? m.kP : I, I != J, mform != 0};
     }
 };
+
+using ModUpIO_B = ModUpIO_BT<false>;
 
 // Divide-and-round by a prime `last` (key-switch mod-down by P, or rescale by q_{l-1}):
 // pass A loads y (coefficient form of the last limb, canonical mod last) and emits
@@ -239,7 +282,7 @@ struct DivRoundIOB {
         {
             u64 r = shoup(p.x + q - v, w, wq, q);
             if (HAS_IN && in) r = addmod(r, p.in, q);
-            out[g] = r;
+            st1m<2>(out + g, r);
         }
         // v: the FP64 NTT output before canonicalisation (|v| < 10 q): (x - v) P^-1 (+ in) with one exact
         // fp_mulmod (|x - v| < 11 q) and one canonicalisation, instead of Shoup on u64 plus fp_canon
@@ -247,7 +290,7 @@ struct DivRoundIOB {
         {
             double r = fp_mulmod(u2d(p.x) - v, u2d(w), pr.qd, pr.qinv);
             if (HAS_IN && in) r += u2d(p.in);
-            out[g] = fp_canon(r, pr.qd, pr.qinv);
+            st1m<2>(out + g, fp_canon(r, pr.qd, pr.qinv));
         }
     };
     __device__ Bound bind(int job) const
@@ -994,7 +1037,8 @@ static void run_ntt2(Ctx &c, int njobs, const IO1 &first, const IO2 &second, int
             // mod-up digits; the divide-and-round post-op keeps the LDS pass (its 16 outputs and post-op operands
             // in registers at once would cost it a wave per SIMD)
             constexpr bool kDR = std::is_same_v<IO2, DivRoundIOB<false>> || std::is_same_v<IO2, DivRoundIOB<true>>;
-            if constexpr (LOGC == 7 && (std::is_same_v<IO2, StridedIO> || std::is_same_v<IO2, ModUpIO_B> || kDR)) {
+            if constexpr (LOGC == 7 && (std::is_same_v<IO2, StridedIO> || std::is_same_v<IO2, ModUpIO_B> ||
+                                        std::is_same_v<IO2, ModUpIO_BT<true>> || kDR)) {
                 if (c.nttb_shfl && (!kDR || c.nttb_shfl_dr)) {
                     if (c.nttb_shfl == 2)
                         k_nttb_shfl<IO2, true><<<dim3(R / 32, njobs), 256, 0, c.stream>>>(second, fwd, c.primes, c.logN);
@@ -1054,8 +1098,13 @@ void ks_modup(Ctx &c, const u64 *D, u64 *E, int B, int l, int stages, bool mform
 {
     ModUpMap m{l, c.logN, (int)c.K - 1};
     ModUpIO_A a{m, D, E, c.primes};
-    ModUpIO_B b{m, E, mform ? 1 : 0};
-    ntt_dispatch<false>(c, B * l * l, a, b, stages);
+    if (c.nt_e) {
+        ModUpIO_BT<true> b{m, E, mform ? 1 : 0};
+        ntt_dispatch<false>(c, B * l * l, a, b, stages);
+    } else {
+        ModUpIO_B b{m, E, mform ? 1 : 0};
+        ntt_dispatch<false>(c, B * l * l, a, b, stages);
+    }
 }
 
 void divide_round(Ctx &c, const u64 *Y, u64 ysb, u64 ysk, PolyArr X, PolyArr IN, int in_nk, PolyArr OUT, int B,
@@ -1406,7 +1455,7 @@ __global__ void __launch_bounds__(NSEG *(1 << LOGP) / 16)
         else ntt_round_r<LOGP, 4, LOGP, false, false>(v, ts, tw, pt);
         // (16-B stores and loads through lane-pair trades measured slower: 2,613 vs 2,580 ms per step, round 4)
 #pragma unroll
-        for (int k = 0; k < 16; ++k) tgt.out[gblock(k)] = v[k];
+        for (int k = 0; k < 16; ++k) st1m<1>(tgt.out + gblock(k), v[k]);
     }
 }
 
@@ -1553,7 +1602,7 @@ __global__ void __launch_bounds__(NSEG *(1 << LOGP) / 16, 2)  // 2 waves per SIM
             }
             // (16-B stores and loads through lane-pair trades measured slower: 2,613 vs 2,580 ms per step, round 4)
 #pragma unroll
-            for (int k = 0; k < 16; ++k) tgt.out[gblock(k)] = v[k];
+            for (int k = 0; k < 16; ++k) st1m<1>(tgt.out + gblock(k), v[k]);
         }
         // a target slice [t0, t1) without a valid target for this job (gridDim.z > 1) loaded nothing above: the next
         // job's source still has to replace d (block-uniform, never taken with one target group)
@@ -2023,8 +2072,8 @@ __device__ __forceinline__ void hmacm_body(PolyArr X1, PolyArr X0, const u64 *__
             for (int i = 0; i < 4; ++i) r[i] = fp_canon(f[q][t][i], pr.qd, pr.qinv);
             u64 *o0 = ch.c[q].ACC + (((u64)((b * 2 + 0) * (l + 1) + I)) << logN) + kc[q];
             u64 *o1 = ch.c[q].ACC + (((u64)((b * 2 + 1) * (l + 1) + I)) << logN) + kc[q];
-            *(ulonglong2 *)o0 = sw[q] ? ulonglong2{r[1], r[0]} : ulonglong2{r[0], r[1]};
-            *(ulonglong2 *)o1 = sw[q] ? ulonglong2{r[3], r[2]} : ulonglong2{r[2], r[3]};
+            st2m<4>(o0, sw[q] ? ulonglong2{r[1], r[0]} : ulonglong2{r[0], r[1]});
+            st2m<4>(o1, sw[q] ? ulonglong2{r[3], r[2]} : ulonglong2{r[2], r[3]});
         }
     }
 }
@@ -2149,8 +2198,8 @@ __device__ __forceinline__ void hmacm_body_u64(PolyArr X1, PolyArr X0, const u64
             for (int i = 0; i < 4; ++i) r[i] = barrett128(a[q][t][i].lo, a[q][t][i].hi, pr.q, pr.r0, pr.r1);
             u64 *o0 = ch.c[q].ACC + (((u64)((b * 2 + 0) * (l + 1) + I)) << logN) + kc[q];
             u64 *o1 = ch.c[q].ACC + (((u64)((b * 2 + 1) * (l + 1) + I)) << logN) + kc[q];
-            *(ulonglong2 *)o0 = sw[q] ? ulonglong2{r[1], r[0]} : ulonglong2{r[0], r[1]};
-            *(ulonglong2 *)o1 = sw[q] ? ulonglong2{r[3], r[2]} : ulonglong2{r[2], r[3]};
+            st2m<4>(o0, sw[q] ? ulonglong2{r[1], r[0]} : ulonglong2{r[0], r[1]});
+            st2m<4>(o1, sw[q] ? ulonglong2{r[3], r[2]} : ulonglong2{r[2], r[3]});
         }
     }
 }
@@ -2288,8 +2337,8 @@ __device__ __forceinline__ void hmacm_body_int(PolyArr X1, PolyArr X0, const u64
             for (int i = 0; i < 4; ++i) r[i] = barrett128(a[q][t][i].lo, a[q][t][i].hi, pr.q, pr.r0, pr.r1);
             u64 *o0 = ch.c[q].ACC + (((u64)((b * 2 + 0) * (l + 1) + I)) << logN) + kc[q];
             u64 *o1 = ch.c[q].ACC + (((u64)((b * 2 + 1) * (l + 1) + I)) << logN) + kc[q];
-            *(ulonglong2 *)o0 = sw[q] ? ulonglong2{r[1], r[0]} : ulonglong2{r[0], r[1]};
-            *(ulonglong2 *)o1 = sw[q] ? ulonglong2{r[3], r[2]} : ulonglong2{r[2], r[3]};
+            st2m<4>(o0, sw[q] ? ulonglong2{r[1], r[0]} : ulonglong2{r[0], r[1]});
+            st2m<4>(o1, sw[q] ? ulonglong2{r[3], r[2]} : ulonglong2{r[2], r[3]});
         }
     }
 }

@@ -68,14 +68,15 @@ int hec_context_synchronize(hec_context *ctx);
  * "split_bfly", "bmac_split", "nttb_shfl" (the forward pass B at 128 points with its exchanges as DPP lane moves
  * instead of LDS: 1, 16 outputs per lane; 2, swapped back for coalesced stores), "nttb_shfl_dr" (the same for the
  * divide-and-round pass B), "moddown1" (the single-pass mod-down at N = 2^15), "hmac_int" (0: the 60-bit hoisted MAC
- * targets on the round-5 loop), "kernel_memops" (0: workspace fills and device copies through the runtime's
+ * targets on the round-5 loop), "nt_e" (0: the hoisted digits stored with the default cache policy instead of
+ * non-temporally), "kernel_memops" (0: workspace fills and device copies through the runtime's
  * hipMemsetAsync / hipMemcpyAsync instead of engine kernels; A/B only), and three debug switches:
  * "poison" (every workspace carve and fresh output buffer is filled with 0xFF bytes before use, so a read of
  * memory the call never wrote becomes a deterministic wrong result), "lane_serial" (batch lanes run one after
  * another) and "debug_lanes" (per-call zero-list and key-table reports on stderr).  Every schedule is
  * bit-identical.  Applies to the context and its batch lanes; HEC_EINVAL for an unknown name, and for a value
  * outside an enumerated knob's range ("split_bfly" 0..4, "hmac" 0..2, "hmac_odd3" 0..1, "hoist_scan" 0..1,
- * "nttb_shfl" 0..2, "nttb_shfl_dr" 0..1, "moddown1" 0..1, "hmac_int" 0..1). */
+ * "nttb_shfl" 0..2, "nttb_shfl_dr" 0..1, "moddown1" 0..1, "hmac_int" 0..1, "nt_e" 0..1). */
 int hec_context_set_option(hec_context *ctx, const char *name, int64_t value);
 uint64_t hec_context_poly_degree(const hec_context *ctx);
 uint64_t hec_context_key_moduli(const hec_context *ctx); /* K */
